@@ -1,0 +1,148 @@
+"""ORACLE (test infrastructure only) -- CPU restatement of the TopK / RandK baselines.
+
+Restates comm_hooks/sparse_hook.py (fixed ratio) and comm_hooks/sparse_hook_c4.py
+(gradual ratio 0.8 -> target, the copy the reference registry actually uses,
+comm_hooks/utils.py:94) with ``sparse_type='tensor'`` -- the only working type
+(row/column return 2-tuples where 3 are unpacked, sparse_hook.py:54, :75, :96).
+
+  sparsify   TopK: topk(|x|, k, sorted=False) -> int32 idx; RandK: randperm(numel)[:k]
+             after the shared reseed (sparse_hook.py:16-34, :230-235)
+  pack       values/indices per tensor; EF14 zero / EF21 keep-only (:92-110)
+  decode     RandK: all-reduce, /ws, scatter (=) (:270-278)
+             TopK : all-gather, scatter-add in rank order, /ws (:279-292)
+  EF         pre-apply (:202-226) and residual persistence (:257-267), EF21 gE (:295-297)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+
+def numel_of(shape) -> int:
+    n = 1
+    for d in shape:
+        n *= int(d)
+    return n
+
+
+def cal_k(numel: int, ratio: float) -> int:  # sparse_hook.py:77-78
+    return max(1, int(numel * ratio))
+
+
+def gradual_ratio(base: float, it: int, start: int, warmup_iters: int = 100,
+                  started: bool = True, gradual: bool = True) -> float:
+    """sparse_hook_c4.py:175-189 (note warmup span = start + warmup_iters, :151)."""
+    if not gradual or not started:
+        return base
+    span = start + warmup_iters
+    prog = it - start
+    if prog < span:
+        cur = 0.8 - (0.8 - base) * (prog / span)
+        return max(cur, base)
+    return base
+
+
+def topk_indices(x: torch.Tensor, k: int) -> torch.Tensor:
+    _, idx = torch.topk(x.abs(), k, sorted=False)
+    return idx.to(torch.int32)
+
+
+def randk_indices(numel: int, k: int, g: torch.Generator) -> torch.Tensor:
+    return torch.randperm(numel, generator=g)[:k].to(torch.int32)
+
+
+def encode(G, E, ef):
+    X = G.clone()
+    if E is not None:
+        if ef == "ef14":
+            X.add_(E, alpha=1.0)
+        elif ef == "ef21":
+            X.add_(E, alpha=-1.0)
+    return X
+
+
+def pack(X: torch.Tensor, shapes, ratio: float, ef: str, random: bool, seed: Optional[int]):
+    """Returns (values, indices int32, k_list, bits_sum); mutates X per EF mode."""
+    g = torch.Generator().manual_seed(int(seed)) if random else None
+    vals, idxs, ks, bits = [], [], [], 0
+    off = 0
+    for s in shapes:
+        n = numel_of(s)
+        v = X[off:off + n]
+        k = cal_k(n, ratio)
+        idx = randk_indices(n, k, g) if random else topk_indices(v, k)
+        val = v[idx.long()].clone()
+        vals.append(val)
+        idxs.append(idx)
+        ks.append(k)
+        bits += val.numel() * torch.finfo(X.dtype).bits + (0 if random else idx.numel() * 32)
+        if ef == "ef14":
+            v[idx.long()] = 0
+        elif ef == "ef21":
+            v.zero_()
+            v[idx.long()] = val
+        off += n
+    return torch.cat(vals), torch.cat(idxs), ks, bits
+
+
+def decode_randk(vsum: torch.Tensor, idx: torch.Tensor, shapes, ks, ws: int, numel: int):
+    vals = vsum.clone()
+    vals.div_(ws)
+    out = torch.zeros(numel, dtype=vsum.dtype)
+    off = koff = 0
+    for s, k in zip(shapes, ks):
+        n = numel_of(s)
+        out[off:off + n][idx[koff:koff + k].long()] = vals[koff:koff + k]
+        off += n
+        koff += k
+    return out
+
+
+def decode_topk(all_vals: List[torch.Tensor], all_idx: List[torch.Tensor], shapes, ks, ws: int,
+                numel: int):
+    out = torch.zeros(numel, dtype=all_vals[0].dtype)
+    for vals, idx in zip(all_vals, all_idx):  # rank order
+        off = koff = 0
+        for s, k in zip(shapes, ks):
+            n = numel_of(s)
+            view = out[off:off + n]
+            view[idx[koff:koff + k].long()] += vals[koff:koff + k]
+            off += n
+            koff += k
+    out.div_(ws)
+    return out
+
+
+def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed: Optional[int]):
+    """One steady-state compressed call on len(Gs) ranks in one process."""
+    ws = len(Gs)
+    Xs, packs = [], []
+    for G, E in zip(Gs, Es):
+        X = encode(G, E, ef)
+        packs.append(pack(X, shapes, ratio, ef, random, seed))
+        Xs.append(X)
+    ks = packs[0][2]
+    numel = Gs[0].numel()
+    if random:
+        vsum = packs[0][0].clone()
+        for q in range(1, ws):
+            vsum = vsum + packs[q][0]
+        out = decode_randk(vsum, packs[0][1], shapes, ks, ws, numel)
+    else:
+        out = decode_topk([p[0] for p in packs], [p[1] for p in packs], shapes, ks, ws, numel)
+    E_new = []
+    for X, E in zip(Xs, Es):
+        if ef == "ef14":
+            E_new.append(X.clone())
+        elif ef == "ef21":
+            E_new.append(E + X)  # error_decay = 1.0 (sparse_hook.py:145)
+        else:
+            E_new.append(None)
+    gE_new = None
+    if ef == "ef21":
+        gE_new = gE + out
+        out = gE_new.clone()
+    return dict(X=Xs, values=[p[0] for p in packs], indices=[p[1] for p in packs], ks=ks,
+                bits=packs[0][3], out=out, E_new=E_new, gE_new=gE_new)

@@ -1,0 +1,184 @@
+"""Pin the CPU oracle against golden vectors produced by the reference hooks.
+
+Every fixture under tests/golden/ was produced by running the reference
+(Aris-ma/AllreduceTopK comm_hooks/*) on a gloo group; here the oracle replays
+the same inputs and must reproduce every captured intermediate and output
+bit for bit (ws=2 sums are two-operand and therefore order-free).
+"""
+import json
+import os
+
+import pytest
+import torch
+
+from golden_io import GOLDEN, Golden, case_names
+from oracle import arctopk as A
+from oracle import sparse as S
+
+
+def _eq(a, b, what):
+    a = torch.as_tensor(a)
+    b = torch.as_tensor(b)
+    assert a.shape == b.shape, f"{what}: shape {tuple(a.shape)} vs {tuple(b.shape)}"
+    assert torch.equal(a, b), f"{what}: max |diff| {(a.double() - b.double()).abs().max().item()}"
+
+
+@pytest.mark.parametrize("name", case_names("arc_"))
+def test_arc_oracle_matches_reference(name):
+    g = Golden(name)
+    m = g.meta
+    ws, shapes, ef = m["ws"], [tuple(s) for s in m["shapes"]], m["ef"]
+    st = A.OracleState(r=m["r"], compress_ratio=m["ratio"], start_compress_iter=m["start"],
+                       use_error_feedback=ef, seed=m["seed"])
+    Es = [None] * ws
+    gE = None
+    bits = 0
+    it_count = 0
+    for it in range(m["iters"]):
+        Gs = [g.t(q, it, "G") for q in range(ws)]
+        if it_count < m["start"]:  # warm-up: dense mean (default_hooks._allreduce_fut)
+            acc = Gs[0] / ws
+            for q in range(1, ws):
+                acc = acc + Gs[q] / ws
+            for q in range(ws):
+                _eq(acc, g.t(q, it, "out"), f"{name} it{it} warm-up out")
+            bits += 2 * (ws - 1) * Gs[0].numel() * 32
+        elif ef == "ef21" and Es[0] is None:  # EF21 init (ref :236-250)
+            Es = [G.clone() for G in Gs]
+            acc = Gs[0].clone()
+            for q in range(1, ws):
+                acc = acc + Gs[q]
+            acc.div_(ws)
+            gE = acc.clone()
+            for q in range(ws):
+                _eq(acc, g.t(q, it, "out"), f"{name} it{it} ef21-init out")
+                _eq(gE, g.t(q, it, "gE"), f"{name} it{it} ef21-init gE")
+                _eq(Es[q], g.t(q, it, "E"), f"{name} it{it} ef21-init E")
+            bits += Gs[0].numel() * 32
+        else:
+            if ef == "ef14" and Es[0] is None:
+                Es = [None] * ws
+                first = True
+            else:
+                first = False
+            seed = st.next_seed()
+            for q in range(ws):
+                assert int(g.np(q, it, "seed")[0]) == seed
+            res = A.simulate_step(Gs, Es, gE, shapes, m["ratio"], m["r"], ef, seed)
+            segs = res["segs"]
+            vi = 0
+            for j, s in enumerate(segs):
+                if s.kind == A.SKETCH:
+                    _eq(res["V"][j], g.t(0, it, f"V{vi}"), f"{name} it{it} V{vi}")
+                    vi += 1
+                _eq(res["norms"][j], g.t(0, it, f"topk{j}_in"), f"{name} it{it} norms seg{j}")
+                assert int(g.np(0, it, f"topk{j}_k")) == s.k_rows
+                _eq(res["rows"][j], g.t(0, it, f"topk{j}_idx"), f"{name} it{it} rows seg{j}")
+            for q in range(ws):
+                _eq(res["out"], g.t(q, it, "out"), f"{name} it{it} r{q} out")
+                if ef in ("ef14", "ef21"):
+                    _eq(res["E_new"][q], g.t(q, it, "E"), f"{name} it{it} r{q} E")
+                if ef == "ef21":
+                    _eq(res["gE_new"], g.t(q, it, "gE"), f"{name} it{it} r{q} gE")
+            if ef in ("ef14", "ef21"):
+                Es = res["E_new"]
+            if ef == "ef21":
+                gE = res["gE_new"]
+            bits += 2 * (ws - 1) * A.bits_per_call(segs, m["r"], 32)
+            del first
+        it_count += 1
+        for q in range(ws):
+            assert int(g.np(q, it, "bits")) == bits, f"{name} it{it} comm bits"
+
+
+@pytest.mark.parametrize("name", case_names("topk_") + case_names("randk_"))
+def test_sparse_oracle_matches_reference(name):
+    g = Golden(name)
+    m = g.meta
+    ws, shapes, ef, random = m["ws"], [tuple(s) for s in m["shapes"]], m["ef"], m["random"]
+    gradual = m["hook"] == "sparse_c4"
+    rng = torch.Generator().manual_seed(m["seed"])
+    Es, gE, bits = [None] * ws, None, 0
+    started = False
+    for it in range(m["iters"]):
+        Gs = [g.t(q, it, "G") for q in range(ws)]
+        if it < m["start"]:
+            acc = Gs[0] / ws
+            for q in range(1, ws):
+                acc = acc + Gs[q] / ws
+            for q in range(ws):
+                _eq(acc, g.t(q, it, "out"), f"{name} it{it} warm-up out")
+            bits += 2 * (ws - 1) * Gs[0].numel() * 32
+            continue
+        started = True
+        ratio = (S.gradual_ratio(m["ratio"], it, m["start"], started=started) if gradual
+                 else m["ratio"])
+        if ef == "ef21" and Es[0] is None:
+            Es = [G.clone() for G in Gs]
+            acc = Gs[0].clone()
+            for q in range(1, ws):
+                acc = acc + Gs[q]
+            acc.div_(ws)
+            gE = acc.clone()
+            for q in range(ws):
+                _eq(acc, g.t(q, it, "out"), f"{name} it{it} ef21-init out")
+            continue  # sparse hook does not count the EF21 init bits
+        seed = None
+        if random:
+            seed = int(torch.randint(0, 1_000_000_000, (1,), generator=rng).item())
+            assert int(g.np(0, it, "seed")[0]) == seed
+        res = S.simulate_step(Gs, Es, gE, shapes, ratio, ef, random, seed)
+        if random:
+            off = 0
+            for j, s in enumerate(shapes):
+                k = res["ks"][j]
+                perm = g.t(0, it, f"perm{j}")[:k].to(torch.int32)
+                _eq(res["indices"][0][off:off + k], perm, f"{name} it{it} randperm seg{j}")
+                off += k
+        else:
+            off = 0
+            for j, s in enumerate(shapes):
+                k = res["ks"][j]
+                assert int(g.np(0, it, f"topk{j}_k")) == k
+                for q in range(ws):
+                    _eq(res["indices"][q][off:off + k], g.t(q, it, f"topk{j}_idx").to(torch.int32),
+                        f"{name} it{it} r{q} topk idx seg{j}")
+                off += k
+        for q in range(ws):
+            _eq(res["out"], g.t(q, it, "out"), f"{name} it{it} r{q} out")
+            if ef in ("ef14", "ef21"):
+                _eq(res["E_new"][q], g.t(q, it, "E"), f"{name} it{it} r{q} E")
+        if ef in ("ef14", "ef21"):
+            Es = res["E_new"]
+        if ef == "ef21":
+            gE = res["gE_new"]
+        bits += (2 * (ws - 1) if random else (ws - 1) * ws) * res["bits"]
+        for q in range(ws):
+            assert int(g.np(q, it, "bits")) == bits, f"{name} it{it} comm bits"
+        if gradual:
+            assert abs(float(g.np(0, it, "ratio_now")) -
+                       S.gradual_ratio(m["ratio"], it + 1, m["start"])) < 1e-15
+
+
+def test_nd_indivisible_raises():
+    with open(os.path.join(GOLDEN, "nd_indivisible_error.json")) as f:
+        meta = json.load(f)
+    with pytest.raises(RuntimeError):
+        A.geometry(meta["shape"])
+    assert meta["raises"] == "RuntimeError"
+
+
+def test_projection_stream_equals_global_reseed():
+    """A private generator seeded with `seed` draws the V the reference draws after
+    torch.manual_seed(seed) (ref :254-255, :49, :79) -- including sizes < 16
+    (m=2 -> V[2,4]) that take torch's serial normal path."""
+    segs = A.segments([(40, 16), (16, 8, 1, 1), (4, 3, 3, 3), (10,), (96, 40)], 0.2)
+    state = torch.random.get_rng_state()
+    try:
+        torch.manual_seed(424242)
+        ref = [torch.randn(s.m, 4) if s.kind == A.SKETCH else None for s in segs]
+    finally:
+        torch.random.set_rng_state(state)
+    mine = A.draw_projections(424242, segs, 4)
+    for a, b in zip(ref, mine):
+        assert (a is None and b is None) or torch.equal(a, b)
