@@ -1,0 +1,112 @@
+"""ctypes binding of libarctopk.so (declared in include/arctopk.h).
+
+The shipped hooks run only through this library: if it is missing or cannot
+be loaded, ``lib()`` raises -- there is no CPU or eager-torch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ARCTOPK_LIB", os.path.join(PKG, "lib", "libarctopk.so"))
+
+EF_NONE, EF14, EF21 = 0, 1, 2
+EF_CODE = {"noef": EF_NONE, "ef14": EF14, "ef21": EF21}
+SEG_RAW, SEG_SKETCH = 0, 1
+F32 = 0
+
+STATUS = {1001: "invalid argument", 1002: "ND tensor numel not divisible by 2*t^2",
+          1003: "unsupported dtype", 1004: "empty tensor"}
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [("numel", c_int64), ("sketch_len", c_int64), ("v_len", c_int64),
+                ("packed_len", c_int64), ("sel_rows", c_int64), ("rows_total", c_int64),
+                ("nseg", c_int32), ("r", c_int32)]
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [("offset", c_int64), ("n", c_int64), ("m", c_int64), ("k_rows", c_int64),
+                ("sketch_off", c_int64), ("v_off", c_int64), ("packed_off", c_int64),
+                ("row_off", c_int64), ("sel_off", c_int64), ("kind", c_int32), ("pad", c_int32)]
+
+
+_SIGS = {
+    "arctopk_plan_create": (c_int32, [POINTER(c_int64), POINTER(c_int32), c_int32, c_int32, c_double,
+                                      c_int32, c_int32, POINTER(c_void_p)]),
+    "arctopk_plan_destroy": (c_int32, [c_void_p]),
+    "arctopk_plan_describe": (c_int32, [POINTER(c_int64), POINTER(c_int32), c_int32, c_int32, c_double,
+                                        c_void_p, POINTER(PlanInfo)]),
+    "arctopk_plan_query": (c_int32, [c_void_p, POINTER(PlanInfo)]),
+    "arctopk_plan_segment": (c_int32, [c_void_p, c_int32, POINTER(Segment)]),
+    "arctopk_encode": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                 c_void_p]),
+    "arctopk_select": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "arctopk_row_energy": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "arctopk_decode": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                 c_void_p]),
+    "arctopk_sparse_workspace_bytes": (c_int64, []),
+    "arctopk_topk_select": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
+                                      POINTER(c_int64), POINTER(c_int64), c_void_p, c_void_p, c_void_p,
+                                      c_void_p]),
+    "arctopk_randk_indices": (c_int32, [c_int32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64),
+                                        c_uint64, c_void_p, c_void_p]),
+    "arctopk_sparse_gather": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
+                                        POINTER(c_int64), c_void_p, c_void_p, c_void_p]),
+    "arctopk_sparse_residual": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
+                                          POINTER(c_int64), c_void_p, c_void_p, c_int32, c_void_p]),
+    "arctopk_sparse_decode": (c_int32, [c_void_p, c_int64, c_int32, POINTER(c_int64), POINTER(c_int64),
+                                        POINTER(c_int64), c_int64, c_void_p, c_void_p, c_int32, c_int32,
+                                        c_int32, c_void_p, c_void_p]),
+    "arctopk_ef_apply": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
+    "arctopk_version": (c_char_p, []),
+}
+
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeLibraryMissing(ImportError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load libarctopk.so once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"libarctopk.so not found at {LIB_PATH}: build it with "
+                "`python -m allreducetopk_amd.build` (hipcc, gfx950). There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status:
+        msg = STATUS.get(int(status), f"hip error {int(status)}")
+        raise RuntimeError(f"{what} failed: {msg} (status {int(status)})")
+
+
+def i64_array(values):
+    arr = (c_int64 * len(values))(*[int(v) for v in values])
+    return arr
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,339 @@
+"""ARC-TopK DDP comm hook on MI355X -- drop-in for the reference's
+comm_hooks/group_topk_hook_no_reshape.py (``GroupTopKState`` :143-171,
+``cal_k`` :173-187, ``group_topk_hook`` :190-297).
+
+Per bucket call the codec runs as four HIP kernels of libarctopk.so with two
+RCCL all-reduces in between, all enqueued on the caller's current stream with
+no host synchronisation:
+
+    encode  (EF pre-apply + rank-r sketch of every tensor, one HBM pass)
+    all_reduce(sketch)            one call per bucket (the reference: one per tensor)
+    select  (mean sketch -> row energy -> exact top-k rows)
+    pack    (gather selected rows, EF14/EF21 residual update)
+    all_reduce(packed values)     index-free: every rank selected the same rows
+    decode  (mean of the selected rows into the bucket, EF21 global residual)
+
+Semantics kept from the reference: same state attributes (``iter``,
+``error_dict``, ``global_error_dict``, ``rng``, ``comm_bits_this_round`` ...),
+same warm-up and EF21-init paths, the same seed draw and global reseed, the
+same projections V (torch CPU generator), the same k per tensor, the same
+output bucket and residuals.  Selected rows are identical to the reference's
+except where two rows' sketch energies are equal within fp32 rounding of the
+sketch (the GPU sums G.V in a different order than CPU sgemm); exact ties at
+the k-th energy are resolved lowest-row-first.  The hook returns an already
+completed Future holding the bucket, as the reference does (:294-297).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, List, Tuple
+
+import torch
+import torch.distributed as dist
+
+from allreducetopk_amd import _native as N
+from allreducetopk_amd.comm_hooks import default_hooks
+from allreducetopk_amd.comm_hooks.projections import ProjectionSource
+from allreducetopk_amd.comm_hooks.utils import HookState, dtype_bits, tensor_bits
+
+logger = logging.getLogger(__name__)
+
+__all__ = ["GroupTopKState", "cal_k", "group_topk_hook", "BucketPlan"]
+
+
+def _geometry(shape) -> Tuple[int, int, int]:
+    """(kind, n, m) as the reference reads a gradient (:19, :44-46, :73-76)."""
+    shape = tuple(int(s) for s in shape)
+    d = 1
+    for s in shape:
+        d *= s
+    if len(shape) == 1:
+        return N.SEG_RAW, d, 1
+    if len(shape) == 2:
+        return N.SEG_SKETCH, shape[0], shape[1]
+    t = shape[-1]
+    m = 2 * t * t
+    return N.SEG_SKETCH, d // m if m else 0, m
+
+
+class BucketPlan:
+    """Native plan + persistent device buffers of one bucket layout."""
+
+    def __init__(self, shapes: List[Tuple[int, ...]], r: int, ratio: float, dtype, device):
+        if dtype != torch.float32:
+            raise TypeError(f"ARC-TopK HIP codec supports float32 buckets, got {dtype}")
+        L = N.lib()
+        dims: List[int] = []
+        nd: List[int] = []
+        for s in shapes:
+            dims.extend(int(d) for d in s)
+            nd.append(len(s))
+        self.shapes = shapes
+        self.r = r
+        self.ratio = ratio
+        self.device = torch.device(device)
+        handle = N.c_void_p()
+        st = L.arctopk_plan_create((N.c_int64 * max(1, len(dims)))(*dims), (N.c_int32 * len(nd))(*nd),
+                                   len(nd), r, float(ratio), N.F32, self.device.index or 0,
+                                   N.ctypes.byref(handle))
+        N.check(st, f"arctopk_plan_create(shapes={shapes}, r={r}, ratio={ratio})")
+        self.handle = handle
+        info = N.PlanInfo()
+        N.check(L.arctopk_plan_query(handle, N.ctypes.byref(info)), "arctopk_plan_query")
+        self.info = info
+        self.segments = []
+        for i in range(info.nseg):
+            seg = N.Segment()
+            N.check(L.arctopk_plan_segment(handle, i, N.ctypes.byref(seg)), "arctopk_plan_segment")
+            self.segments.append(seg)
+        self.ms = tuple(int(s.m) for s in self.segments if s.kind == N.SEG_SKETCH)
+        dev = self.device
+        self.sketch = torch.empty(max(1, info.sketch_len), dtype=torch.float32, device=dev)
+        self.packed = torch.empty(max(1, info.packed_len), dtype=torch.float32, device=dev)
+        self.rowlist = torch.empty(max(1, info.sel_rows), dtype=torch.int32, device=dev)
+        self.slotmap = torch.empty(max(1, info.rows_total), dtype=torch.int32, device=dev)
+        self.V = torch.empty(max(1, info.v_len), dtype=torch.float32, device=dev)
+        bits = dtype_bits(dtype)
+        # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
+        self.bits_sum = sum(((s.n if s.kind == N.SEG_RAW else s.n * r) + s.k_rows * s.m) * bits
+                            for s in self.segments)
+
+    @property
+    def sketch_view(self):
+        return self.sketch[:self.info.sketch_len]
+
+    @property
+    def packed_view(self):
+        return self.packed[:self.info.packed_len]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and N._lib is not None:
+            try:
+                N._lib.arctopk_plan_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self.handle = None
+
+    # ---- the four codec phases (each enqueues on `stream`) --------------------
+    def encode(self, grad, err, ef: int, err_in: bool, V, stream: int):
+        N.check(N.lib().arctopk_encode(self.handle, grad.data_ptr(), N.ptr(err), ef, int(err_in),
+                                       V.data_ptr(), self.sketch.data_ptr(), stream),
+                "arctopk_encode")
+
+    def select(self, world_size: int, stream: int):
+        N.check(N.lib().arctopk_select(self.handle, self.sketch.data_ptr(), world_size,
+                                       self.rowlist.data_ptr(), self.slotmap.data_ptr(), stream),
+                "arctopk_select")
+
+    def pack(self, grad, err, ef: int, stream: int):
+        N.check(N.lib().arctopk_pack(self.handle, N.ptr(grad), N.ptr(err), ef,
+                                     self.rowlist.data_ptr(), self.packed.data_ptr(), stream),
+                "arctopk_pack")
+
+    def decode(self, world_size: int, ef: int, gerr, out, stream: int):
+        N.check(N.lib().arctopk_decode(self.handle, self.packed.data_ptr(), self.slotmap.data_ptr(),
+                                       world_size, ef, N.ptr(gerr), out.data_ptr(), stream),
+                "arctopk_decode")
+
+    def row_energy(self, world_size: int, out, stream: int):
+        N.check(N.lib().arctopk_row_energy(self.handle, self.sketch.data_ptr(), world_size,
+                                           out.data_ptr(), stream), "arctopk_row_energy")
+
+
+class GroupTopKState(HookState):
+    """State of the ARC-TopK hook (reference :143-171; same constructor)."""
+
+    def __init__(self, process_group: dist.ProcessGroup, r: int = 4, compress_ratio: float = 0.08,
+                 start_compress_iter: int = 2, use_error_feedback="noef", seed=0, error_decay=1.0):
+        super().__init__(process_group)
+        self.r = r
+        self.compress_ratio = compress_ratio
+        self.iter = 0
+        self.start_compress_iter = start_compress_iter
+        self.seed = seed
+        self.use_error_feedback = use_error_feedback
+        self.error_dict: Dict[int, torch.Tensor] = {}
+        self.global_error_dict: Dict[int, torch.Tensor] = {}
+        self.error_decay = error_decay
+        self.rng = torch.Generator()
+        self.rng.manual_seed(seed)
+        # MI355X codec state (not in the reference)
+        self._plans: Dict[int, Tuple[tuple, BucketPlan]] = {}
+        self._proj = ProjectionSource(r)
+        self._order: List[int] = []  # bucket indices in call order within one backward
+        # optional phase timing: a list that receives one dict of HIP events for every
+        # `phase_event_every`-th call (HIP events on the hook's stream)
+        self.phase_events = None
+        self.phase_event_every = 1
+        self._ev_calls = 0
+
+    def _plan_for(self, bucket) -> BucketPlan:
+        buf = bucket.buffer()
+        grads = bucket.gradients()
+        shapes = [tuple(g.shape) for g in grads]
+        key = (tuple(shapes), buf.dtype, buf.device, self.r, float(self.compress_ratio))
+        hit = self._plans.get(bucket.index())
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        _check_bucket_layout(buf, grads)
+        plan = BucketPlan(shapes, self.r, self.compress_ratio, buf.dtype, buf.device)
+        self._plans[bucket.index()] = (key, plan)
+        return plan
+
+    def _upcoming_ms(self, bucket) -> List[Tuple[int, ...]]:
+        """Column lists of the next calls, assuming the bucket order repeats."""
+        b = bucket.index()
+        if b not in self._order:
+            self._order.append(b)
+        order = self._order
+        pos = order.index(b)
+        out = []
+        for i in range(1, self._proj.depth + 1):
+            nb = order[(pos + i) % len(order)]
+            ent = self._plans.get(nb)
+            if ent is None:
+                break
+            out.append(ent[1].ms)
+        return out
+
+
+_RESEED_FAST = None
+
+
+def _reseed_global(seed: int) -> None:
+    """``torch.manual_seed(seed)`` (ref :255) without its per-call Python overhead.
+
+    torch.manual_seed reseeds the CPU generator and every CUDA device's default
+    generator (plus MPS/XPU/custom devices, absent on ROCm builds).  When only CPU and
+    CUDA exist this does exactly that; otherwise it defers to torch.manual_seed.
+    """
+    global _RESEED_FAST
+    if _RESEED_FAST is None:
+        fast = (torch.cuda.is_available() and not torch.backends.mps.is_available()
+                and not (hasattr(torch, "xpu") and torch.xpu.is_available())
+                and torch._C._get_privateuse1_backend_name() == "privateuseone")
+        _RESEED_FAST = [torch.cuda.default_generators[i] for i in range(torch.cuda.device_count())] \
+            if fast else False
+    if _RESEED_FAST is False or not torch.cuda.is_initialized():
+        torch.manual_seed(seed)
+        return
+    for g in _RESEED_FAST:
+        g.manual_seed(seed)
+    torch.default_generator.manual_seed(seed)
+
+
+def cal_k(state, tensor) -> int:
+    """Selected elements of one tensor (reference :173-187)."""
+    kind, n, m = _geometry(tensor.shape)
+    return max(1, int(n * state.compress_ratio)) * m
+
+
+def _check_bucket_layout(buf: torch.Tensor, grads) -> None:
+    if not buf.is_cuda:
+        raise RuntimeError("ARC-TopK HIP codec needs the bucket on a GPU (got CPU tensor); "
+                           "the CPU reference algorithm lives in oracle/ (tests only)")
+    if buf.dim() != 1 or not buf.is_contiguous():
+        raise RuntimeError("bucket buffer must be a contiguous 1-D tensor")
+    esz = buf.element_size()
+    off = 0
+    for g in grads:
+        if not g.is_contiguous():
+            raise RuntimeError("bucket gradient views must be contiguous (view(-1) in the reference)")
+        if (g.data_ptr() - buf.data_ptr()) // esz != off:
+            raise RuntimeError("bucket gradient views must tile the buffer in order")
+        off += g.numel()
+    if off != buf.numel():
+        raise RuntimeError("bucket gradient views do not cover the buffer")
+
+
+def group_topk_hook(state: GroupTopKState, bucket) -> torch.futures.Future:
+    state.maybe_accumulate_momentum_on_bucket(bucket)
+    group = state.process_group if state.process_group is not None else dist.group.WORLD
+    world_size = group.size()
+    input_tensor = bucket.buffer()
+
+    # warm-up: dense all-reduce for the first start_compress_iter iterations (:213-215)
+    if state.iter < state.start_compress_iter:
+        state.maybe_increase_iter(bucket)
+        return default_hooks._allreduce_fut(group, input_tensor, state)
+
+    b = bucket.index()
+    total = input_tensor.shape[0]
+    ef_name = state.use_error_feedback
+    ef = N.EF_CODE.get(ef_name)
+    if ef is None:
+        raise ValueError(f"use_error_feedback must be noef/ef14/ef21, got {ef_name!r}")
+    err = gerr = None
+    err_in = True
+    if ef == N.EF14:
+        if b not in state.error_dict:
+            logger.info("A zero tensor of length %s that represents local error is created.", total)
+            state.error_dict[b] = torch.zeros(total, device=input_tensor.device,
+                                              dtype=input_tensor.dtype)
+            err_in = False  # first call: the residual is not added (:228-230)
+        err = state.error_dict[b]
+    elif ef == N.EF21:
+        if b not in state.error_dict:  # E_0 = grad; all-reduce grad; gE_0 = mean (:236-250)
+            logger.info("A tensor of length %s that represents local/global error is created.", total)
+            state.error_dict[b] = torch.clone(input_tensor).detach()
+            state.comm_bits_this_round += tensor_bits(input_tensor)
+            dist.all_reduce(input_tensor, group=group, async_op=False)
+            input_tensor.div_(world_size)
+            state.global_error_dict[b] = torch.clone(input_tensor).detach()
+            state.maybe_increase_iter(bucket)
+            fut = torch.futures.Future()
+            fut.set_result(input_tensor)
+            return fut
+        err = state.error_dict[b]
+        gerr = state.global_error_dict[b]
+    if err is not None and err.numel() != total:
+        raise RuntimeError(f"bucket {b} changed size ({err.numel()} -> {total}) after its "
+                           "residual was created")
+
+    # per-call projection seed, and the reference's global reseed side effect (:254-255)
+    seed = state._proj.consume_seed(state.rng)
+    _reseed_global(seed)
+
+    plan = state._plan_for(bucket)
+    stream = torch.cuda.current_stream(input_tensor.device)
+    sid = stream.cuda_stream
+    host_v = state._proj.get(seed, plan.ms, input_tensor.dtype)
+    if plan.info.v_len:
+        plan.V[:plan.info.v_len].copy_(host_v[:plan.info.v_len], non_blocking=True)
+    state._proj.prefetch(state._upcoming_ms(bucket), input_tensor.dtype)
+
+    evs = None
+    if state.phase_events is not None:
+        state._ev_calls += 1
+        if (state._ev_calls - 1) % state.phase_event_every == 0:
+            evs = {}
+            state.phase_events.append(evs)
+
+    def mark(name):
+        if evs is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            evs[name] = e
+
+    mark("start")
+    plan.encode(input_tensor, err, ef, err_in, plan.V, sid)
+    mark("encode")
+    if world_size > 1:  # a SUM over one rank is the identity: nothing to exchange
+        dist.all_reduce(plan.sketch_view, group=group, async_op=False)
+    mark("sketch_allreduce")
+    plan.select(world_size, sid)
+    mark("select")
+    plan.pack(input_tensor, err, ef, sid)
+    mark("pack")
+    state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum
+    if world_size > 1:
+        dist.all_reduce(plan.packed_view, group=group, async_op=False)
+    mark("packed_allreduce")
+    plan.decode(world_size, ef, gerr, input_tensor, sid)
+    mark("decode")
+
+    state.maybe_increase_iter(bucket)
+    fut = torch.futures.Future()
+    fut.set_result(input_tensor)
+    return fut

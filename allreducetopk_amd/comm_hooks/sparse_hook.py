@@ -1,0 +1,232 @@
+"""TopK / RandK DDP comm hooks on MI355X -- drop-in for the reference's
+comm_hooks/sparse_hook.py (``SparseState`` :127-160, ``cal_k`` :77-78,
+``sparse_hook_sync`` :163-304).
+
+Per bucket call (all on the caller's stream, no host synchronisation):
+
+    ef_apply        (EF14: x += E, E = x | EF21: x -= E), one fused pass
+    TopK : topk_select  exact element top-k of |x| per tensor (radix select),
+                        ascending int32 indices + gathered values
+    RandK: indices      torch.randperm(numel, device)[:k] after the shared reseed
+                        (parity mode: the reference's own draw), or a keyed device
+                        permutation (index_source="hash", perf mode); then gather
+    residual        EF14: E[idx] = 0 | EF21: E[idx] += values
+    RandK: all_reduce(values)              -> decode: zero + scatter(values / ws)
+    TopK : all_gather(values), all_gather(indices)
+                                           -> decode: zero + rank-ordered scatter-add, / ws
+    EF21: gE += out; out = gE (fused into decode)
+
+Only ``sparse_type="tensor"`` works in the reference (row/column unpack 2 values
+where 3 are expected, :54, :75, :96); the same types raise here.
+Ties at the k-th |x| resolve lowest-index first.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, List
+
+import torch
+import torch.distributed as dist
+
+from allreducetopk_amd import _native as N
+from allreducetopk_amd.comm_hooks import default_hooks
+from allreducetopk_amd.comm_hooks.utils import (HookState, _get_allgather_out_list, dtype_bits,
+                                                tensor_bits)
+
+logger = logging.getLogger(__name__)
+
+__all__ = ["SparseState", "sparse_hook_sync", "cal_k"]
+
+
+def cal_k(tensor, compress_ratio):
+    """k of a tensor (ref sparse_hook.py:77-78)."""
+    return max(1, int(tensor.numel() * compress_ratio))
+
+
+class SparseState(HookState):
+    """State of the TopK/RandK hook (reference sparse_hook.py:127-160)."""
+
+    def __init__(self, process_group: dist.ProcessGroup, compress_ratio: float = 0.01,
+                 start_compress_iter: int = 2, sparse_type: str = "row", random: bool = False,
+                 use_error_feedback: str = "noef", random_seed: int = 0,
+                 index_source: str = "torch"):
+        super().__init__(process_group)
+        self.total_bit_before_compression = 0
+        self.total_bit_after_compression = 0
+        self.compress_ratio = compress_ratio
+        self.iter = 0
+        self.start_compress_iter = start_compress_iter
+        self.error_decay = 1.0
+        self.large_batch_init = False
+        self.sparse_type = sparse_type
+        self.compressor_name = f"{sparse_type}-wise sparsification"
+        self.random = random
+        self.rng = torch.Generator()
+        self.rng.manual_seed(random_seed)
+        self.use_error_feedback = use_error_feedback
+        self.error_dict: Dict[int, torch.Tensor] = {}
+        self.global_error_dict: Dict[int, torch.Tensor] = {}
+        self.random_seed = random_seed
+        if index_source not in ("torch", "hash"):
+            raise ValueError("index_source must be 'torch' or 'hash'")
+        self.index_source = index_source
+        self._workspace = None
+
+    # ratio of this call; the c4 variant overrides (gradual compression)
+    def _call_ratio(self) -> float:
+        return self.compress_ratio
+
+    def _on_compression_start(self):
+        pass
+
+
+def _workspace(state, device) -> torch.Tensor:
+    ws = state._workspace
+    if ws is None or ws.device != device:
+        nbytes = int(N.lib().arctopk_sparse_workspace_bytes())
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        state._workspace = ws
+    return ws
+
+
+def _sparse_hook_impl(state: SparseState, bucket) -> torch.futures.Future:
+    if state.use_error_feedback == "ef21" and state.large_batch_init:
+        raise NotImplementedError("large_batch_init EF21 (dead code in the reference, "
+                                  "sparse_hook.py:156) is not provided")
+    state.maybe_accumulate_momentum_on_bucket(bucket)
+    group = state.process_group if state.process_group is not None else dist.group.WORLD
+    world_size = group.size()
+    input_tensor = bucket.buffer()
+    tensors = bucket.gradients()
+
+    if state.iter < state.start_compress_iter:  # (:190-193)
+        state.maybe_increase_iter(bucket)
+        return default_hooks._allreduce_fut(group, input_tensor, state)
+
+    state._on_compression_start()
+    if state.sparse_type != "tensor":  # the reference crashes for row/column (:96)
+        raise ValueError(f"not enough values to unpack (sparse_type={state.sparse_type!r}: only "
+                         "'tensor' is functional in the reference)")
+    if not input_tensor.is_cuda or input_tensor.dtype != torch.float32:
+        raise RuntimeError("sparse HIP codec needs a float32 bucket on a GPU")
+    L = N.lib()
+    device = input_tensor.device
+    dtype = input_tensor.dtype
+    b = bucket.index()
+    total = input_tensor.shape[0]
+    stream = torch.cuda.current_stream(device).cuda_stream
+    ef = N.EF_CODE[state.use_error_feedback]
+
+    if ef == N.EF14:
+        err_in = b in state.error_dict
+        if not err_in:
+            logger.info("A zero tensor of length %s that represents local error is created.", total)
+            state.error_dict[b] = torch.zeros(total, device=device, dtype=dtype)
+        N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), state.error_dict[b].data_ptr(), total,
+                                   N.EF14, int(err_in), stream), "arctopk_ef_apply")
+    elif ef == N.EF21:
+        if b in state.error_dict:
+            N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), state.error_dict[b].data_ptr(),
+                                       total, N.EF21, 1, stream), "arctopk_ef_apply")
+        else:  # (:213-226)
+            logger.info("A tensor of length %s that represents local/global error is created.", total)
+            state.error_dict[b] = torch.clone(input_tensor).detach()
+            dist.all_reduce(input_tensor, group=group, async_op=False)
+            input_tensor.div_(world_size)
+            state.global_error_dict[b] = torch.clone(input_tensor).detach()
+            state.maybe_increase_iter(bucket)
+            fut = torch.futures.Future()
+            fut.set_result(input_tensor)
+            return fut
+
+    seed = None
+    if state.random:  # shared reseed so every rank draws the same indices (:230-235)
+        seed = torch.randint(0, 1_000_000_000, (1,), generator=state.rng).item()
+        torch.manual_seed(seed)
+
+    ratio = state._call_ratio()
+    numels = [t.numel() for t in tensors]
+    ks = [max(1, int(n * ratio)) for n in numels]
+    offsets: List[int] = []
+    off = 0
+    for t in tensors:
+        if (t.data_ptr() - input_tensor.data_ptr()) // input_tensor.element_size() != off:
+            raise RuntimeError("bucket gradient views must tile the buffer in order")
+        offsets.append(off)
+        off += t.numel()
+    k_off: List[int] = []
+    acc = 0
+    for k in ks:
+        k_off.append(acc)
+        acc += k
+    sum_k = acc
+    nt = len(tensors)
+    a_off, a_n, a_k, a_ko = (N.i64_array(offsets), N.i64_array(numels), N.i64_array(ks),
+                             N.i64_array(k_off))
+    values = torch.empty(sum_k, dtype=dtype, device=device)
+    indices = torch.empty(sum_k, dtype=torch.int32, device=device)
+    x = input_tensor.data_ptr()
+    if state.random:
+        if state.index_source == "torch":  # the reference's own draw (:20), per tensor in order
+            for t, k, ko in zip(tensors, ks, k_off):
+                indices[ko:ko + k].copy_(torch.randperm(t.numel(), device=device)[:k])
+        else:
+            N.check(L.arctopk_randk_indices(nt, a_n, a_k, a_ko, int(seed), indices.data_ptr(),
+                                            stream), "arctopk_randk_indices")
+        N.check(L.arctopk_sparse_gather(x, nt, a_off, a_k, a_ko, indices.data_ptr(),
+                                        values.data_ptr(), stream), "arctopk_sparse_gather")
+        bits_sum = sum_k * dtype_bits(dtype)
+    else:
+        ws_buf = _workspace(state, device)
+        N.check(L.arctopk_topk_select(x, nt, a_off, a_n, a_k, a_ko, indices.data_ptr(),
+                                      values.data_ptr(), ws_buf.data_ptr(), stream),
+                "arctopk_topk_select")
+        bits_sum = sum_k * (dtype_bits(dtype) + 32)
+
+    if ef != N.EF_NONE:  # residual persistence (:257-267)
+        N.check(L.arctopk_sparse_residual(state.error_dict[b].data_ptr(), nt, a_off, a_k, a_ko,
+                                          indices.data_ptr(), values.data_ptr(), ef, stream),
+                "arctopk_sparse_residual")
+    gerr = state.global_error_dict[b].data_ptr() if ef == N.EF21 else None
+
+    if state.random:
+        state.comm_bits_this_round += 2 * (world_size - 1) * bits_sum
+        if world_size > 1:
+            dist.all_reduce(values, group=group, async_op=False)
+        N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, indices.data_ptr(),
+                                        values.data_ptr(), 1, world_size, 0, gerr, stream),
+                "arctopk_sparse_decode")
+    else:
+        state.comm_bits_this_round += (world_size - 1) * world_size * bits_sum
+        if world_size > 1:
+            all_vals = torch.empty(world_size * sum_k, dtype=dtype, device=device)
+            all_idx = torch.empty(world_size * sum_k, dtype=torch.int32, device=device)
+            _all_gather_flat(all_vals, values, group, world_size)
+            _all_gather_flat(all_idx, indices, group, world_size)
+        else:  # gathering from one rank is the identity
+            all_vals, all_idx = values, indices
+        N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, all_idx.data_ptr(),
+                                        all_vals.data_ptr(), world_size, world_size, 1, gerr,
+                                        stream), "arctopk_sparse_decode")
+
+    state.maybe_increase_iter(bucket)
+    fut = torch.futures.Future()
+    fut.set_result(input_tensor)
+    return fut
+
+
+def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group, world_size: int) -> None:
+    try:
+        dist.all_gather_into_tensor(out, inp, group=group, async_op=False)
+    except (RuntimeError, NotImplementedError, AttributeError):  # backends without the flat form
+        parts = _get_allgather_out_list(inp, world_size)
+        dist.all_gather(parts, inp, group=group, async_op=False)
+        torch.cat(parts, out=out)
+
+
+def sparse_hook_sync(state: SparseState, bucket) -> torch.futures.Future:
+    return _sparse_hook_impl(state, bucket)
+
+
+# bits helpers kept for drivers that import them from here
+__all__ += ["tensor_bits", "dtype_bits"]

@@ -1,0 +1,899 @@
+// ARC-TopK per-bucket codec kernels for MI355X (gfx950, wave64).
+//
+//   K1 encode : EF pre-apply + rank-r sketch, one HBM pass over the bucket
+//   K2 select : mean sketch -> row energy -> exact top-k rows by LDS radix select
+//   K3 pack   : gather selected rows into the packed buffer + residual update
+//   K4 decode : one full-bucket write of the mean of the selected rows (+ EF21 gE)
+//
+// All kernels are HBM-streaming except K2 (latency-bound, a few KiB per segment).
+// Reference: comm_hooks/group_topk_hook_no_reshape.py (see include/arctopk.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.h"
+
+using namespace arctopk;
+
+namespace {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int EF, bool ERR_IN>
+__device__ __forceinline__ float4 ef_apply4(const float4* __restrict__ g4, float4* __restrict__ e4,
+                                            int64_t i) {
+    float4 x = g4[i];
+    if constexpr (EF == ARCTOPK_EF14) {
+        if constexpr (ERR_IN) {
+            const float4 e = e4[i];
+            x.x += e.x; x.y += e.y; x.z += e.z; x.w += e.w;
+        }
+    } else if constexpr (EF == ARCTOPK_EF21) {
+        const float4 e = e4[i];
+        x.x -= e.x; x.y -= e.y; x.z -= e.z; x.w -= e.w;
+    }
+    return x;
+}
+
+template <int EF, bool ERR_IN>
+__device__ __forceinline__ float ef_apply1(const float* __restrict__ g, const float* __restrict__ e,
+                                           int64_t i) {
+    float x = g[i];
+    if constexpr (EF == ARCTOPK_EF14) {
+        if constexpr (ERR_IN) x += e[i];
+    } else if constexpr (EF == ARCTOPK_EF21) {
+        x -= e[i];
+    }
+    return x;
+}
+
+// ---------------------------------------------------------------------------
+// K1 encode
+// ---------------------------------------------------------------------------
+// One block (256 threads = 4 waves) per tile.
+//  ENC_ROW_VEC    : wave per row, float4 columns, V^T staged in LDS ([R][m]) -- the
+//                   [2048,2048] fast path; every lane keeps 8 x 16 B loads in flight.
+//  ENC_ROW_SCALAR : same, scalar columns (misaligned rows / m % 4 != 0).
+//  ENC_TILE       : m < 64 (ND convs, m = 2*t^2): the tile's rows are loaded coalesced
+//                   into LDS, then one thread per row forms its R dot products.
+//  ENC_RAW        : 1-D tensors: the sketch is the (EF-applied) values themselves.
+template <int R, int EF, bool ERR_IN, bool VLDS>
+__global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
+                                                const EncTile* __restrict__ tiles,
+                                                const float* __restrict__ G, float* __restrict__ E,
+                                                const float* __restrict__ V,
+                                                float* __restrict__ sketch) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const EncTile t = tiles[blockIdx.x];
+    const SegDev s = segs[t.seg];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    constexpr bool WRITE_E = (EF == ARCTOPK_EF14);
+
+    if (t.mode == ENC_RAW) {
+        const int64_t base = s.offset + t.row0;
+        float* out = sketch + s.sketch_off + t.row0;
+        for (int64_t i = tid; i < t.nrows; i += 256) {
+            const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, i);
+            if constexpr (WRITE_E) E[base + i] = x;
+            out[i] = x;
+        }
+        return;
+    }
+
+    const int m = (int)s.m;
+    const float* __restrict__ Vs = V + s.v_off;  // [m][R]
+
+    if (t.mode == ENC_TILE) {
+        // LDS: tile [nrows*m] then V [m][R]
+        float* tile = lds;
+        float* vl = lds + kTileRows * m;
+        for (int i = tid; i < m * R; i += 256) vl[i] = Vs[i];
+        const int64_t base = s.offset + t.row0 * m;
+        const int cnt = (int)t.nrows * m;
+        for (int i = tid; i < cnt; i += 256) {
+            const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, i);
+            if constexpr (WRITE_E) E[base + i] = x;
+            tile[i] = x;
+        }
+        __syncthreads();
+        if (tid < t.nrows) {
+            float acc[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc[j] = 0.f;
+            const float* row = tile + tid * m;
+            for (int c = 0; c < m; ++c) {
+                const float x = row[c];
+#pragma unroll
+                for (int j = 0; j < R; ++j) acc[j] = fmaf(x, vl[c * R + j], acc[j]);
+            }
+            float* out = sketch + s.sketch_off + (t.row0 + tid) * R;
+#pragma unroll
+            for (int j = 0; j < R; ++j) out[j] = acc[j];
+        }
+        return;
+    }
+
+    // wave-per-row modes: stage V^T ([R][m]) in LDS when it fits (conflict-free writes:
+    // consecutive lanes take consecutive columns c of one j)
+    if constexpr (VLDS) {
+        if constexpr (R == 4) {
+            const float4* v4 = reinterpret_cast<const float4*>(Vs);
+            for (int c = tid; c < m; c += 256) {
+                const float4 v = v4[c];
+                lds[c] = v.x;
+                lds[m + c] = v.y;
+                lds[2 * m + c] = v.z;
+                lds[3 * m + c] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                for (int c = tid; c < m; c += 256) lds[j * m + c] = Vs[c * R + j];
+        }
+        __syncthreads();
+    }
+    const int64_t row_end = t.row0 + t.nrows;
+    if (t.mode == ENC_ROW_VEC) {
+        // Software-pipelined stream: a wave walks its rows in steps of 64*U float4
+        // (U per lane) with two register buffers: the loads of the next step are in
+        // flight while the current step forms its dot products, stores E and (at a
+        // row end) reduces.  V is read from LDS (VLDS) or L2, chosen at compile time so
+        // the compiler never orders an LDS read behind the prefetched global loads.
+        constexpr int U = 4;
+        constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
+        const int m4 = m >> 2;
+        const int steps = (m4 + 64 * U - 1) / (64 * U);
+        const float4* vt4 = reinterpret_cast<const float4*>(lds);
+        float4 ga[U], ea[U], gb[U], eb[U];
+        float acc[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[j] = 0.f;
+
+        auto issue = [&](float4 (&gx)[U], float4 (&ex)[U], int64_t r_, int st_) {
+            const float4* g4 = reinterpret_cast<const float4*>(G + s.offset + r_ * m);
+            const float4* e4 = reinterpret_cast<const float4*>(E + s.offset + r_ * m);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: no exec-masked blocks
+                const int c = min(st_ * 64 * U + u * 64 + lane, m4 - 1);
+                gx[u] = g4[c];
+                if constexpr (LOAD_E) ex[u] = e4[c];
+            }
+        };
+        auto consume = [&](float4 (&gx)[U], float4 (&ex)[U], int64_t r_, int st_) {
+            float4* e4 = reinterpret_cast<float4*>(E + s.offset + r_ * m);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int cu = st_ * 64 * U + u * 64 + lane;
+                const bool ok = cu < m4;  // lanes past the row end loaded a clamped copy
+                const int c = ok ? cu : m4 - 1;
+                float4 x = gx[u];
+                if constexpr (EF == ARCTOPK_EF14 && ERR_IN) {
+                    x.x += ex[u].x; x.y += ex[u].y; x.z += ex[u].z; x.w += ex[u].w;
+                } else if constexpr (EF == ARCTOPK_EF21) {
+                    x.x -= ex[u].x; x.y -= ex[u].y; x.z -= ex[u].z; x.w -= ex[u].w;
+                }
+                if constexpr (WRITE_E) {
+                    if (ok) e4[c] = x;
+                }
+                if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    float4 v;
+                    if constexpr (VLDS) {
+                        v = vt4[j * m4 + c];
+                    } else {
+                        const float* vp = Vs + (int64_t)(4 * c) * R + j;
+                        v = make_float4(vp[0], vp[R], vp[2 * R], vp[3 * R]);
+                    }
+                    float a = acc[j];
+                    a = fmaf(x.x, v.x, a);
+                    a = fmaf(x.y, v.y, a);
+                    a = fmaf(x.z, v.z, a);
+                    a = fmaf(x.w, v.w, a);
+                    acc[j] = a;
+                }
+            }
+            if (st_ == steps - 1) {
+#pragma unroll
+                for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
+                if (lane < R) {
+                    float v = acc[0];
+#pragma unroll
+                    for (int j = 1; j < R; ++j)
+                        if (lane == j) v = acc[j];
+                    sketch[s.sketch_off + r_ * R + lane] = v;
+                }
+#pragma unroll
+                for (int j = 0; j < R; ++j) acc[j] = 0.f;
+            }
+        };
+        // cursor over (row, step) pairs of this wave: rows row0+wave, +4, ...
+        int64_t ra = t.row0 + wave;
+        int sa = 0;
+        if (ra < row_end) issue(ga, ea, ra, sa);
+        while (ra < row_end) {
+            int64_t rb = ra;
+            int sb = sa + 1;
+            if (sb == steps) { sb = 0; rb += 4; }
+            if (rb < row_end) issue(gb, eb, rb, sb);
+            consume(ga, ea, ra, sa);
+            if (rb >= row_end) break;
+            ra = rb;
+            sa = sb + 1;
+            if (sa == steps) { sa = 0; ra += 4; }
+            if (ra < row_end) issue(ga, ea, ra, sa);
+            consume(gb, eb, rb, sb);
+        }
+    } else {  // ENC_ROW_SCALAR
+        for (int64_t row = t.row0 + wave; row < row_end; row += 4) {
+            const int64_t base = s.offset + row * m;
+            float acc[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc[j] = 0.f;
+            for (int c = lane; c < m; c += 64) {
+                const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, c);
+                if constexpr (WRITE_E) E[base + c] = x;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    float v;
+                    if constexpr (VLDS) v = lds[j * m + c];
+                    else v = Vs[(int64_t)c * R + j];
+                    acc[j] = fmaf(x, v, acc[j]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
+            if (lane < R) {
+                float v = acc[0];
+#pragma unroll
+                for (int j = 1; j < R; ++j)
+                    if (lane == j) v = acc[j];
+                sketch[s.sketch_off + row * R + lane] = v;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2 select
+// ---------------------------------------------------------------------------
+// Energy of a row exactly as the reference forms it on the all-reduced sketch:
+// p_j = P_j / ws (IEEE division, ref `P /= ws`), q_j = p_j * p_j (`P ** 2`), then
+// ((q_0 + q_1) + q_2) + q_3 (torch.sum over dim 1, sequential for r <= 4).
+// __fmul_rn/__fadd_rn keep the compiler from contracting into FMAs.
+__device__ __forceinline__ float row_energy(const float* __restrict__ p, int R, float wsf, int kind) {
+    if (kind == ARCTOPK_SEG_RAW) {
+        const float v = __fdiv_rn(p[0], wsf);
+        return __fmul_rn(v, v);
+    }
+    float a = __fdiv_rn(p[0], wsf);
+    float s = __fmul_rn(a, a);
+    for (int j = 1; j < R; ++j) {
+        const float b = __fdiv_rn(p[j], wsf);
+        s = __fadd_rn(s, __fmul_rn(b, b));
+    }
+    return s;
+}
+
+// Order key: energies are >= +0 or NaN; as uint32 the non-negative floats are
+// ordered, and every NaN (either sign) maps above +inf, as torch.topk ranks NaN largest.
+__device__ __forceinline__ uint32_t energy_key(float e) {
+    uint32_t u = __float_as_uint(e);
+    if (e != e) u = 0xFFFFFFFFu;  // NaN largest
+    return u & 0x7FFFFFFFu ? u : 0u;  // -0 cannot occur; keep +0 = 0
+}
+
+__global__ void __launch_bounds__(256) k_energy(const SegDev* __restrict__ segs, int nseg,
+                                                const float* __restrict__ sketch, int R, float wsf,
+                                                uint32_t* __restrict__ keys, float* __restrict__ energy) {
+    const int si = blockIdx.y;
+    const SegDev s = segs[si];
+    const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
+    for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < s.n;
+         row += (int64_t)gridDim.x * 256) {
+        const float e = row_energy(sketch + s.sketch_off + row * stride, R, wsf, s.kind);
+        if (keys) keys[s.row_off + row] = energy_key(e);
+        if (energy) energy[s.row_off + row] = e;
+    }
+}
+
+constexpr int kSelThreads = 1024;
+constexpr int kSelWaves = kSelThreads / 64;
+
+// exclusive scan of one value per thread across the block; returns the block total
+__device__ __forceinline__ int64_t block_exscan(int64_t v, int64_t* wsum, int64_t& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        int64_t w = lane < kSelWaves ? wsum[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < kSelWaves) wsum[lane] = w;  // inclusive
+    }
+    __syncthreads();
+    const int64_t before = (wave ? wsum[wave - 1] : 0) + x - v;
+    total = wsum[kSelWaves - 1];
+    __syncthreads();
+    return before;
+}
+
+struct SelShared {
+    uint32_t hist[256];
+    int64_t wsum[kSelWaves];
+    uint32_t digit;
+    int64_t kk;
+};
+
+// One block: MSB-first 8-bit radix select of the k-th largest of keys[0..n) (LDS or
+// global), then an index-ordered compaction (ties at the threshold: lowest rows
+// first) writing the ascending row list and every row's slot (or -1).
+template <typename KeyT>
+__device__ void select_rows(const KeyT* keys, int64_t n, int64_t k, int32_t* __restrict__ rl,
+                            int32_t* __restrict__ sm, SelShared& sh) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    uint32_t prefix = 0, mask = 0;
+    int64_t kk = k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = tid; i < 256; i += kSelThreads) sh.hist[i] = 0;
+        __syncthreads();
+        for (int64_t i = tid; i < n; i += kSelThreads) {
+            const uint32_t key = keys[i];
+            if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            uint32_t c[4];
+            uint32_t sum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = sh.hist[255 - 4 * lane - q];
+                sum += c[q];
+            }
+            uint32_t incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t excl = incl - sum;
+            if ((uint64_t)excl < (uint64_t)kk && (uint64_t)incl >= (uint64_t)kk) {
+                uint32_t acc = excl;
+                int q = 0;
+                for (; q < 3; ++q) {
+                    if ((uint64_t)(acc + c[q]) >= (uint64_t)kk) break;
+                    acc += c[q];
+                }
+                sh.digit = 255 - 4 * lane - q;
+                sh.kk = kk - acc;
+            }
+        }
+        __syncthreads();
+        prefix |= sh.digit << shift;
+        mask |= 255u << shift;
+        kk = sh.kk;
+        __syncthreads();
+    }
+    const uint32_t T = prefix;
+    const int64_t need_eq = kk;
+    const int64_t per = (n + kSelThreads - 1) / kSelThreads;
+    const int64_t r0 = min<int64_t>(n, tid * per), r1 = min<int64_t>(n, r0 + per);
+    int64_t gt = 0, eq = 0;
+    for (int64_t i = r0; i < r1; ++i) {
+        const uint32_t key = keys[i];
+        gt += key > T;
+        eq += key == T;
+    }
+    int64_t tot;
+    const int64_t eq_before = block_exscan(eq, sh.wsum, tot);
+    int64_t take_eq = need_eq - eq_before;
+    take_eq = take_eq < 0 ? 0 : (take_eq > eq ? eq : take_eq);
+    int64_t slot = block_exscan(gt + take_eq, sh.wsum, tot);
+    int64_t eq_seen = 0;
+    for (int64_t i = r0; i < r1; ++i) {
+        const uint32_t key = keys[i];
+        bool sel = key > T;
+        if (key == T) {
+            sel = eq_seen < take_eq;
+            ++eq_seen;
+        }
+        if (sel) {
+            rl[slot] = (int32_t)i;
+            sm[i] = (int32_t)slot;
+            ++slot;
+        } else {
+            sm[i] = -1;
+        }
+    }
+}
+
+// Radix select without atomics, for keys resident in LDS: 8 passes of 4-bit digits,
+// each digit's count formed by wave ballots (energies of one tensor share their top
+// bits, so per-key LDS atomics would serialise on one or two histogram bins).
+struct SelSharedB {
+    uint32_t cnt[kSelWaves][16];
+    int64_t wsum[kSelWaves];
+    uint32_t digit;
+    int64_t kk;
+};
+
+__device__ void select_rows_lds(const uint32_t* keys, int n, int64_t k, int32_t* __restrict__ rl,
+                                int32_t* __restrict__ sm, SelSharedB& sh) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    uint32_t prefix = 0, mask = 0;
+    int64_t kk = k;
+    for (int shift = 28; shift >= 0; shift -= 4) {
+        uint32_t mycnt = 0;  // lane d < 16 accumulates this wave's count of digit d
+        for (int base = 0; base < n; base += kSelThreads) {
+            const int i = base + tid;
+            const uint32_t key = i < n ? keys[i] : 0u;
+            const bool live = i < n && (key & mask) == prefix;
+            const uint32_t dig = (key >> shift) & 15u;
+#pragma unroll
+            for (int d = 0; d < 16; ++d) {
+                const uint32_t c = (uint32_t)__popcll(__ballot(live && dig == (uint32_t)d));
+                if (lane == d) mycnt += c;
+            }
+        }
+        if (lane < 16) sh.cnt[wave][lane] = mycnt;
+        __syncthreads();
+        if (wave == 0) {
+            // lane q (< 16) owns digit 15 - q: descending order for a prefix scan
+            uint32_t c = 0;
+            if (lane < 16) {
+#pragma unroll
+                for (int w = 0; w < kSelWaves; ++w) c += sh.cnt[w][15 - lane];
+            }
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t excl = incl - c;
+            if (lane < 16 && (uint64_t)excl < (uint64_t)kk && (uint64_t)incl >= (uint64_t)kk) {
+                sh.digit = 15 - lane;
+                sh.kk = kk - excl;
+            }
+        }
+        __syncthreads();
+        prefix |= sh.digit << shift;
+        mask |= 15u << shift;
+        kk = sh.kk;
+        __syncthreads();
+    }
+    const uint32_t T = prefix;
+    const int64_t need_eq = kk;
+    const int per = (n + kSelThreads - 1) / kSelThreads;
+    const int r0 = min(n, tid * per), r1 = min(n, r0 + per);
+    int64_t gt = 0, eq = 0;
+    for (int i = r0; i < r1; ++i) {
+        const uint32_t key = keys[i];
+        gt += key > T;
+        eq += key == T;
+    }
+    int64_t tot;
+    const int64_t eq_before = block_exscan(eq, sh.wsum, tot);
+    int64_t take_eq = need_eq - eq_before;
+    take_eq = take_eq < 0 ? 0 : (take_eq > eq ? eq : take_eq);
+    int64_t slot = block_exscan(gt + take_eq, sh.wsum, tot);
+    int64_t eq_seen = 0;
+    for (int i = r0; i < r1; ++i) {
+        const uint32_t key = keys[i];
+        bool sel = key > T;
+        if (key == T) {
+            sel = eq_seen < take_eq;
+            ++eq_seen;
+        }
+        if (sel) {
+            rl[slot] = i;
+            sm[i] = (int32_t)slot;
+            ++slot;
+        } else {
+            sm[i] = -1;
+        }
+    }
+}
+
+// Segments with n <= kSmallSelRows: energies straight into LDS, select, compact -- one launch.
+__global__ void __launch_bounds__(kSelThreads) k_select_small(const SegDev* __restrict__ segs,
+                                                              const int32_t* __restrict__ seg_ids,
+                                                              const float* __restrict__ sketch,
+                                                              int R, float wsf,
+                                                              int32_t* __restrict__ rowlist,
+                                                              int32_t* __restrict__ slotmap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t skeys[];
+    __shared__ SelSharedB sh;
+    const SegDev s = segs[seg_ids[blockIdx.x]];
+    const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
+    const float* sk = sketch + s.sketch_off;
+    for (int64_t row = threadIdx.x; row < s.n; row += kSelThreads)
+        skeys[row] = energy_key(row_energy(sk + row * stride, R, wsf, s.kind));
+    __syncthreads();
+    select_rows_lds(skeys, (int)s.n, s.k_rows, rowlist + s.sel_off, slotmap + s.row_off, sh);
+}
+
+// Larger segments: keys precomputed by k_energy into global memory.
+__global__ void __launch_bounds__(kSelThreads) k_select(const SegDev* __restrict__ segs,
+                                                        const int32_t* __restrict__ seg_ids,
+                                                        const uint32_t* __restrict__ keys_all,
+                                                        int32_t* __restrict__ rowlist,
+                                                        int32_t* __restrict__ slotmap) {
+    __shared__ SelShared sh;
+    const SegDev s = segs[seg_ids[blockIdx.x]];
+    select_rows(keys_all + s.row_off, s.n, s.k_rows, rowlist + s.sel_off, slotmap + s.row_off, sh);
+}
+
+// mean of the all-reduced values: x / ws exactly; for a power-of-two ws the
+// reciprocal is exact and x * (1/ws) rounds the same real number as x / ws.
+struct Scale {
+    float ws, inv;
+    int pow2;
+    __device__ __forceinline__ float operator()(float x) const {
+        return pow2 ? x * inv : __fdiv_rn(x, ws);
+    }
+    __device__ __forceinline__ float4 operator()(float4 x) const {
+        return make_float4((*this)(x.x), (*this)(x.y), (*this)(x.z), (*this)(x.w));
+    }
+};
+
+__device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m >= 256; }
+
+// ---------------------------------------------------------------------------
+// K3 pack
+// ---------------------------------------------------------------------------
+template <int EF>
+__device__ __forceinline__ float4 pack4(const float* __restrict__ G, float* __restrict__ E,
+                                        int64_t src) {
+    float4 v;
+    if constexpr (EF == ARCTOPK_EF_NONE) {
+        v = *reinterpret_cast<const float4*>(G + src);
+    } else if constexpr (EF == ARCTOPK_EF14) {
+        v = *reinterpret_cast<const float4*>(E + src);
+        *reinterpret_cast<float4*>(E + src) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+        const float4 g = *reinterpret_cast<const float4*>(G + src);
+        float4 ev = *reinterpret_cast<const float4*>(E + src);
+        v = make_float4(g.x - ev.x, g.y - ev.y, g.z - ev.z, g.w - ev.w);
+        ev.x += v.x; ev.y += v.y; ev.z += v.z; ev.w += v.w;
+        *reinterpret_cast<float4*>(E + src) = ev;
+    }
+    return v;
+}
+
+template <int EF>
+__global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
+                                              const Chunk* __restrict__ chunks,
+                                              const float* __restrict__ G, float* __restrict__ E,
+                                              const int32_t* __restrict__ rowlist,
+                                              float* __restrict__ packed) {
+    const Chunk ch = chunks[blockIdx.x];
+    const SegDev s = segs[ch.seg];
+    const int m = (int)s.m;
+    const int32_t* rl = rowlist + s.sel_off + ch.row0;
+    float* dst = packed + s.packed_off + ch.row0 * m;
+    if (row_path(s)) {  // wave per selected row: all of a row's loads first, then stores
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int m4 = m >> 2;
+        constexpr int U = 8;
+        for (int64_t j = wave; j < ch.nrows; j += 4) {
+            const int64_t src_row = s.offset + (int64_t)rl[j] * m;
+            const float4* g4 = reinterpret_cast<const float4*>(G + src_row);
+            float4* e4 = reinterpret_cast<float4*>(E + src_row);
+            float4* d4 = reinterpret_cast<float4*>(dst + j * m);
+            for (int c0 = 0; c0 < m4; c0 += 64 * U) {
+                float4 a[U], b[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int c = min(c0 + u * 64 + lane, m4 - 1);
+                    if constexpr (EF == ARCTOPK_EF_NONE) a[u] = g4[c];
+                    else if constexpr (EF == ARCTOPK_EF14) a[u] = e4[c];
+                    else { a[u] = g4[c]; b[u] = e4[c]; }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int c = c0 + u * 64 + lane;
+                    if (c < m4) {
+                        if constexpr (EF == ARCTOPK_EF_NONE) {
+                            d4[c] = a[u];
+                        } else if constexpr (EF == ARCTOPK_EF14) {
+                            d4[c] = a[u];
+                            e4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        } else {
+                            const float4 dv = make_float4(a[u].x - b[u].x, a[u].y - b[u].y,
+                                                          a[u].z - b[u].z, a[u].w - b[u].w);
+                            d4[c] = dv;
+                            e4[c] = make_float4(b[u].x + dv.x, b[u].y + dv.y, b[u].z + dv.z,
+                                                b[u].w + dv.w);
+                        }
+                    }
+                }
+            }
+        }
+        return;
+    }
+    const uint32_t cnt = (uint32_t)(ch.nrows * m);
+    if (s.vec) {
+        const uint32_t cnt4 = cnt >> 2;
+        for (uint32_t q = threadIdx.x; q < cnt4; q += 256) {
+            const uint32_t e = q << 2;
+            const uint32_t srow = fdiv(e, s.mdiv);
+            const uint32_t col = e - srow * (uint32_t)m;
+            const int64_t src = s.offset + (int64_t)rl[srow] * m + col;
+            *reinterpret_cast<float4*>(dst + e) = pack4<EF>(G, E, src);
+        }
+    } else {
+        for (uint32_t e = threadIdx.x; e < cnt; e += 256) {
+            const uint32_t srow = fdiv(e, s.mdiv);
+            const uint32_t col = e - srow * (uint32_t)m;
+            const int64_t src = s.offset + (int64_t)rl[srow] * m + col;
+            float v;
+            if constexpr (EF == ARCTOPK_EF_NONE) {
+                v = G[src];
+            } else if constexpr (EF == ARCTOPK_EF14) {
+                v = E[src];
+                E[src] = 0.f;
+            } else {
+                const float ev = E[src];
+                v = G[src] - ev;
+                E[src] = ev + v;
+            }
+            dst[e] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4 decode
+// ---------------------------------------------------------------------------
+template <int EF>
+__global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
+                                                const Chunk* __restrict__ chunks,
+                                                const float* __restrict__ packed,
+                                                const int32_t* __restrict__ slotmap, Scale sc,
+                                                float* __restrict__ gE, float* __restrict__ out) {
+    const Chunk ch = chunks[blockIdx.x];
+    const SegDev s = segs[ch.seg];
+    const int m = (int)s.m;
+    const int64_t base = s.offset + ch.row0 * m;
+    const int32_t* sm = slotmap + s.row_off + ch.row0;
+    const float* pk = packed + s.packed_off;
+    if (row_path(s)) {  // wave per row: one slot lookup per row, float4 streams
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int m4 = m >> 2;
+        for (int64_t j = wave; j < ch.nrows; j += 4) {
+            const int32_t slot = sm[j];
+            float4* o4 = reinterpret_cast<float4*>(out + base + j * m);
+            float4* g4 = reinterpret_cast<float4*>(gE + base + j * m);
+            if (slot < 0) {
+                if constexpr (EF == ARCTOPK_EF21) {
+#pragma unroll 4
+                    for (int c = lane; c < m4; c += 64) {
+                        const float4 g = g4[c];
+                        o4[c] = make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f);
+                    }
+                } else {
+#pragma unroll 8
+                    for (int c = lane; c < m4; c += 64) o4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            } else {
+                const float4* p4 = reinterpret_cast<const float4*>(pk + (int64_t)slot * m);
+#pragma unroll 4
+                for (int c = lane; c < m4; c += 64) {
+                    float4 v = sc(p4[c]);
+                    if constexpr (EF == ARCTOPK_EF21) {
+                        const float4 g = g4[c];
+                        v = make_float4(g.x + v.x, g.y + v.y, g.z + v.z, g.w + v.w);
+                        g4[c] = v;
+                    }
+                    o4[c] = v;
+                }
+            }
+        }
+        return;
+    }
+    const uint32_t cnt = (uint32_t)(ch.nrows * m);
+    if (s.vec) {
+        const uint32_t cnt4 = cnt >> 2;
+        for (uint32_t q = threadIdx.x; q < cnt4; q += 256) {
+            const uint32_t e = q << 2;
+            const uint32_t row = fdiv(e, s.mdiv);
+            const uint32_t col = e - row * (uint32_t)m;
+            const int32_t slot = sm[row];
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (slot >= 0) v = sc(*reinterpret_cast<const float4*>(pk + (int64_t)slot * m + col));
+            if constexpr (EF == ARCTOPK_EF21) {
+                const float4 g = *reinterpret_cast<const float4*>(gE + base + e);
+                v = make_float4(g.x + v.x, g.y + v.y, g.z + v.z, g.w + v.w);
+                if (slot >= 0) *reinterpret_cast<float4*>(gE + base + e) = v;
+            }
+            *reinterpret_cast<float4*>(out + base + e) = v;
+        }
+    } else {
+        for (uint32_t e = threadIdx.x; e < cnt; e += 256) {
+            const uint32_t row = fdiv(e, s.mdiv);
+            const uint32_t col = e - row * (uint32_t)m;
+            const int32_t slot = sm[row];
+            float v = 0.f;
+            if (slot >= 0) v = sc(pk[(int64_t)slot * m + col]);
+            if constexpr (EF == ARCTOPK_EF21) {
+                v = gE[base + e] + v;
+                if (slot >= 0) gE[base + e] = v;
+            }
+            out[base + e] = v;
+        }
+    }
+}
+
+template <int EF, bool ERR_IN>
+__global__ void __launch_bounds__(256) k_ef_apply(float* __restrict__ x, float* __restrict__ E,
+                                                  int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t n4 = n >> 2;
+    float4* x4 = reinterpret_cast<float4*>(x);
+    float4* e4 = reinterpret_cast<float4*>(E);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+        const float4 v = ef_apply4<EF, ERR_IN>(x4, e4, i);
+        if constexpr (EF == ARCTOPK_EF14) e4[i] = v;
+        if constexpr (EF != ARCTOPK_EF14 || ERR_IN) x4[i] = v;
+    }
+    for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const float v = ef_apply1<EF, ERR_IN>(x, E, i);
+        if constexpr (EF == ARCTOPK_EF14) E[i] = v;
+        if constexpr (EF != ARCTOPK_EF14 || ERR_IN) x[i] = v;
+    }
+}
+
+template <int R, bool VLDS>
+int launch_encode_rv(const arctopk_plan* p, const float* G, float* E, int ef, int err_in,
+                     const float* V, float* sk, hipStream_t st) {
+    dim3 grid(p->n_enc), block(256);
+    const size_t lds = p->enc_lds_bytes;
+    if (ef == ARCTOPK_EF_NONE)
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF_NONE, false, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+    else if (ef == ARCTOPK_EF14 && err_in)
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, true, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+    else if (ef == ARCTOPK_EF14)
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, false, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+    else
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF21, true, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+    return (int)hipGetLastError();
+}
+
+template <int R>
+int launch_encode_r(const arctopk_plan* p, const float* G, float* E, int ef, int err_in,
+                    const float* V, float* sk, hipStream_t st) {
+    return p->enc_vlds ? launch_encode_rv<R, true>(p, G, E, ef, err_in, V, sk, st)
+                       : launch_encode_rv<R, false>(p, G, E, ef, err_in, V, sk, st);
+}
+
+}  // namespace
+
+extern "C" int arctopk_encode(const arctopk_plan* p, const float* grad, float* err, int32_t ef,
+                              int32_t err_in, const float* V, float* sketch, void* stream) {
+    if (!p || !grad || !sketch) return ARCTOPK_EINVAL;
+    if (ef != ARCTOPK_EF_NONE && !err) return ARCTOPK_EINVAL;
+    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
+    if (p->info.v_len > 0 && !V) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    switch (p->r) {
+        case 1: return launch_encode_r<1>(p, grad, err, ef, err_in, V, sketch, st);
+        case 2: return launch_encode_r<2>(p, grad, err, ef, err_in, V, sketch, st);
+        case 3: return launch_encode_r<3>(p, grad, err, ef, err_in, V, sketch, st);
+        case 4: return launch_encode_r<4>(p, grad, err, ef, err_in, V, sketch, st);
+        case 5: return launch_encode_r<5>(p, grad, err, ef, err_in, V, sketch, st);
+        case 6: return launch_encode_r<6>(p, grad, err, ef, err_in, V, sketch, st);
+        case 7: return launch_encode_r<7>(p, grad, err, ef, err_in, V, sketch, st);
+        case 8: return launch_encode_r<8>(p, grad, err, ef, err_in, V, sketch, st);
+    }
+    return ARCTOPK_EINVAL;
+}
+
+static int launch_energy(const arctopk_plan* p, const float* sketch, int32_t ws, uint32_t* keys,
+                         float* energy, hipStream_t st) {
+    int64_t maxn = 0;
+    for (int i = 0; i < p->nseg; ++i) maxn = std::max<int64_t>(maxn, p->h_segs[i].n);
+    int gx = (int)std::min<int64_t>(1024, (maxn + 255) / 256);
+    dim3 grid(gx, p->nseg);
+    hipLaunchKernelGGL(k_energy, grid, dim3(256), 0, st, p->d_segs, p->nseg, sketch, p->r,
+                       (float)ws, keys, energy);
+    return (int)hipGetLastError();
+}
+
+extern "C" int arctopk_row_energy(const arctopk_plan* p, const float* sketch, int32_t ws,
+                                  float* energy, void* stream) {
+    if (!p || !sketch || !energy || ws < 1) return ARCTOPK_EINVAL;
+    return launch_energy(p, sketch, ws, nullptr, energy, (hipStream_t)stream);
+}
+
+extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_t ws,
+                              int32_t* rowlist, int32_t* slotmap, void* stream) {
+    if (!p || !sketch || !rowlist || !slotmap || ws < 1) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (p->n_small) {
+        hipLaunchKernelGGL(k_select_small, dim3(p->n_small), dim3(kSelThreads),
+                           (size_t)p->small_lds, st, p->d_segs, p->d_small, sketch, p->r, (float)ws,
+                           rowlist, slotmap);
+    }
+    if (p->n_large) {
+        int e = launch_energy(p, sketch, ws, p->d_keys, nullptr, st);
+        if (e) return e;
+        hipLaunchKernelGGL(k_select, dim3(p->n_large), dim3(kSelThreads), 0, st, p->d_segs,
+                           p->d_large, p->d_keys, rowlist, slotmap);
+    }
+    return (int)hipGetLastError();
+}
+
+extern "C" int arctopk_pack(const arctopk_plan* p, const float* grad, float* err, int32_t ef,
+                            const int32_t* rowlist, float* packed, void* stream) {
+    if (!p || !rowlist || !packed) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF_NONE ? !grad : !err) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF21 && !grad) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid(p->n_pack), block(256);
+    if (ef == ARCTOPK_EF_NONE)
+        hipLaunchKernelGGL(k_pack<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, p->d_pack, grad, err, rowlist, packed);
+    else if (ef == ARCTOPK_EF14)
+        hipLaunchKernelGGL(k_pack<ARCTOPK_EF14>, grid, block, 0, st, p->d_segs, p->d_pack, grad, err, rowlist, packed);
+    else if (ef == ARCTOPK_EF21)
+        hipLaunchKernelGGL(k_pack<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, p->d_pack, grad, err, rowlist, packed);
+    else
+        return ARCTOPK_EINVAL;
+    return (int)hipGetLastError();
+}
+
+extern "C" int arctopk_decode(const arctopk_plan* p, const float* packed, const int32_t* slotmap,
+                              int32_t ws, int32_t ef, float* gerr, float* out, void* stream) {
+    if (!p || !packed || !slotmap || !out || ws < 1) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF21 && !gerr) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid(p->n_dec), block(256);
+    Scale sc;
+    sc.ws = (float)ws;
+    sc.pow2 = (ws & (ws - 1)) == 0;
+    sc.inv = 1.0f / (float)ws;
+    if (ef == ARCTOPK_EF21)
+        hipLaunchKernelGGL(k_decode<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, p->d_dec, packed, slotmap, sc, gerr, out);
+    else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
+        hipLaunchKernelGGL(k_decode<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, p->d_dec, packed, slotmap, sc, gerr, out);
+    else
+        return ARCTOPK_EINVAL;
+    return (int)hipGetLastError();
+}
+
+extern "C" int arctopk_ef_apply(float* x, float* E, int64_t n, int32_t ef, int32_t err_in,
+                                void* stream) {
+    if (!x || n < 0) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF_NONE || n == 0) return 0;
+    if (!E) return ARCTOPK_EINVAL;
+    // float4 path needs 16-B aligned x and E (torch allocations are)
+    if (((uintptr_t)x | (uintptr_t)E) & 15) return ARCTOPK_EINVAL;
+    const int grid = (int)std::min<int64_t>(8192, (n / 4 + 255) / 256 + 1);
+    hipStream_t st = (hipStream_t)stream;
+    if (ef == ARCTOPK_EF14 && err_in)
+        hipLaunchKernelGGL((k_ef_apply<ARCTOPK_EF14, true>), dim3(grid), dim3(256), 0, st, x, E, n);
+    else if (ef == ARCTOPK_EF14)
+        hipLaunchKernelGGL((k_ef_apply<ARCTOPK_EF14, false>), dim3(grid), dim3(256), 0, st, x, E, n);
+    else if (ef == ARCTOPK_EF21)
+        hipLaunchKernelGGL((k_ef_apply<ARCTOPK_EF21, true>), dim3(grid), dim3(256), 0, st, x, E, n);
+    else
+        return ARCTOPK_EINVAL;
+    return (int)hipGetLastError();
+}

@@ -1,0 +1,85 @@
+// Shared device-side structures of libarctopk (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "arctopk.h"
+
+namespace arctopk {
+
+constexpr int kMaxR = 8;           // sketch rank supported by the kernels
+constexpr int kTileRows = 256;     // rows of one small-m encode tile (thread per row)
+constexpr int kSmallM = 64;        // m below this: thread-per-row tiles; else wave-per-row
+constexpr int kVLdsMaxBytes = 64 * 1024;  // V staged in LDS up to this size, else read from L2
+constexpr int kChunkElems = 16384; // target elements per pack/decode work chunk
+constexpr int kSmallSelRows = 15360;  // rows up to this: keys in LDS (60 KiB + statics < 64 KiB)
+
+// 32-bit quotient by a runtime divisor: q = mulhi64(x, ceil(2^64/d)) is exact for
+// x, d < 2^32 (the fractional error x/2^64 < 1/d never crosses an integer).
+struct FastDiv {
+    uint64_t magic;
+    uint32_t d;
+    uint32_t pad;
+};
+
+__host__ inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    f.pad = 0;
+    f.magic = (d <= 1) ? 0 : (~0ull / d) + 1ull;
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+    return f.d <= 1 ? x : (uint32_t)__umul64hi((uint64_t)x, f.magic);
+}
+
+struct SegDev {
+    int64_t offset, n, m, k_rows, sketch_off, v_off, packed_off, row_off, sel_off;
+    int32_t kind;
+    int32_t vec;       // 1: m % 4 == 0 and offset % 4 == 0 and packed_off % 4 == 0
+    FastDiv mdiv;      // division by m
+};
+
+// encode tile modes
+enum : int32_t { ENC_ROW_VEC = 0, ENC_ROW_SCALAR = 1, ENC_TILE = 2, ENC_RAW = 3 };
+
+struct EncTile {
+    int32_t seg;
+    int32_t mode;
+    int64_t row0;      // first row (RAW: first element)
+    int64_t nrows;     // rows (RAW: elements)
+};
+
+struct Chunk {         // pack: selected-row range; decode: row range
+    int32_t seg;
+    int32_t pad;
+    int64_t row0;
+    int64_t nrows;
+};
+
+}  // namespace arctopk
+
+struct arctopk_plan {
+    int device;
+    int r;
+    double ratio;
+    int nseg;
+    arctopk_plan_info info;
+    arctopk_segment* h_segs;      // host copy
+    arctopk::SegDev* d_segs;
+    arctopk::EncTile* d_enc;
+    int n_enc;
+    int enc_lds_bytes;
+    int enc_vlds;                 // every wave-per-row segment's V fits in LDS
+    arctopk::Chunk* d_pack;
+    int n_pack;
+    arctopk::Chunk* d_dec;
+    int n_dec;
+    uint32_t* d_keys;             // select workspace: one key per row
+    int32_t* d_small;             // segments selected by the fused one-block kernel
+    int n_small;
+    int small_lds;                // bytes of LDS keys for the largest small segment
+    int32_t* d_large;             // segments whose keys go through global memory
+    int n_large;
+};

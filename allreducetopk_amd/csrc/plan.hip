@@ -1,0 +1,229 @@
+// Bucket plan: geometry of every gradient view (reference cal_k / reshape rules),
+// buffer offsets, and the work tables of the encode / pack / decode kernels.
+// Built once per bucket layout; nothing here runs per call.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "common.h"
+
+using namespace arctopk;
+
+namespace {
+
+int build_segments(const int64_t* dims, const int32_t* ndims, int32_t ntensors, int r, double ratio,
+                   std::vector<arctopk_segment>& segs, arctopk_plan_info& info) {
+    int64_t off = 0, sk = 0, vo = 0, po = 0, ro = 0, so = 0;
+    const int64_t* d = dims;
+    for (int i = 0; i < ntensors; ++i) {
+        const int nd = ndims[i];
+        if (nd < 1) return ARCTOPK_EINVAL;  // 0-dim: shape[-1] fails in the reference
+        int64_t numel = 1;
+        for (int j = 0; j < nd; ++j) numel *= d[j];
+        arctopk_segment s;
+        std::memset(&s, 0, sizeof(s));
+        s.offset = off;
+        if (nd == 1) {                      // ref :19-41
+            s.kind = ARCTOPK_SEG_RAW;
+            s.n = numel;
+            s.m = 1;
+        } else if (nd == 2) {               // ref :44-47
+            s.kind = ARCTOPK_SEG_SKETCH;
+            s.n = d[0];
+            s.m = d[1];
+        } else {                            // ref :72-77
+            const int64_t t = d[nd - 1];
+            s.kind = ARCTOPK_SEG_SKETCH;
+            s.m = 2 * t * t;
+            if (s.m == 0) return ARCTOPK_EEMPTY;
+            s.n = numel / s.m;
+            if (s.n * s.m != numel) return ARCTOPK_ERESHAPE;
+        }
+        if (numel == 0 || s.n == 0 || s.m == 0) return ARCTOPK_EEMPTY;
+        if (numel >= (int64_t(1) << 31)) return ARCTOPK_EINVAL;  // 32-bit in-segment indexing
+        // k = max(1, int(n * ratio)): float64 product, truncation (ref cal_k :173-187)
+        int64_t k = (int64_t)((double)s.n * ratio);
+        if (k < 1) k = 1;
+        if (k > s.n) return ARCTOPK_EINVAL;  // torch.topk raises for k > n
+        s.k_rows = k;
+        s.sketch_off = sk;
+        sk += (s.kind == ARCTOPK_SEG_RAW) ? s.n : s.n * r;
+        s.v_off = (s.kind == ARCTOPK_SEG_RAW) ? -1 : vo;
+        if (s.kind == ARCTOPK_SEG_SKETCH) vo += s.m * r;
+        s.packed_off = po;
+        po += k * s.m;
+        s.row_off = ro;
+        ro += s.n;
+        s.sel_off = so;
+        so += k;
+        segs.push_back(s);
+        off += numel;
+        d += nd;
+    }
+    info.numel = off;
+    info.sketch_len = sk;
+    info.v_len = vo;
+    info.packed_len = po;
+    info.sel_rows = so;
+    info.rows_total = ro;
+    info.nseg = ntensors;
+    info.r = r;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, int32_t ntensors,
+                                   int32_t r, double compress_ratio, int32_t dtype, int32_t device,
+                                   arctopk_plan** out) {
+    if (!dims || !ndims || !out || ntensors < 1) return ARCTOPK_EINVAL;
+    if (r < 1 || r > kMaxR) return ARCTOPK_EINVAL;
+    if (!(compress_ratio > 0.0) || compress_ratio > 1.0) return ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32) return ARCTOPK_EDTYPE;
+    *out = nullptr;
+
+    std::vector<arctopk_segment> segs;
+    arctopk_plan_info info;
+    std::memset(&info, 0, sizeof(info));
+    int st = build_segments(dims, ndims, ntensors, r, compress_ratio, segs, info);
+    if (st) return st;
+
+    std::vector<SegDev> dsegs(segs.size());
+    std::vector<int32_t> small_ids, large_ids;
+    int64_t small_rows = 0;
+    std::vector<EncTile> enc;
+    std::vector<Chunk> pack, dec;
+    int lds = 0;
+    int vlds = 1;
+    for (size_t i = 0; i < segs.size(); ++i) {
+        const arctopk_segment& s = segs[i];
+        SegDev& g = dsegs[i];
+        g.offset = s.offset; g.n = s.n; g.m = s.m; g.k_rows = s.k_rows;
+        g.sketch_off = s.sketch_off; g.v_off = s.v_off; g.packed_off = s.packed_off;
+        g.row_off = s.row_off; g.sel_off = s.sel_off; g.kind = s.kind;
+        g.vec = (s.m % 4 == 0 && s.offset % 4 == 0 && s.packed_off % 4 == 0) ? 1 : 0;
+        g.mdiv = make_fastdiv((uint32_t)s.m);
+        if (s.n <= kSmallSelRows) {
+            small_ids.push_back((int32_t)i);
+            small_rows = std::max<int64_t>(small_rows, s.n);
+        } else {
+            large_ids.push_back((int32_t)i);
+        }
+        // ---- encode tiles
+        if (s.kind == ARCTOPK_SEG_RAW) {
+            const int64_t per = 4096;
+            for (int64_t e = 0; e < s.n; e += per)
+                enc.push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e)});
+        } else if (s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536) {
+            for (int64_t row = 0; row < s.n; row += kTileRows)
+                enc.push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(kTileRows, s.n - row)});
+            lds = std::max<int>(lds, (int)(kTileRows * s.m * 4 + s.m * r * 4));
+        } else {
+            // rows per tile: ~64K elements per block (4 waves), at least 4 rows
+            int64_t per = std::max<int64_t>(4, (64 * 1024) / s.m);
+            const int mode = g.vec ? ENC_ROW_VEC : ENC_ROW_SCALAR;
+            for (int64_t row = 0; row < s.n; row += per)
+                enc.push_back(EncTile{(int32_t)i, mode, row, std::min(per, s.n - row)});
+            const int vbytes = (int)(s.m * r * 4);
+            if (vbytes <= kVLdsMaxBytes) lds = std::max(lds, vbytes);
+            else vlds = 0;
+        }
+        // ---- pack chunks: selected rows, ~kChunkElems elements each
+        {
+            int64_t per = std::max<int64_t>(1, kChunkElems / s.m);
+            for (int64_t j = 0; j < s.k_rows; j += per)
+                pack.push_back(Chunk{(int32_t)i, 0, j, std::min(per, s.k_rows - j)});
+        }
+        // ---- decode chunks: all rows
+        {
+            int64_t per = std::max<int64_t>(1, kChunkElems / s.m);
+            for (int64_t row = 0; row < s.n; row += per)
+                dec.push_back(Chunk{(int32_t)i, 0, row, std::min(per, s.n - row)});
+        }
+    }
+
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return (int)e;
+    arctopk_plan* p = new (std::nothrow) arctopk_plan;
+    if (!p) return ARCTOPK_EINVAL;
+    std::memset(p, 0, sizeof(*p));
+    p->device = device;
+    p->r = r;
+    p->ratio = compress_ratio;
+    p->nseg = (int)segs.size();
+    p->info = info;
+    p->h_segs = new arctopk_segment[segs.size()];
+    std::copy(segs.begin(), segs.end(), p->h_segs);
+    p->n_enc = (int)enc.size();
+    p->n_pack = (int)pack.size();
+    p->n_dec = (int)dec.size();
+    p->enc_vlds = vlds;
+    p->enc_lds_bytes = vlds ? lds : std::max(0, lds);
+    p->n_small = (int)small_ids.size();
+    p->n_large = (int)large_ids.size();
+    p->small_lds = (int)(small_rows * 4);
+#define ALLOC_COPY(dst, vec)                                                                  \
+    do {                                                                                      \
+        e = hipMalloc((void**)&dst, std::max<size_t>(1, vec.size() * sizeof(vec[0])));        \
+        if (e == hipSuccess && !vec.empty())                                                  \
+            e = hipMemcpy(dst, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice); \
+        if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }                      \
+    } while (0)
+    ALLOC_COPY(p->d_segs, dsegs);
+    ALLOC_COPY(p->d_enc, enc);
+    ALLOC_COPY(p->d_pack, pack);
+    ALLOC_COPY(p->d_dec, dec);
+    ALLOC_COPY(p->d_small, small_ids);
+    ALLOC_COPY(p->d_large, large_ids);
+#undef ALLOC_COPY
+    e = hipMalloc((void**)&p->d_keys, std::max<size_t>(4, info.rows_total * sizeof(uint32_t)));
+    if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
+    *out = p;
+    return 0;
+}
+
+extern "C" int arctopk_plan_describe(const int64_t* dims, const int32_t* ndims, int32_t ntensors,
+                                     int32_t r, double compress_ratio, arctopk_segment* segs_out,
+                                     arctopk_plan_info* info) {
+    if (!dims || !ndims || !info || ntensors < 1) return ARCTOPK_EINVAL;
+    if (r < 1 || r > kMaxR) return ARCTOPK_EINVAL;
+    if (!(compress_ratio > 0.0) || compress_ratio > 1.0) return ARCTOPK_EINVAL;
+    std::vector<arctopk_segment> segs;
+    std::memset(info, 0, sizeof(*info));
+    int st = build_segments(dims, ndims, ntensors, r, compress_ratio, segs, *info);
+    if (st) return st;
+    if (segs_out) std::copy(segs.begin(), segs.end(), segs_out);
+    return 0;
+}
+
+extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
+    if (!p) return 0;
+    (void)hipSetDevice(p->device);
+    if (p->d_segs) (void)hipFree(p->d_segs);
+    if (p->d_enc) (void)hipFree(p->d_enc);
+    if (p->d_pack) (void)hipFree(p->d_pack);
+    if (p->d_dec) (void)hipFree(p->d_dec);
+    if (p->d_keys) (void)hipFree(p->d_keys);
+    if (p->d_small) (void)hipFree(p->d_small);
+    if (p->d_large) (void)hipFree(p->d_large);
+    delete[] p->h_segs;
+    delete p;
+    return 0;
+}
+
+extern "C" int arctopk_plan_query(const arctopk_plan* p, arctopk_plan_info* info) {
+    if (!p || !info) return ARCTOPK_EINVAL;
+    *info = p->info;
+    return 0;
+}
+
+extern "C" int arctopk_plan_segment(const arctopk_plan* p, int32_t i, arctopk_segment* seg) {
+    if (!p || !seg || i < 0 || i >= p->nseg) return ARCTOPK_EINVAL;
+    *seg = p->h_segs[i];
+    return 0;
+}
+
+extern "C" const char* arctopk_version(void) {
+    return "libarctopk 0.1 gfx950 (ARC-TopK encode/select/pack/decode, TopK/RandK)";
+}

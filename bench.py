@@ -1,0 +1,191 @@
+"""Benchmark of the ARC-TopK comm-hook codec on MI355X (BASELINE.json metric).
+
+One "step" = one ``group_topk_hook`` call on one 256 MiB fp32 gradient bucket
+(16 x [2048, 2048], the Llama-1B projection shape):
+encode -> RCCL all_reduce(sketch) -> select -> pack -> RCCL all_reduce(packed)
+-> decode, steady-state EF14 (configs[1]'s mode), compress_ratio 0.2, r 4,
+inputs resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W --ef ef14|ef21|noef]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line (rank 0).  ``value`` = bucket bytes processed by all ranks
+/ wall time of the K timed steps (max over ranks).  ``roofline`` prices the
+dominant kernel (encode) by its algorithmic HBM bytes over its HIP-event
+duration; ``cpu_baseline`` times the CPU oracle (test infrastructure) on a
+bounded sample of the same bucket on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel  # noqa: E402
+from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import (GroupTopKState,  # noqa: E402
+                                                                      group_topk_hook)
+
+METRIC = "compressed grad GB/s (device-resident) per GPU at k=0.2, r=4; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
+HEADLINE = [[2048, 2048]] * 16
+PHASES = ["encode", "sketch_allreduce", "select", "pack", "packed_allreduce", "decode"]
+
+
+def algorithmic_bytes(ef: str, shapes, ratio: float, r: int):
+    """Minimum HBM bytes per call, per phase (fp32, fused design)."""
+    n_el = bucket_numel(shapes)
+    rows = sum(s[0] for s in shapes)
+    k_el = sum(max(1, int(s[0] * ratio)) * s[1] for s in shapes)
+    sk = rows * r * 4
+    vbytes = sum(s[1] for s in shapes) * r * 4
+    if ef == "noef":
+        enc = 4 * n_el + sk + vbytes
+        pack = 4 * k_el + 4 * k_el
+        dec = 4 * k_el + 4 * n_el
+    elif ef == "ef14":
+        enc = 12 * n_el + sk + vbytes          # read G, E; write E := G + E
+        pack = 4 * k_el + 4 * k_el + 4 * k_el  # read E rows, write packed, zero E rows
+        dec = 4 * k_el + 4 * n_el
+    else:  # ef21
+        enc = 8 * n_el + sk + vbytes           # read G, E
+        pack = 8 * k_el + 4 * k_el + 4 * k_el  # read G, E rows; write packed, E rows
+        dec = 4 * k_el + 4 * n_el + 4 * n_el + 4 * k_el  # packed, gE, out, gE rows
+    sel = 2 * sk
+    return dict(encode=enc, select=sel, pack=pack, decode=dec, total=enc + sel + pack + dec)
+
+
+def cpu_baseline(ef: str, seconds: float, rank: int):
+    """Time the CPU oracle (a restatement of the reference hook) on the same bucket."""
+    from oracle import arctopk as A
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(1000 + rank)
+    n = bucket_numel(HEADLINE)
+    G = torch.randn(n, generator=g)
+    E = torch.randn(n, generator=g) * 0.1 if ef != "noef" else None
+    gE = torch.zeros(n) if ef == "ef21" else None
+    st = A.OracleState(r=4, compress_ratio=0.2, use_error_feedback=ef, seed=1234)
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 2:
+        seed = st.next_seed()
+        t0 = time.perf_counter()
+        A.simulate_step([G], [E], gE, HEADLINE, 0.2, 4, ef, seed)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(4 * n / med / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{len(times)} oracle calls (torch-CPU restatement of group_topk_hook, "
+                      f"ws=1, {ef}) on one 16x[2048,2048] fp32 bucket, median {med * 1e3:.1f} ms, "
+                      f"{os.cpu_count()} host CPUs visible"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--ef", default="ef14", choices=["noef", "ef14", "ef21"])
+    ap.add_argument("--ratio", type=float, default=0.2)
+    ap.add_argument("--r", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-phase-events", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    shapes = HEADLINE
+    n = bucket_numel(shapes)
+    bucket_bytes = 4 * n
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    buf = torch.randn(n, device=dev, generator=g)
+    bucket = SyntheticBucket(buf, shapes, index=0, is_last=True)
+    st = GroupTopKState(None, r=args.r, compress_ratio=args.ratio, start_compress_iter=0,
+                        use_error_feedback=args.ef, seed=1234)
+    # warm-up (EF14: first call creates E; EF21: first call is the dense init)
+    for _ in range(max(args.warmup, 2 if args.ef == "ef21" else 1)):
+        group_topk_hook(st, bucket)
+    torch.cuda.synchronize()
+    if not args.no_phase_events:
+        st.phase_events = []
+        st.phase_event_every = 4  # sample HIP events on every 4th timed call
+
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        group_topk_hook(st, bucket)
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    phase_ms = {}
+    if st.phase_events:
+        order = ["start"] + PHASES
+        for a, b in zip(order[:-1], order[1:]):
+            ds = [ev[a].elapsed_time(ev[b]) for ev in st.phase_events]
+            phase_ms[b] = statistics.mean(ds)
+        phase_ms["hook_device_total"] = statistics.mean(
+            ev["start"].elapsed_time(ev["decode"]) for ev in st.phase_events)
+
+    value = world * args.steps * bucket_bytes / elapsed / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+    alg = algorithmic_bytes(args.ef, shapes, args.ratio, args.r)
+    roof = None
+    if phase_ms:
+        enc_s = phase_ms["encode"] / 1e3
+        ach = alg["encode"] / enc_s / 1e9
+        roof = {"bound": "hbm", "kernel": "k_encode (EF pre-apply + rank-r sketch)",
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes_per_launch": alg["encode"],
+                "avg_launch_us": round(phase_ms["encode"] * 1e3, 2)}
+        hook_s = phase_ms["hook_device_total"] / 1e3
+        roof["hook"] = {"algorithmic_bytes": alg["total"], "device_us": round(hook_s * 1e6, 1),
+                        "achieved": round(alg["total"] / hook_s / 1e9, 1),
+                        "frac": round(alg["total"] / hook_s / 1e9 / HBM_PEAK_GBS, 4)}
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (N(0,1) fp32 gradients, per-rank seed)",
+        "config": {"workload": f"arctopk_{args.ef}_bucket_16x2048x2048_fp32_256MiB",
+                   "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
+                   "bucket_bytes": bucket_bytes, "parallelism": f"dp{world}",
+                   "collectives": "RCCL all_reduce x2 per bucket"},
+        "per_gpu_value": round(value / world, 2),
+        "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, rank)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+/*
+ * arctopk.h -- C ABI of libarctopk.so, the MI355X (gfx950) ARC-TopK / TopK /
+ * RandK gradient-bucket codec.
+ *
+ * Boundary.  The reference (Aris-ma/AllreduceTopK) is pure Python: its hot path
+ * is the DDP comm hook `group_topk_hook(state, bucket)`
+ * (comm_hooks/group_topk_hook_no_reshape.py:190-297) plus the TopK/RandK hook
+ * `sparse_hook_sync` (comm_hooks/sparse_hook.py:163-304), and all arithmetic in
+ * them is torch aten ops.  This library replaces exactly those aten op sequences
+ * with stream-ordered HIP kernels; the collectives stay with the caller
+ * (torch.distributed / RCCL), so the drop-in Python hooks in
+ * allreducetopk_amd/comm_hooks/ call, per bucket:
+ *
+ *     arctopk_encode  -> all_reduce(sketch) -> arctopk_select -> arctopk_pack
+ *                     -> all_reduce(packed) -> arctopk_decode
+ *
+ * Conventions.
+ *  - Every entry point returns 0 on success or a nonzero status (a hipError_t
+ *    value, or one of the ARCTOPK_E* codes below).  Nothing throws across the ABI.
+ *  - Device pointers are plain element pointers into device memory; `stream` is
+ *    a hipStream_t passed as void*.  Compute entry points only enqueue work on
+ *    `stream`: no host synchronisation, no allocation (graph-capturable).
+ *  - A plan owns its device tables and a select workspace; calls that share a
+ *    plan must be ordered on one stream.
+ *  - Element type: ARCTOPK_F32 (the bucket dtype of every BASELINE config).
+ */
+#ifndef ARCTOPK_H
+#define ARCTOPK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes besides hipError_t */
+#define ARCTOPK_OK 0
+#define ARCTOPK_EINVAL 1001     /* bad argument (null pointer, ratio out of (0,1], r out of range) */
+#define ARCTOPK_ERESHAPE 1002   /* ND tensor numel not divisible by m = 2*t^2 (ref :76 raises) */
+#define ARCTOPK_EDTYPE 1003     /* unsupported element type */
+#define ARCTOPK_EEMPTY 1004     /* empty tensor: torch.topk(k=1) on 0 elements raises */
+
+/* error-feedback modes (ref GroupTopKState.use_error_feedback, :149, :224-250) */
+#define ARCTOPK_EF_NONE 0
+#define ARCTOPK_EF14 1
+#define ARCTOPK_EF21 2
+
+/* element types */
+#define ARCTOPK_F32 0
+
+/* segment kinds */
+#define ARCTOPK_SEG_RAW 0     /* 1-D tensor: the "sketch" is the tensor itself (ref :19-41) */
+#define ARCTOPK_SEG_SKETCH 1  /* 2-D [n,m] or ND reshaped to [d/m, m], m = 2*t^2 (ref :44-102) */
+
+typedef struct arctopk_plan arctopk_plan;
+
+/* Totals of a plan, for sizing the caller's buffers. */
+typedef struct {
+    int64_t numel;       /* bucket elements (bucket.buffer().numel())                  */
+    int64_t sketch_len;  /* floats of the concatenated sketch: sum n*r (SKETCH) + d (RAW) */
+    int64_t v_len;       /* floats of the concatenated projections: sum m*r over SKETCH   */
+    int64_t packed_len;  /* sum_k: selected elements (ref values_memory length, :261-263)  */
+    int64_t sel_rows;    /* sum of selected rows (length of the row list)                 */
+    int64_t rows_total;  /* sum n (length of the slot map)                                */
+    int32_t nseg;        /* gradient views in the bucket                                  */
+    int32_t r;           /* sketch rank                                                   */
+} arctopk_plan_info;
+
+/* Per-segment geometry (for the host-side mirror and tests). */
+typedef struct {
+    int64_t offset;      /* element offset in the bucket                 */
+    int64_t n, m;        /* rows, columns (m = 1 for RAW)                 */
+    int64_t k_rows;      /* selected rows: max(1, int(n * ratio))  (ref cal_k :173-187) */
+    int64_t sketch_off;  /* float offset in the sketch buffer            */
+    int64_t v_off;       /* float offset in the projection buffer (-1: RAW) */
+    int64_t packed_off;  /* element offset in the packed buffer          */
+    int64_t row_off;     /* offset in the slot map (global row index)    */
+    int64_t sel_off;     /* offset in the selected-row list              */
+    int32_t kind;        /* ARCTOPK_SEG_RAW / ARCTOPK_SEG_SKETCH          */
+    int32_t pad;
+} arctopk_segment;
+
+/*
+ * Build the plan of one bucket layout.  `dims` holds the shapes of
+ * bucket.gradients() concatenated, `ndims[i]` the rank of tensor i.  Geometry and
+ * k follow the reference: 1-D -> RAW; 2-D -> [shape0, shape1]; ND -> [d/m, m]
+ * with m = 2*shape[-1]^2 (group_topk_hook_no_reshape.py:16-102, cal_k :173-187).
+ * Replaces: the per-call Python loop over bucket.gradients() (:111-129, :259).
+ */
+int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, int32_t ntensors, int32_t r,
+                        double compress_ratio, int32_t dtype, int32_t device, arctopk_plan** out);
+int arctopk_plan_destroy(arctopk_plan* plan);
+/* Host-only: the geometry a plan would have (no device memory touched); segs_out may be NULL. */
+int arctopk_plan_describe(const int64_t* dims, const int32_t* ndims, int32_t ntensors, int32_t r,
+                          double compress_ratio, arctopk_segment* segs_out, arctopk_plan_info* info);
+int arctopk_plan_query(const arctopk_plan* plan, arctopk_plan_info* info);
+int arctopk_plan_segment(const arctopk_plan* plan, int32_t i, arctopk_segment* seg);
+
+/*
+ * K1 encode.  EF pre-apply fused with the rank-r sketch of every tensor.
+ *   ef = NONE : X = G
+ *   ef = EF14 : X = G + E (err_in = 1) or X = G (first call, err_in = 0); writes E := X
+ *   ef = EF21 : X = G - E (nothing written but the sketch)
+ * sketch[SKETCH seg] = X.view(n,m) @ V  ([n][r] row-major); sketch[RAW seg] = X.
+ * `V` is the concatenation of each SKETCH tensor's [m][r] projection in bucket order.
+ * Replaces: input_tensor.add_(error, alpha=+-1) (:227, :234), tensor @ V (:53, :83),
+ *           P = P_local.clone() (:31, :56, :86).
+ */
+int arctopk_encode(const arctopk_plan* plan, const float* grad, float* err, int32_t ef,
+                   int32_t err_in, const float* V, float* sketch, void* stream);
+
+/*
+ * K2 select.  From the all-reduced sketch: P /= world_size, row energy
+ * sum_j P[row][j]^2 (sequential j, as torch.sum over dim 1 for r <= 4) or P^2
+ * (RAW), top-k_rows rows per segment.  Ties at the k-th energy: lowest rows
+ * first.  Writes the selected rows ascending (rowlist[sel_off ..]) and, for every
+ * row, its packed slot or -1 (slotmap[row_off + row]).
+ * Replaces: P /= ws; norms = sum(P**2, 1); torch.topk(norms, k, sorted=False);
+ *           row*m + arange(m) index materialisation (:34-38, :59-66, :89-96).
+ */
+int arctopk_select(const arctopk_plan* plan, const float* sketch, int32_t world_size,
+                   int32_t* rowlist, int32_t* slotmap, void* stream);
+
+/*
+ * K2 variant for tests/bit-exact checks: the per-row energy keys only
+ * (float bits of the energy the reference feeds torch.topk), keys[row_off + row].
+ */
+int arctopk_row_energy(const arctopk_plan* plan, const float* sketch, int32_t world_size,
+                       float* energy, void* stream);
+
+/*
+ * K3 pack.  Gather the selected rows into the packed buffer (segment order,
+ * ascending rows) and update the local residual:
+ *   NONE : packed = G[sel]
+ *   EF14 : packed = E[sel] (E holds X after encode); E[sel] = 0
+ *   EF21 : D = G[sel] - E[sel]; packed = D; E[sel] = E[sel] + D
+ * Replaces: tensor[topk_indices] gathers (:70-71, :101-102), values_memory /
+ * indices_memory packing (:116-117), EF14 tensor.view(-1)[indices] = 0 (:124),
+ * EF21 zero_/index_put (:126-128) and the residual persistence (:270-275).
+ */
+int arctopk_pack(const arctopk_plan* plan, const float* grad, float* err, int32_t ef,
+                 const int32_t* rowlist, float* packed, void* stream);
+
+/*
+ * K4 decode.  From the all-reduced packed values:
+ *   NONE/EF14 : out = scatter(packed / world_size) into zeros
+ *   EF21      : out = gE + scatter(packed / world_size); gE[sel] = out[sel]
+ * `out` may alias the bucket (it is the bucket in the hook).
+ * Replaces: values_memory.div_(ws) (:281), input_tensor.zero_() (:284), the
+ * per-tensor index_put scatter (:131-141) and gE.add_/input.copy_ (:288-290).
+ */
+int arctopk_decode(const arctopk_plan* plan, const float* packed, const int32_t* slotmap,
+                   int32_t world_size, int32_t ef, float* gerr, float* out, void* stream);
+
+/* ---- TopK / RandK baselines (comm_hooks/sparse_hook.py, sparse_hook_c4.py) ---------- */
+/*
+ * Tensors of a bucket are described by host arrays of `ntensors` entries:
+ * offsets[i] (element offset in the bucket), numels[i], ks[i] (= max(1, int(numel*ratio)),
+ * sparse_hook.py:77-78) and k_off[i] (offset of tensor i's k entries in the packed
+ * idx/vals buffers).  Up to ARCTOPK_SPARSE_MAX_BATCH tensors go into one launch; more
+ * are processed in batches.
+ */
+#define ARCTOPK_SPARSE_MAX_BATCH 64
+
+/* bytes of `workspace` that arctopk_topk_select needs (independent of the tensors) */
+int64_t arctopk_sparse_workspace_bytes(void);
+
+/*
+ * Exact element top-k of |x| per tensor by multi-block radix select; ties at the
+ * k-th |x|: lowest index first.  Writes each tensor's k indices ascending as int32
+ * (idx[k_off[i] ..]) and the values x[idx] (vals[k_off[i] ..]).
+ * Replaces: torch.topk(tensor.abs(), k, sorted=False), .to(int32), tensor[indices]
+ * (sparse_hook.py:26-28, :97-98).
+ */
+int arctopk_topk_select(const float* x, int32_t ntensors, const int64_t* offsets,
+                        const int64_t* numels, const int64_t* ks, const int64_t* k_off,
+                        int32_t* idx, float* vals, void* workspace, void* stream);
+
+/*
+ * RandK index source, device-side: idx[k_off[i] + j] = pi_i(j) for j < k, where pi_i is
+ * a keyed pseudo-random permutation of [0, numel_i) (4-round Feistel network with cycle
+ * walking, keyed by (seed, i)).  The k indices are distinct.  This is the performance
+ * mode; the parity mode draws torch.randperm on the host (sparse_hook.py:20).
+ */
+int arctopk_randk_indices(int32_t ntensors, const int64_t* numels, const int64_t* ks,
+                          const int64_t* k_off, uint64_t seed, int32_t* idx, void* stream);
+
+/* Gather vals[k_off[i] + j] = x[offsets[i] + idx[k_off[i] + j]]  (sparse_hook.py:22). */
+int arctopk_sparse_gather(const float* x, int32_t ntensors, const int64_t* offsets,
+                          const int64_t* ks, const int64_t* k_off, const int32_t* idx,
+                          float* vals, void* stream);
+
+/*
+ * Residual persistence at the selected entries (sparse_hook.py:103-109, :257-267):
+ *   EF14 : E[off + idx] = 0        (E already holds x = G + E_prev, see arctopk_ef_apply)
+ *   EF21 : E[off + idx] += vals    (E_new = E + C(G - E); C(.) is zero elsewhere)
+ */
+int arctopk_sparse_residual(float* E, int32_t ntensors, const int64_t* offsets,
+                            const int64_t* ks, const int64_t* k_off, const int32_t* idx,
+                            const float* vals, int32_t ef, void* stream);
+
+/*
+ * Decode into `out` (every element written):
+ *   accumulate = 0 (RandK): out = 0; out[off + idx[j]] = vals[j] / world_size     (:273-278)
+ *   accumulate = 1 (TopK) : out = 0; for rank q = 0..nranks-1 in order:
+ *                           out[off + idx_q[j]] += vals_q[j]; then out /= world_size (:285-292)
+ * `vals`/`idx` hold nranks consecutive payloads of packed_len entries each.
+ * EF21 (gerr != NULL): gE += out; out = gE (:295-297).
+ */
+int arctopk_sparse_decode(float* out, int64_t numel, int32_t ntensors, const int64_t* offsets,
+                          const int64_t* ks, const int64_t* k_off, int64_t packed_len,
+                          const int32_t* idx, const float* vals, int32_t nranks,
+                          int32_t world_size, int32_t accumulate, float* gerr, void* stream);
+
+/*
+ * EF pre-apply on a whole bucket, one pass (ARC-TopK fuses this into arctopk_encode):
+ *   EF14 : x = x + E (err_in = 1) or x unchanged (first call); then E = x
+ *   EF21 : x = x - E
+ * Replaces: input_tensor.add_(error_dict[b], alpha=+-1) (sparse_hook.py:205, :212) and the
+ * full-bucket E.copy_(input_tensor) of EF14 (:258).
+ */
+int arctopk_ef_apply(float* x, float* E, int64_t numel, int32_t ef, int32_t err_in, void* stream);
+
+/* library build identification (for smoke tests) */
+const char* arctopk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ARCTOPK_H */

@@ -254,12 +254,14 @@ def oracle_group_topk_hook(state: OracleState, bucket, group=None) -> torch.Tens
 
 
 def simulate_step(Gs: List[torch.Tensor], Es: List[Optional[torch.Tensor]], gE: Optional[torch.Tensor],
-                  shapes, ratio: float, r: int, ef: str, seed: int):
+                  shapes, ratio: float, r: int, ef: str, seed: int, rows_override=None):
     """One steady-state compressed call on ``len(Gs)`` ranks in one process.
 
     Collectives are sums in rank order.  Returns a dict of intermediates and
     per-rank results: V, P_local, P_sum, norms, rows, X (post-pack bucket
-    contents), values, out, E_new, gE_new.
+    contents), values, out, E_new, gE_new.  ``rows_override`` (list of row index
+    tensors per segment) replaces the top-k choice -- used to compare a device
+    run's outputs bit for bit given the rows that run selected.
     """
     ws = len(Gs)
     segs = segments(shapes, ratio)
@@ -276,6 +278,8 @@ def simulate_step(Gs: List[torch.Tensor], Es: List[Optional[torch.Tensor]], gE: 
             acc = acc + Pls[q][j]
         P_sum.append(acc)
     norms, rows = select(P_sum, ws, segs)
+    if rows_override is not None:
+        rows = [torch.as_tensor(x, dtype=torch.int64) for x in rows_override]
     vals = [pack(X, rows, segs, ef) for X in Xs]
     vsum = vals[0].clone()
     for q in range(1, ws):

@@ -63,16 +63,23 @@ def encode(G, E, ef):
     return X
 
 
-def pack(X: torch.Tensor, shapes, ratio: float, ef: str, random: bool, seed: Optional[int]):
-    """Returns (values, indices int32, k_list, bits_sum); mutates X per EF mode."""
-    g = torch.Generator().manual_seed(int(seed)) if random else None
+def pack(X: torch.Tensor, shapes, ratio: float, ef: str, random: bool, seed: Optional[int],
+         indices_override=None):
+    """Returns (values, indices int32, k_list, bits_sum); mutates X per EF mode.
+
+    ``indices_override`` (one index tensor per tensor) replaces the index draw.
+    """
+    g = torch.Generator().manual_seed(int(seed)) if (random and indices_override is None) else None
     vals, idxs, ks, bits = [], [], [], 0
     off = 0
     for s in shapes:
         n = numel_of(s)
         v = X[off:off + n]
         k = cal_k(n, ratio)
-        idx = randk_indices(n, k, g) if random else topk_indices(v, k)
+        if indices_override is not None:
+            idx = torch.as_tensor(indices_override[len(ks)]).to(torch.int32)
+        else:
+            idx = randk_indices(n, k, g) if random else topk_indices(v, k)
         val = v[idx.long()].clone()
         vals.append(val)
         idxs.append(idx)
@@ -115,13 +122,19 @@ def decode_topk(all_vals: List[torch.Tensor], all_idx: List[torch.Tensor], shape
     return out
 
 
-def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed: Optional[int]):
-    """One steady-state compressed call on len(Gs) ranks in one process."""
+def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed: Optional[int],
+                  indices_override=None):
+    """One steady-state compressed call on len(Gs) ranks in one process.
+
+    ``indices_override``: per rank, a list of per-tensor index tensors (RandK draws
+    made elsewhere, e.g. by the device generator).
+    """
     ws = len(Gs)
     Xs, packs = [], []
-    for G, E in zip(Gs, Es):
+    for q, (G, E) in enumerate(zip(Gs, Es)):
         X = encode(G, E, ef)
-        packs.append(pack(X, shapes, ratio, ef, random, seed))
+        ov = indices_override[q] if indices_override is not None else None
+        packs.append(pack(X, shapes, ratio, ef, random, seed, ov))
         Xs.append(X)
     ks = packs[0][2]
     numel = Gs[0].numel()

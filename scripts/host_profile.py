@@ -1,0 +1,59 @@
+"""Host-side cost of one ARC-TopK hook call (cProfile + loop timings). GPU box only."""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel  # noqa: E402
+from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import GroupTopKState, group_topk_hook  # noqa: E402
+
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+os.environ.setdefault("MASTER_PORT", "29511")
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+shapes = [[2048, 2048]] * 16
+buf = torch.randn(bucket_numel(shapes), device="cuda:0")
+b = SyntheticBucket(buf, shapes)
+st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback="ef14", seed=1)
+for _ in range(5):
+    group_topk_hook(st, b)
+torch.cuda.synchronize()
+
+
+def loop(n):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        group_topk_hook(st, b)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    return (t1 - t0) / n * 1e6, (t2 - t0) / n * 1e6
+
+
+print("no events: host enqueue %.1f us/step, wall %.1f us/step" % loop(50))
+st.phase_events = []
+print("events   : host enqueue %.1f us/step, wall %.1f us/step" % loop(50))
+st.phase_events = None
+print("proj hits/misses", st._proj.hits, st._proj.misses)
+# components
+t = time.perf_counter()
+for _ in range(200):
+    torch.manual_seed(123)
+print("torch.manual_seed %.1f us" % ((time.perf_counter() - t) / 200 * 1e6))
+x = torch.empty(1, device="cuda:0")
+t = time.perf_counter()
+for _ in range(200):
+    dist.all_reduce(x)
+torch.cuda.synchronize()
+print("dist.all_reduce(1 elem) %.1f us" % ((time.perf_counter() - t) / 200 * 1e6))
+pr = cProfile.Profile()
+pr.enable()
+loop(50)
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+dist.destroy_process_group()

@@ -1,0 +1,254 @@
+"""ARC-TopK HIP path vs the CPU oracle, on an MI355X (run with -m gpu).
+
+Parity bar (BASELINE north_star): selected rows identical to the reference's
+(exactly, when the select kernel is fed the oracle's sketch; modulo sketch
+rounding at the k-th energy end to end), and every output / residual
+bit-identical given the selected rows (the codec only copies, adds and
+divides fp32 values in the reference's order).  The sketch itself (G @ V, a
+2048-term fp32 dot product) is compared to torch CPU mm within 2e-5 relative.
+"""
+import pytest
+import torch
+
+from allreducetopk_amd import _native as N
+from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
+from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import (BucketPlan, GroupTopKState,
+                                                                      group_topk_hook)
+from golden_io import Golden, case_names
+from oracle import arctopk as A
+from parity import (assert_bitwise, assert_close_rel, check_rows_tie_aware, ensure_group)
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+MIX = [[10], [40, 16], [4, 3, 3, 3], [16, 8, 3, 3], [16, 8, 1, 1], [96, 40], [7], [256, 512],
+       [33, 130], [1000], [64, 70], [8, 8, 5, 5], [130, 2048]]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def group():
+    ensure_group("nccl")
+    yield
+
+
+def _rand_bucket(shapes, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(bucket_numel(shapes), generator=g)
+
+
+def _gpu_rows(plan: BucketPlan):
+    rl = plan.rowlist.cpu()
+    out = []
+    for s in plan.segments:
+        out.append(rl[s.sel_off:s.sel_off + s.k_rows].long())
+    return out
+
+
+def test_plan_geometry_matches_oracle():
+    plan = BucketPlan([tuple(s) for s in MIX], 4, 0.2, torch.float32, DEV)
+    segs = A.segments(MIX, 0.2)
+    for s, o in zip(plan.segments, segs):
+        assert (s.offset, s.n, s.m, s.k_rows) == (o.offset, o.n, o.m, o.k_rows)
+    assert plan.info.packed_len == sum(o.k for o in segs)
+
+
+@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
+def test_kernel_phases_bitexact(ef):
+    """encode -> select (fed the oracle's sketch) -> pack -> decode, phase by phase."""
+    shapes = MIX
+    segs = A.segments(shapes, 0.2)
+    plan = BucketPlan([tuple(s) for s in shapes], 4, 0.2, torch.float32, DEV)
+    G = _rand_bucket(shapes, 1)
+    E = _rand_bucket(shapes, 2) * 0.5 if ef != "noef" else None
+    gE = _rand_bucket(shapes, 3) if ef == "ef21" else None
+    seed = 987654
+    Vs = A.draw_projections(seed, segs, 4)
+    X, Ps = A.encode(G, E, ef, segs, Vs)
+    # --- encode
+    Vflat = torch.cat([v.flatten() for v in Vs if v is not None]).to(DEV)
+    g_d = G.to(DEV)
+    e_d = E.to(DEV) if E is not None else None
+    stream = torch.cuda.current_stream().cuda_stream
+    plan.encode(g_d, e_d, N.EF_CODE[ef], True, Vflat, stream)
+    torch.cuda.synchronize()
+    sk = plan.sketch_view.cpu()
+    for s, P in zip(plan.segments, Ps):
+        n = P.numel()
+        got = sk[s.sketch_off:s.sketch_off + n].view_as(P)
+        if s.kind == N.SEG_RAW:
+            assert_bitwise(got, P, f"RAW sketch seg@{s.offset}")
+        else:
+            assert_close_rel(got, P, 2e-5, f"sketch seg@{s.offset} m={s.m}")
+    if ef == "ef14":
+        assert_bitwise(e_d, X, "E := G + E after encode")
+    # --- select on the oracle's sketch: bit-exact energies and the exact tie rule
+    ref_sketch = torch.cat([p.flatten() for p in Ps])
+    plan.sketch[:ref_sketch.numel()].copy_(ref_sketch.to(DEV))
+    energy = torch.empty(plan.info.rows_total, device=DEV)
+    plan.row_energy(1, energy, stream)
+    plan.select(1, stream)
+    torch.cuda.synchronize()
+    norms, _ = A.select(Ps, 1, segs)
+    en = energy.cpu()
+    for s, nrm in zip(plan.segments, norms):
+        assert_bitwise(en[s.row_off:s.row_off + s.n], nrm, f"energy seg@{s.offset}")
+    rows = _gpu_rows(plan)
+    for r_, nrm, s in zip(rows, norms, plan.segments):
+        diff = check_rows_tie_aware(r_, nrm, int(s.k_rows), band=0.0)
+        assert diff == 0
+        assert torch.all(r_[1:] > r_[:-1]), "row list must be ascending"
+    sm = plan.slotmap.cpu()
+    for s, r_ in zip(plan.segments, rows):
+        slots = sm[s.row_off:s.row_off + s.n]
+        assert int((slots >= 0).sum()) == s.k_rows
+        assert torch.equal(slots[r_], torch.arange(s.k_rows, dtype=torch.int32))
+    # --- pack (rows ascending) and residual
+    Xo = X.clone()
+    vals = A.pack(Xo, rows, segs, ef)
+    plan.pack(g_d, e_d, N.EF_CODE[ef], stream)
+    torch.cuda.synchronize()
+    assert_bitwise(plan.packed_view, vals, "packed values")
+    if ef == "ef14":
+        assert_bitwise(e_d, Xo, "EF14 residual")
+    elif ef == "ef21":
+        assert_bitwise(e_d, E + Xo, "EF21 residual")
+    # --- decode
+    out = torch.empty_like(g_d)
+    ge_d = gE.to(DEV) if gE is not None else None
+    plan.decode(1, N.EF_CODE[ef], ge_d, out, stream)
+    torch.cuda.synchronize()
+    ref_out = A.decode(vals, 1, rows, segs, G.numel(), G.dtype)
+    if ef == "ef21":
+        ref_out = gE + ref_out
+        sel_mask = torch.zeros(G.numel(), dtype=torch.bool)
+        for s, r_ in zip(segs, rows):
+            sel_mask[s.offset:s.offset + s.numel].view(s.n, s.m)[r_] = True
+        assert_bitwise(ge_d.cpu()[sel_mask], ref_out[sel_mask], "gE (selected rows)")
+        assert_bitwise(ge_d.cpu()[~sel_mask], gE[~sel_mask], "gE (untouched rows)")
+    assert_bitwise(out, ref_out, "decoded bucket")
+
+
+@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
+def test_hook_end_to_end_vs_oracle(ef):
+    shapes = MIX
+    numel = bucket_numel(shapes)
+    st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                        use_error_feedback=ef, seed=1234)
+    ost = A.OracleState(r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback=ef,
+                        seed=1234)
+    E = gE = None
+    flips = 0
+    for it in range(4):
+        G = _rand_bucket(shapes, 100 + it)
+        bucket = SyntheticBucket(G.to(DEV), shapes, index=0, is_last=True)
+        out = group_topk_hook(st, bucket).wait()
+        torch.cuda.synchronize()
+        if ef == "ef21" and E is None:  # init call
+            E, gE = G.clone(), G.clone()
+            assert_bitwise(out, G, "EF21 init out")
+            continue
+        seed = ost.next_seed()
+        plan = st._plans[0][1]
+        rows = _gpu_rows(plan)
+        first_ef14 = (ef == "ef14" and E is None)
+        res = A.simulate_step([G], [None if first_ef14 else E], gE, shapes, 0.2, 4, ef, seed,
+                              rows_override=rows)
+        for r_, nrm, s in zip(rows, res["norms"], plan.segments):
+            flips += check_rows_tie_aware(r_, nrm, int(s.k_rows), band=2e-4)
+        assert_bitwise(out, res["out"], f"it{it} output bucket")
+        if ef in ("ef14", "ef21"):
+            assert_bitwise(st.error_dict[0], res["E_new"][0], f"it{it} E")
+            E = res["E_new"][0]
+        if ef == "ef21":
+            assert torch.equal(st.global_error_dict[0].cpu(), res["gE_new"])
+            gE = res["gE_new"]
+        assert st.iter == it + 1
+    assert flips <= 2, f"{flips} rows differ from the oracle's selection (near-ties only)"
+    assert numel == bucket.buffer().numel()
+
+
+@pytest.mark.parametrize("name", [n for n in case_names("arc_") if n.endswith("ws1")])
+def test_golden_vectors_on_gpu(name):
+    """Replay reference-generated golden vectors through the HIP hook."""
+    g = Golden(name)
+    m = g.meta
+    shapes = [tuple(s) for s in m["shapes"]]
+    st = GroupTopKState(None, r=m["r"], compress_ratio=m["ratio"],
+                        start_compress_iter=m["start"], use_error_feedback=m["ef"], seed=m["seed"])
+    for it in range(m["iters"]):
+        G = g.t(0, it, "G")
+        bucket = SyntheticBucket(G.to(DEV), shapes, index=0, is_last=True)
+        out = group_topk_hook(st, bucket).wait()
+        torch.cuda.synchronize()
+        ties = m.get("ties", False)
+        if g.has(0, it, "topk0_in") and not ties:
+            plan = st._plans[0][1]
+            for j, r_ in enumerate(_gpu_rows(plan)):
+                ref = g.t(0, it, f"topk{j}_idx")
+                assert sorted(r_.tolist()) == sorted(ref.tolist()), f"{name} it{it} seg{j} rows"
+        if ties and g.has(0, it, "topk0_in"):
+            plan = st._plans[0][1]
+            for j, r_ in enumerate(_gpu_rows(plan)):
+                check_rows_tie_aware(r_, g.t(0, it, f"topk{j}_in"), int(g.np(0, it, f"topk{j}_k")))
+            # zero-energy ties select all-zero rows: outputs agree regardless of which
+        assert_bitwise(out, g.t(0, it, "out"), f"{name} it{it} out")
+        if g.has(0, it, "E"):
+            assert_bitwise(st.error_dict[0], g.t(0, it, "E"), f"{name} it{it} E")
+        if g.has(0, it, "gE"):
+            assert_bitwise(st.global_error_dict[0], g.t(0, it, "gE"), f"{name} it{it} gE")
+        assert st.comm_bits_this_round == int(g.np(0, it, "bits"))
+
+
+@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
+def test_headline_bucket_properties(ef):
+    """16 x [2048, 2048] fp32 (256 MiB): size-independent invariants at full size."""
+    shapes = [[2048, 2048]] * 16
+    numel = bucket_numel(shapes)
+    torch.manual_seed(0)
+    G0 = torch.randn(numel, device=DEV)
+    st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                        use_error_feedback=ef, seed=1234)
+    bucket = SyntheticBucket(G0.clone(), shapes)
+    group_topk_hook(st, bucket).wait()  # EF21: init call
+    G1 = torch.randn(numel, device=DEV)
+    E_before = st.error_dict[0].clone() if ef != "noef" else None
+    gE_before = st.global_error_dict[0].clone() if ef == "ef21" else None
+    bucket = SyntheticBucket(G1.clone(), shapes)
+    out = group_topk_hook(st, bucket).wait()
+    torch.cuda.synchronize()
+    plan = st._plans[0][1]
+    k_rows = plan.segments[0].k_rows
+    assert k_rows == 409 and plan.info.packed_len == 13_402_112
+    rows = _gpu_rows(plan)
+    energy = torch.empty(plan.info.rows_total, device=DEV)
+    plan.row_energy(1, energy, torch.cuda.current_stream().cuda_stream)
+    en = energy.cpu()
+    sel = torch.zeros(numel // 2048, dtype=torch.bool)
+    for s, r_ in zip(plan.segments, rows):
+        e = en[s.row_off:s.row_off + s.n]
+        mask = torch.zeros(s.n, dtype=torch.bool)
+        mask[r_] = True
+        assert e[mask].min() >= e[~mask].max(), "a dropped row outranks a selected one"
+        sel[s.row_off:s.row_off + s.n] = mask
+    out2 = out.view(-1, 2048)
+    X = G1 if ef == "noef" else (G1 + E_before if ef == "ef14" else G1 - E_before)
+    X2 = X.view(-1, 2048)
+    selc = sel.to(DEV)
+    if ef in ("noef", "ef14"):
+        assert torch.equal(out2[~selc], torch.zeros_like(out2[~selc]))
+        assert torch.equal(out2[selc], X2[selc])  # ws = 1: the mean is the row itself
+    if ef == "ef14":  # conservation: out + E_new == G + E_old, bit for bit
+        assert torch.equal(out + st.error_dict[0], X)
+    if ef == "ef21":
+        E2 = st.error_dict[0].view(-1, 2048)
+        assert torch.equal(E2[~selc], E_before.view(-1, 2048)[~selc])
+        assert torch.equal(E2[selc], (E_before.view(-1, 2048) + X2)[selc])
+        assert torch.equal(out2[selc], (gE_before.view(-1, 2048) + X2)[selc])
+        assert torch.equal(out2[~selc], gE_before.view(-1, 2048)[~selc])
+
+
+def test_encode_rejects_bad_layout():
+    buf = torch.zeros(100, device=DEV)
+    st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0)
+    with pytest.raises(RuntimeError):
+        group_topk_hook(st, SyntheticBucket(buf, [[3, 5, 2], [70]]))  # 30 % 8 != 0

@@ -1,0 +1,164 @@
+"""TopK / RandK HIP path vs the CPU oracle and the reference's golden vectors (MI355X)."""
+import pytest
+import torch
+
+from allreducetopk_amd import _native as N
+from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
+from allreducetopk_amd.comm_hooks import sparse_hook, sparse_hook_c4
+from golden_io import Golden, case_names
+from oracle import sparse as S
+from parity import assert_bitwise, check_rows_tie_aware, ensure_group
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SHAPES = [[10], [40, 16], [4, 3, 3, 3], [96, 40], [256, 512], [1000], [3, 7]]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def group():
+    ensure_group("nccl")
+    yield
+
+
+def _rand(shapes, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(bucket_numel(shapes), generator=g)
+
+
+@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
+def test_topk_hook_vs_oracle(ef):
+    st = sparse_hook.SparseState(None, compress_ratio=0.2, start_compress_iter=0,
+                                 sparse_type="tensor", random=False, use_error_feedback=ef)
+    E = gE = None
+    for it in range(3):
+        G = _rand(SHAPES, 50 + it)
+        out = sparse_hook.sparse_hook_sync(st, SyntheticBucket(G.to(DEV), SHAPES)).wait()
+        torch.cuda.synchronize()
+        if ef == "ef21" and E is None:
+            E, gE = G.clone(), G.clone()
+            continue
+        res = S.simulate_step([G], [E if not (ef == "ef14" and E is None) else None], gE, SHAPES,
+                              0.2, ef, False, None)
+        assert_bitwise(out, res["out"], f"it{it} out")
+        if ef != "noef":
+            assert_bitwise(st.error_dict[0], res["E_new"][0], f"it{it} E")
+            E = res["E_new"][0]
+        if ef == "ef21":
+            assert_bitwise(st.global_error_dict[0], res["gE_new"], f"it{it} gE")
+            gE = res["gE_new"]
+
+
+def test_topk_select_kernel_ties_and_order():
+    """Exact tie rule (lowest index first) and ascending output on a tie-heavy tensor."""
+    L = N.lib()
+    n = 100_000
+    x = torch.zeros(n)
+    g = torch.Generator().manual_seed(3)
+    nz = torch.randperm(n, generator=g)[:30_000]
+    x[nz] = torch.randn(30_000, generator=g)
+    x[nz[:500]] = 2.5          # a large block of exact |x| ties
+    x[nz[500:1000]] = -2.5
+    k = 20_000
+    xd = x.to(DEV)
+    idx = torch.empty(k, dtype=torch.int32, device=DEV)
+    vals = torch.empty(k, device=DEV)
+    ws = torch.empty(int(L.arctopk_sparse_workspace_bytes()), dtype=torch.uint8, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    N.check(L.arctopk_topk_select(xd.data_ptr(), 1, N.i64_array([0]), N.i64_array([n]),
+                                  N.i64_array([k]), N.i64_array([0]), idx.data_ptr(),
+                                  vals.data_ptr(), ws.data_ptr(), st), "topk_select")
+    torch.cuda.synchronize()
+    i = idx.cpu().long()
+    assert torch.all(i[1:] > i[:-1])
+    assert torch.equal(vals.cpu(), x[i])
+    check_rows_tie_aware(i, x.abs(), k, band=0.0)
+    # zero ties: k beyond the non-zeros selects the lowest-index zeros
+    k2 = 40_000
+    idx2 = torch.empty(k2, dtype=torch.int32, device=DEV)
+    vals2 = torch.empty(k2, device=DEV)
+    N.check(L.arctopk_topk_select(xd.data_ptr(), 1, N.i64_array([0]), N.i64_array([n]),
+                                  N.i64_array([k2]), N.i64_array([0]), idx2.data_ptr(),
+                                  vals2.data_ptr(), ws.data_ptr(), st), "topk_select")
+    torch.cuda.synchronize()
+    assert check_rows_tie_aware(idx2.cpu(), x.abs(), k2, band=0.0) == 0
+
+
+@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
+@pytest.mark.parametrize("source", ["torch", "hash"])
+def test_randk_hook_vs_oracle(ef, source):
+    st = sparse_hook.SparseState(None, compress_ratio=0.2, start_compress_iter=0,
+                                 sparse_type="tensor", random=True, use_error_feedback=ef,
+                                 random_seed=9, index_source=source)
+    rng = torch.Generator().manual_seed(9)
+    E = gE = None
+    numels = [int(torch.Size(s).numel()) for s in SHAPES]
+    ks = [max(1, int(n * 0.2)) for n in numels]
+    for it in range(3):
+        G = _rand(SHAPES, 70 + it)
+        out = sparse_hook.sparse_hook_sync(st, SyntheticBucket(G.to(DEV), SHAPES)).wait()
+        torch.cuda.synchronize()
+        if ef == "ef21" and E is None:
+            E, gE = G.clone(), G.clone()
+            continue
+        seed = int(torch.randint(0, 1_000_000_000, (1,), generator=rng).item())
+        if source == "torch":  # the device draw the hook made (deterministic per seed)
+            torch.manual_seed(seed)
+            idx = [torch.randperm(n, device=DEV)[:k].cpu() for n, k in zip(numels, ks)]
+        else:
+            kof = [sum(ks[:i]) for i in range(len(ks))]
+            buf = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
+            N.check(N.lib().arctopk_randk_indices(len(ks), N.i64_array(numels), N.i64_array(ks),
+                                                  N.i64_array(kof), seed, buf.data_ptr(),
+                                                  torch.cuda.current_stream().cuda_stream), "randk")
+            flat = buf.cpu()
+            idx = [flat[o:o + k] for o, k in zip(kof, ks)]
+            for t, n in zip(idx, numels):
+                assert t.min() >= 0 and t.max() < n and torch.unique(t).numel() == t.numel()
+        res = S.simulate_step([G], [E if not (ef == "ef14" and E is None) else None], gE, SHAPES,
+                              0.2, ef, True, None, indices_override=[idx])
+        assert_bitwise(out, res["out"], f"it{it} out")
+        if ef != "noef":
+            assert_bitwise(st.error_dict[0], res["E_new"][0], f"it{it} E")
+            E = res["E_new"][0]
+        if ef == "ef21":
+            gE = res["gE_new"]
+
+
+@pytest.mark.parametrize("name", [n for n in case_names("topk_") if n.endswith("ws1")])
+def test_topk_golden_on_gpu(name):
+    g = Golden(name)
+    m = g.meta
+    mod = sparse_hook_c4 if m["hook"] == "sparse_c4" else sparse_hook
+    st = mod.SparseState(None, compress_ratio=m["ratio"], start_compress_iter=m["start"],
+                         sparse_type="tensor", random=False, use_error_feedback=m["ef"],
+                         random_seed=m["seed"])
+    shapes = [tuple(s) for s in m["shapes"]]
+    for it in range(m["iters"]):
+        out = mod.sparse_hook_sync(st, SyntheticBucket(g.t(0, it, "G").to(DEV), shapes)).wait()
+        torch.cuda.synchronize()
+        assert_bitwise(out, g.t(0, it, "out"), f"{name} it{it} out")
+        if g.has(0, it, "E"):
+            assert_bitwise(st.error_dict[0], g.t(0, it, "E"), f"{name} it{it} E")
+        assert st.comm_bits_this_round == int(g.np(0, it, "bits"))
+
+
+def test_topk_headline_bucket_properties():
+    """16 x [2048, 2048]: |selected| >= |dropped| per tensor, k exact, EF14 conservation."""
+    shapes = [[2048, 2048]] * 16
+    n = bucket_numel(shapes)
+    torch.manual_seed(1)
+    G = torch.randn(n, device=DEV)
+    E0 = torch.randn(n, device=DEV) * 0.1
+    st = sparse_hook.SparseState(None, compress_ratio=0.2, start_compress_iter=0,
+                                 sparse_type="tensor", random=False, use_error_feedback="ef14")
+    st.error_dict[0] = E0.clone()
+    X = G + E0
+    out = sparse_hook.sparse_hook_sync(st, SyntheticBucket(G.clone(), shapes)).wait()
+    torch.cuda.synchronize()
+    assert torch.equal(out + st.error_dict[0], X)
+    nz = (out != 0).view(16, -1)
+    assert torch.all(nz.sum(1) <= 838_860)
+    ax = X.abs().view(16, -1)
+    for t in range(16):
+        sel = (out.view(16, -1)[t] != 0) | ((X.view(16, -1)[t] == 0) & (st.error_dict[0].view(16, -1)[t] == 0))
+        assert ax[t][sel].min() >= ax[t][~sel].max()
