@@ -4,7 +4,6 @@ Mirrors comm_hooks/default_hooks.py of the reference: divide by world size
 first, then an async SUM all-reduce (RCCL on ROCm) whose future yields the
 bucket (:15-35).
 """
-from __future__ import annotations
 
 import torch
 import torch.distributed as dist
@@ -14,7 +13,8 @@ from allreducetopk_amd.comm_hooks.utils import HookState, tensor_bits
 __all__ = ["allreduce_hook", "my_allreduce_hook"]
 
 
-def _allreduce_fut(process_group, tensor: torch.Tensor, hook_state=None):
+def _allreduce_fut(process_group: dist.ProcessGroup, tensor: torch.Tensor,
+                   hook_state=None) -> torch.futures.Future[torch.Tensor]:
     """Average ``tensor`` across the group; returns a Future of it (ref :15-35)."""
     group = process_group if process_group is not None else dist.group.WORLD
     world_size = group.size()
@@ -25,11 +25,13 @@ def _allreduce_fut(process_group, tensor: torch.Tensor, hook_state=None):
         lambda fut: fut.value()[0])
 
 
-def my_allreduce_hook(state: HookState, bucket) -> torch.futures.Future:
+def my_allreduce_hook(state: HookState, bucket: dist.GradBucket
+                      ) -> torch.futures.Future[torch.Tensor]:
     state.maybe_accumulate_momentum_on_bucket(bucket)
     state.maybe_increase_iter(bucket)
     return _allreduce_fut(state.process_group, bucket.buffer(), state)
 
 
-def allreduce_hook(process_group, bucket) -> torch.futures.Future:
+def allreduce_hook(process_group: dist.ProcessGroup, bucket: dist.GradBucket
+                   ) -> torch.futures.Future[torch.Tensor]:
     return _allreduce_fut(process_group, bucket.buffer())

@@ -23,7 +23,6 @@ sketch (the GPU sums G.V in a different order than CPU sgemm); exact ties at
 the k-th energy are resolved lowest-row-first.  The hook returns an already
 completed Future holding the bucket, as the reference does (:294-297).
 """
-from __future__ import annotations
 
 import logging
 from typing import Dict, List, Tuple
@@ -247,7 +246,8 @@ def _check_bucket_layout(buf: torch.Tensor, grads) -> None:
         raise RuntimeError("bucket gradient views do not cover the buffer")
 
 
-def group_topk_hook(state: GroupTopKState, bucket) -> torch.futures.Future:
+def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
+                    ) -> torch.futures.Future[torch.Tensor]:
     state.maybe_accumulate_momentum_on_bucket(bucket)
     group = state.process_group if state.process_group is not None else dist.group.WORLD
     world_size = group.size()

@@ -20,7 +20,6 @@ Only ``sparse_type="tensor"`` works in the reference (row/column unpack 2 values
 where 3 are expected, :54, :75, :96); the same types raise here.
 Ties at the k-th |x| resolve lowest-index first.
 """
-from __future__ import annotations
 
 import logging
 from typing import Dict, List
@@ -89,7 +88,7 @@ def _workspace(state, device) -> torch.Tensor:
     return ws
 
 
-def _sparse_hook_impl(state: SparseState, bucket) -> torch.futures.Future:
+def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch.Tensor]":
     if state.use_error_feedback == "ef21" and state.large_batch_init:
         raise NotImplementedError("large_batch_init EF21 (dead code in the reference, "
                                   "sparse_hook.py:156) is not provided")
@@ -224,7 +223,8 @@ def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group, world_size: in
         torch.cat(parts, out=out)
 
 
-def sparse_hook_sync(state: SparseState, bucket) -> torch.futures.Future:
+def sparse_hook_sync(state: SparseState, bucket: dist.GradBucket
+                     ) -> torch.futures.Future[torch.Tensor]:
     return _sparse_hook_impl(state, bucket)
 
 

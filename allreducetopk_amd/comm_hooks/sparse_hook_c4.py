@@ -7,10 +7,10 @@ Differences from ``sparse_hook`` (reference sparse_hook_c4.py:140-151, :175-189,
 down to ``compress_ratio`` over ``start_compress_iter + warmup_iters`` iterations
 after compression starts, and ``cal_k`` takes ``(state, tensor)``.
 """
-from __future__ import annotations
 
 import logging
 
+import torch
 import torch.distributed as dist
 
 from allreducetopk_amd.comm_hooks import sparse_hook as _base
@@ -60,5 +60,6 @@ def cal_k(state, tensor):
     return max(1, int(tensor.numel() * state.get_current_compress_ratio()))
 
 
-def sparse_hook_sync(state: SparseState, bucket):
+def sparse_hook_sync(state: SparseState, bucket: dist.GradBucket
+                     ) -> torch.futures.Future[torch.Tensor]:
     return _base._sparse_hook_impl(state, bucket)

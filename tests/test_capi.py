@@ -1,0 +1,110 @@
+"""The C-ABI library: loads, exports every entry point include/arctopk.h declares, and
+its host-only geometry (no GPU needed) agrees with the oracle's reading of the
+reference's cal_k / reshape rules (group_topk_hook_no_reshape.py:16-102, :173-187)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from allreducetopk_amd import _native as N
+from allreducetopk_amd.build import LIB, build
+from oracle import arctopk as A
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                      "arctopk.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        build()
+    return N.lib()
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(arctopk_\w+)\s*\(", src,
+                                 flags=re.M)))
+
+
+def test_header_declares_expected_api():
+    names = declared_functions()
+    for must in ("arctopk_plan_create", "arctopk_encode", "arctopk_select", "arctopk_pack",
+                 "arctopk_decode", "arctopk_topk_select", "arctopk_sparse_decode"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert names, "no declarations parsed"
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, f"declared but not exported: {missing}"
+    assert set(names) == set(N.EXPORTS), "ctypes bindings out of sync with include/arctopk.h"
+
+
+def test_version_string(lib):
+    assert b"gfx950" in lib.arctopk_version()
+
+
+def _describe(lib, shapes, r=4, ratio=0.2):
+    dims = [int(d) for s in shapes for d in s]
+    nd = [len(s) for s in shapes]
+    segs = (N.Segment * len(shapes))()
+    info = N.PlanInfo()
+    st = lib.arctopk_plan_describe((ctypes.c_int64 * max(1, len(dims)))(*dims),
+                                   (ctypes.c_int32 * len(nd))(*nd), len(nd), r, ratio,
+                                   ctypes.cast(segs, ctypes.c_void_p), ctypes.byref(info))
+    return st, list(segs), info
+
+
+SHAPE_SETS = [
+    [[2048, 2048]] * 16,
+    [[10], [40, 16], [4, 3, 3, 3], [16, 8, 3, 3], [16, 8, 1, 1], [96, 40], [7]],
+    [[512, 512, 3, 3], [512], [256, 128, 1, 1], [64, 3, 7, 7]],
+    [[32000, 2048], [2048], [5461, 2048], [2048, 5461]],
+    [[1], [3, 1], [5, 4, 2, 2], [2, 1, 1, 1]],
+]
+
+
+@pytest.mark.parametrize("shapes", SHAPE_SETS)
+@pytest.mark.parametrize("ratio", [0.2, 0.08, 0.5, 1.0, 0.001])
+def test_plan_geometry_matches_oracle(lib, shapes, ratio):
+    st, segs, info = _describe(lib, shapes, 4, ratio)
+    assert st == 0
+    ref = A.segments(shapes, ratio)
+    sk = pk = 0
+    for s, o in zip(segs, ref):
+        assert (s.offset, s.n, s.m, s.k_rows) == (o.offset, o.n, o.m, o.k_rows)
+        assert s.kind == o.kind
+        assert s.k_rows * s.m == A.cal_k(o.shape, ratio)
+        assert s.sketch_off == sk and s.packed_off == pk
+        sk += s.n if s.kind == N.SEG_RAW else s.n * 4
+        pk += s.k_rows * s.m
+    assert info.numel == sum(o.numel for o in ref)
+    assert info.packed_len == pk and info.sketch_len == sk
+
+
+def test_plan_errors(lib):
+    assert _describe(lib, [[3, 5, 2]])[0] == 1002       # 30 % (2*2*2) != 0: reshape raises
+    assert _describe(lib, [[4, 0]])[0] == 1004          # empty tensor
+    assert _describe(lib, [[4, 4]], r=0)[0] == 1001
+    assert _describe(lib, [[4, 4]], r=9)[0] == 1001
+    assert _describe(lib, [[4, 4]], ratio=0.0)[0] == 1001
+    assert _describe(lib, [[4, 4]], ratio=1.5)[0] == 1001
+
+
+def test_nd_indivisible_matches_reference_error():
+    with pytest.raises(RuntimeError):
+        A.geometry([3, 5, 2])
+
+
+def test_compute_entry_points_reject_null_without_touching_device(lib):
+    # argument validation happens before any HIP call
+    assert lib.arctopk_encode(None, 0, 0, 0, 1, 0, 0, None) == 1001
+    assert lib.arctopk_select(None, 0, 1, 0, 0, None) == 1001
+    assert lib.arctopk_pack(None, 0, 0, 0, 0, 0, None) == 1001
+    assert lib.arctopk_decode(None, 0, 0, 1, 0, 0, 0, None) == 1001
+    assert lib.arctopk_ef_apply(None, None, 10, 1, 1, None) == 1001
+    assert lib.arctopk_sparse_workspace_bytes() > 0
