@@ -166,6 +166,10 @@ class GroupTopKState(HookState):
         self.phase_events = None
         self.phase_event_every = 1
         self._ev_calls = 0
+        # measurement option (not in the reference): model a NIC-staged exchange by moving
+        # the packed payload device -> pinned host -> device around the all-reduce
+        self.host_staged = False
+        self._host_buf = None
 
     def _plan_for(self, bucket) -> BucketPlan:
         buf = bucket.buffer()
@@ -327,6 +331,15 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     plan.pack(input_tensor, err, ef, sid)
     mark("pack")
     state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum
+    if state.host_staged:  # D2H to a pinned "NIC buffer" and back, stream-ordered
+        pv = plan.packed_view
+        if state._host_buf is None or state._host_buf.numel() < pv.numel():
+            state._host_buf = torch.empty(pv.numel(), dtype=pv.dtype, pin_memory=True)
+        hb = state._host_buf[:pv.numel()]
+        hb.copy_(pv, non_blocking=True)
+        mark("d2h")
+        pv.copy_(hb, non_blocking=True)
+        mark("h2d")
     if world_size > 1:
         dist.all_reduce(plan.packed_view, group=group, async_op=False)
     mark("packed_allreduce")

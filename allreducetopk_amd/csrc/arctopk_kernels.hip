@@ -15,6 +15,17 @@
 
 using namespace arctopk;
 
+#ifdef ARCTOPK_SEL_STAMPS  // diagnostic build only (scripts/seltest.hip): phase timestamps
+__device__ unsigned long long g_sel_stamps[64];
+#define SEL_STAMP(i)                                                        \
+    do {                                                                    \
+        __syncthreads();                                                    \
+        if (threadIdx.x == 0 && blockIdx.x == 0) g_sel_stamps[i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define SEL_STAMP(i) do {} while (0)
+#endif
+
 namespace {
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -263,19 +274,34 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 // ---------------------------------------------------------------------------
 // K2 select
 // ---------------------------------------------------------------------------
+// mean of the all-reduced values: x / ws exactly; for a power-of-two ws the
+// reciprocal is exact and x * (1/ws) rounds the same real number as x / ws.
+struct Scale {
+    float ws, inv;
+    int pow2;
+    __device__ __forceinline__ float operator()(float x) const {
+        return pow2 ? x * inv : __fdiv_rn(x, ws);
+    }
+    __device__ __forceinline__ float4 operator()(float4 x) const {
+        return make_float4((*this)(x.x), (*this)(x.y), (*this)(x.z), (*this)(x.w));
+    }
+};
+
+
 // Energy of a row exactly as the reference forms it on the all-reduced sketch:
 // p_j = P_j / ws (IEEE division, ref `P /= ws`), q_j = p_j * p_j (`P ** 2`), then
 // ((q_0 + q_1) + q_2) + q_3 (torch.sum over dim 1, sequential for r <= 4).
 // __fmul_rn/__fadd_rn keep the compiler from contracting into FMAs.
-__device__ __forceinline__ float row_energy(const float* __restrict__ p, int R, float wsf, int kind) {
+__device__ __forceinline__ float row_energy(const float* __restrict__ p, int R, const Scale& sc,
+                                           int kind) {
     if (kind == ARCTOPK_SEG_RAW) {
-        const float v = __fdiv_rn(p[0], wsf);
+        const float v = sc(p[0]);
         return __fmul_rn(v, v);
     }
-    float a = __fdiv_rn(p[0], wsf);
+    float a = sc(p[0]);
     float s = __fmul_rn(a, a);
     for (int j = 1; j < R; ++j) {
-        const float b = __fdiv_rn(p[j], wsf);
+        const float b = sc(p[j]);
         s = __fadd_rn(s, __fmul_rn(b, b));
     }
     return s;
@@ -290,14 +316,14 @@ __device__ __forceinline__ uint32_t energy_key(float e) {
 }
 
 __global__ void __launch_bounds__(256) k_energy(const SegDev* __restrict__ segs, int nseg,
-                                                const float* __restrict__ sketch, int R, float wsf,
+                                                const float* __restrict__ sketch, int R, Scale sc,
                                                 uint32_t* __restrict__ keys, float* __restrict__ energy) {
     const int si = blockIdx.y;
     const SegDev s = segs[si];
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
     for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < s.n;
          row += (int64_t)gridDim.x * 256) {
-        const float e = row_energy(sketch + s.sketch_off + row * stride, R, wsf, s.kind);
+        const float e = row_energy(sketch + s.sketch_off + row * stride, R, sc, s.kind);
         if (keys) keys[s.row_off + row] = energy_key(e);
         if (energy) energy[s.row_off + row] = e;
     }
@@ -423,111 +449,252 @@ __device__ void select_rows(const KeyT* keys, int64_t n, int64_t k, int32_t* __r
     }
 }
 
-// Radix select without atomics, for keys resident in LDS: 8 passes of 4-bit digits,
-// each digit's count formed by wave ballots (energies of one tensor share their top
-// bits, so per-key LDS atomics would serialise on one or two histogram bins).
-struct SelSharedB {
-    uint32_t cnt[kSelWaves][16];
-    int64_t wsum[kSelWaves];
-    uint32_t digit;
-    int64_t kk;
+// Small segments (n <= kSmallSelRows): one 256-thread block per segment, keys in LDS.
+//  1. energies -> LDS keys; block OR/AND gives the keys' common leading bits, so the
+//     first 8-bit digit covers the most significant *varying* bits (energies of one
+//     tensor share sign/exponent bits; digits on those would pile every key into one
+//     or two histogram bins and serialise the LDS atomics).
+//  2. histogram passes on the varying bits until the bin holding the k-th key has at
+//     most kCandMax keys (usually after one pass);
+//  3. those candidates are ranked exactly by direct comparison -> threshold T and the
+//     number of T-equal keys to take;
+//  4. index-ordered compaction (ties at T: lowest rows first).
+constexpr int kST = 256;
+constexpr int kSTW = kST / 64;
+constexpr int kCandMax = 256;
+
+struct SmallSel {
+    uint32_t hist[256];
+    __attribute__((aligned(16))) uint32_t cand[kCandMax + 4];
+    uint32_t ncand;
+    uint32_t wor[kSTW], wand[kSTW];
+    int64_t wsum[kSTW];
+    uint32_t digit, dcount, T;
+    int64_t kk, need_eq;
 };
 
-__device__ void select_rows_lds(const uint32_t* keys, int n, int64_t k, int32_t* __restrict__ rl,
-                                int32_t* __restrict__ sm, SelSharedB& sh) {
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    uint32_t prefix = 0, mask = 0;
-    int64_t kk = k;
-    for (int shift = 28; shift >= 0; shift -= 4) {
-        uint32_t mycnt = 0;  // lane d < 16 accumulates this wave's count of digit d
-        for (int base = 0; base < n; base += kSelThreads) {
-            const int i = base + tid;
-            const uint32_t key = i < n ? keys[i] : 0u;
-            const bool live = i < n && (key & mask) == prefix;
-            const uint32_t dig = (key >> shift) & 15u;
+__device__ __forceinline__ int64_t block_exscan_s(int64_t v, int64_t* wsum) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t x = v;
 #pragma unroll
-            for (int d = 0; d < 16; ++d) {
-                const uint32_t c = (uint32_t)__popcll(__ballot(live && dig == (uint32_t)d));
-                if (lane == d) mycnt += c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int64_t before = x - v;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    __syncthreads();
+    return before;
+}
+
+__global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__ segs,
+                                                      const int32_t* __restrict__ seg_ids,
+                                                      const float* __restrict__ sketch, int R,
+                                                      Scale sc, int32_t* __restrict__ rowlist,
+                                                      int32_t* __restrict__ slotmap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
+    __shared__ SmallSel sh;
+    const SegDev s = segs[seg_ids[blockIdx.x]];
+    const int n = (int)s.n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
+    const float* sk = sketch + s.sketch_off;
+    SEL_STAMP(0);
+    uint32_t kor = 0u, kand = ~0u;
+    if (R == 4 && s.kind == ARCTOPK_SEG_SKETCH && (s.sketch_off & 3) == 0) {
+        // one float4 per row; 8 rows' loads in flight per thread before any use
+        const float4* p4 = reinterpret_cast<const float4*>(sk);
+        constexpr int B = 8;
+        for (int base = 0; base < n; base += kST * B) {
+            float4 v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) v[u] = p4[min(base + u * kST + tid, n - 1)];
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const int row = base + u * kST + tid;
+                const float a = sc(v[u].x), b = sc(v[u].y), c = sc(v[u].z), d = sc(v[u].w);
+                float e = __fmul_rn(a, a);
+                e = __fadd_rn(e, __fmul_rn(b, b));
+                e = __fadd_rn(e, __fmul_rn(c, c));
+                e = __fadd_rn(e, __fmul_rn(d, d));
+                const uint32_t key = energy_key(e);
+                if (row < n) {
+                    keys[row] = key;
+                    kor |= key;
+                    kand &= key;
+                }
             }
         }
-        if (lane < 16) sh.cnt[wave][lane] = mycnt;
+    } else {
+        for (int row = tid; row < n; row += kST) {
+            const uint32_t key = energy_key(row_energy(sk + (int64_t)row * stride, R, sc, s.kind));
+            keys[row] = key;
+            kor |= key;
+            kand &= key;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 0) {
+        sh.wor[wave] = kor;
+        sh.wand[wave] = kand;
+    }
+    __syncthreads();
+    kor = 0u;
+    kand = ~0u;
+#pragma unroll
+    for (int w = 0; w < kSTW; ++w) {
+        kor |= sh.wor[w];
+        kand &= sh.wand[w];
+    }
+    SEL_STAMP(1);
+    // bits [bit-1 .. 0] still vary among matching keys
+    const uint32_t diff = kor ^ kand;
+    int bit = diff ? 32 - __clz(diff) : 0;
+    uint32_t prefix = kand & ~((bit == 32) ? 0xFFFFFFFFu : ((1u << bit) - 1u));
+    uint32_t mask = (bit == 32) ? 0u : ~((1u << bit) - 1u);
+    int64_t kk = s.k_rows;
+    bool ranked = false;
+    while (bit > 0) {
+        const int w = bit < 8 ? bit : 8;
+        const int shift = bit - w;
+        const uint32_t dmask = (1u << w) - 1u;
+        for (int i = tid; i < 256; i += kST) sh.hist[i] = 0;
         __syncthreads();
-        if (wave == 0) {
-            // lane q (< 16) owns digit 15 - q: descending order for a prefix scan
-            uint32_t c = 0;
-            if (lane < 16) {
+        for (int i = tid; i < n; i += kST) {
+            const uint32_t key = keys[i];
+            if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & dmask], 1u);
+        }
+        SEL_STAMP(5);
+        if (wave == 0) {  // lane l owns digits 255-4l .. 252-4l (descending)
+            uint32_t c[4], sum = 0;
 #pragma unroll
-                for (int w = 0; w < kSelWaves; ++w) c += sh.cnt[w][15 - lane];
+            for (int q = 0; q < 4; ++q) {
+                c[q] = sh.hist[255 - 4 * lane - q];
+                sum += c[q];
             }
-            uint32_t incl = c;
+            uint32_t incl = sum;
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
+            for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(incl, o, 64);
                 if (lane >= o) incl += y;
             }
-            const uint32_t excl = incl - c;
-            if (lane < 16 && (uint64_t)excl < (uint64_t)kk && (uint64_t)incl >= (uint64_t)kk) {
-                sh.digit = 15 - lane;
-                sh.kk = kk - excl;
+            const uint32_t excl = incl - sum;
+            if ((uint64_t)excl < (uint64_t)kk && (uint64_t)incl >= (uint64_t)kk) {
+                uint32_t acc = excl;
+                int q = 0;
+                for (; q < 3; ++q) {
+                    if ((uint64_t)(acc + c[q]) >= (uint64_t)kk) break;
+                    acc += c[q];
+                }
+                sh.digit = 255 - 4 * lane - q;
+                sh.dcount = c[q];
+                sh.kk = kk - acc;
             }
         }
         __syncthreads();
         prefix |= sh.digit << shift;
-        mask |= 15u << shift;
+        mask |= dmask << shift;
         kk = sh.kk;
+        bit = shift;
+        const uint32_t dcount = sh.dcount;
         __syncthreads();
+        if (bit > 0 && dcount <= (uint32_t)kCandMax) {
+            // rank the few keys of the threshold bin directly
+            if (tid == 0) sh.ncand = 0;
+            __syncthreads();
+            for (int i = tid; i < n; i += kST) {
+                const uint32_t key = keys[i];
+                if ((key & mask) == prefix) sh.cand[atomicAdd(&sh.ncand, 1u)] = key;
+            }
+            SEL_STAMP(6);
+            const int nc = (int)sh.ncand;
+            for (int i = nc + tid; i < ((nc + 3) & ~3); i += kST) sh.cand[i] = 0u;  // pad to x4
+            __syncthreads();
+            const uint4* c4 = reinterpret_cast<const uint4*>(sh.cand);
+            for (int t = tid; t < nc; t += kST) {
+                const uint32_t v = sh.cand[t];
+                int gt = 0, ge = 0;
+                const int nq = (nc + 3) >> 2;
+#pragma unroll 4
+                for (int j = 0; j < nq; ++j) {  // 16-B broadcast reads, 4 candidates each
+                    const uint4 c = c4[j];
+                    gt += (c.x > v) + (c.y > v) + (c.z > v) + (c.w > v);
+                    ge += (c.x >= v) + (c.y >= v) + (c.z >= v) + (c.w >= v);
+                }
+                if (v == 0u) ge -= ((nc + 3) & ~3) - nc;  // zero padding equals v only when v == 0
+                if (gt < kk && kk <= ge) {  // every writer writes the same (T, need)
+                    sh.T = v;
+                    sh.need_eq = kk - gt;
+                }
+            }
+            SEL_STAMP(7);
+            ranked = true;
+            break;
+        }
     }
-    const uint32_t T = prefix;
-    const int64_t need_eq = kk;
-    const int per = (n + kSelThreads - 1) / kSelThreads;
+    uint32_t T;
+    int64_t need_eq;
+    if (ranked) {
+        T = sh.T;
+        need_eq = sh.need_eq;
+    } else {  // every bit fixed: the threshold is the prefix itself
+        T = prefix;
+        need_eq = kk;
+    }
+    SEL_STAMP(2);
+    // index-ordered compaction over contiguous per-thread row ranges (multiples of 4
+    // rows, read as 16-B LDS vectors; the key array is padded to a multiple of 4)
+    const int per = (((n + kST - 1) / kST) + 3) & ~3;
     const int r0 = min(n, tid * per), r1 = min(n, r0 + per);
     int64_t gt = 0, eq = 0;
-    for (int i = r0; i < r1; ++i) {
-        const uint32_t key = keys[i];
-        gt += key > T;
-        eq += key == T;
+    for (int i = r0; i < r1; i += 4) {
+        const uint4 q = *reinterpret_cast<const uint4*>(keys + i);
+        const uint32_t kv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i + u < r1) {
+                gt += kv[u] > T;
+                eq += kv[u] == T;
+            }
+        }
     }
-    int64_t tot;
-    const int64_t eq_before = block_exscan(eq, sh.wsum, tot);
+    const int64_t eq_before = block_exscan_s(eq, sh.wsum);
     int64_t take_eq = need_eq - eq_before;
     take_eq = take_eq < 0 ? 0 : (take_eq > eq ? eq : take_eq);
-    int64_t slot = block_exscan(gt + take_eq, sh.wsum, tot);
+    int64_t slot = block_exscan_s(gt + take_eq, sh.wsum);
+    SEL_STAMP(3);
+    int32_t* rl = rowlist + s.sel_off;
+    int32_t* sm = slotmap + s.row_off;
     int64_t eq_seen = 0;
-    for (int i = r0; i < r1; ++i) {
-        const uint32_t key = keys[i];
-        bool sel = key > T;
-        if (key == T) {
-            sel = eq_seen < take_eq;
-            ++eq_seen;
-        }
-        if (sel) {
-            rl[slot] = i;
-            sm[i] = (int32_t)slot;
-            ++slot;
-        } else {
-            sm[i] = -1;
+    for (int i = r0; i < r1; i += 4) {
+        const uint4 q = *reinterpret_cast<const uint4*>(keys + i);
+        const uint32_t kv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i + u < r1) {
+                const uint32_t key = kv[u];
+                bool sel = key > T;
+                if (key == T) {
+                    sel = eq_seen < take_eq;
+                    ++eq_seen;
+                }
+                if (sel) {
+                    rl[slot] = i + u;
+                    sm[i + u] = (int32_t)slot;
+                    ++slot;
+                } else {
+                    sm[i + u] = -1;
+                }
+            }
         }
     }
-}
-
-// Segments with n <= kSmallSelRows: energies straight into LDS, select, compact -- one launch.
-__global__ void __launch_bounds__(kSelThreads) k_select_small(const SegDev* __restrict__ segs,
-                                                              const int32_t* __restrict__ seg_ids,
-                                                              const float* __restrict__ sketch,
-                                                              int R, float wsf,
-                                                              int32_t* __restrict__ rowlist,
-                                                              int32_t* __restrict__ slotmap) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t skeys[];
-    __shared__ SelSharedB sh;
-    const SegDev s = segs[seg_ids[blockIdx.x]];
-    const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
-    const float* sk = sketch + s.sketch_off;
-    for (int64_t row = threadIdx.x; row < s.n; row += kSelThreads)
-        skeys[row] = energy_key(row_energy(sk + row * stride, R, wsf, s.kind));
-    __syncthreads();
-    select_rows_lds(skeys, (int)s.n, s.k_rows, rowlist + s.sel_off, slotmap + s.row_off, sh);
+    SEL_STAMP(4);
 }
 
 // Larger segments: keys precomputed by k_energy into global memory.
@@ -540,19 +707,6 @@ __global__ void __launch_bounds__(kSelThreads) k_select(const SegDev* __restrict
     const SegDev s = segs[seg_ids[blockIdx.x]];
     select_rows(keys_all + s.row_off, s.n, s.k_rows, rowlist + s.sel_off, slotmap + s.row_off, sh);
 }
-
-// mean of the all-reduced values: x / ws exactly; for a power-of-two ws the
-// reciprocal is exact and x * (1/ws) rounds the same real number as x / ws.
-struct Scale {
-    float ws, inv;
-    int pow2;
-    __device__ __forceinline__ float operator()(float x) const {
-        return pow2 ? x * inv : __fdiv_rn(x, ws);
-    }
-    __device__ __forceinline__ float4 operator()(float4 x) const {
-        return make_float4((*this)(x.x), (*this)(x.y), (*this)(x.z), (*this)(x.w));
-    }
-};
 
 __device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m >= 256; }
 
@@ -806,6 +960,14 @@ extern "C" int arctopk_encode(const arctopk_plan* p, const float* grad, float* e
     return ARCTOPK_EINVAL;
 }
 
+static Scale make_scale(int32_t ws) {
+    Scale sc;
+    sc.ws = (float)ws;
+    sc.pow2 = (ws & (ws - 1)) == 0;
+    sc.inv = 1.0f / (float)ws;
+    return sc;
+}
+
 static int launch_energy(const arctopk_plan* p, const float* sketch, int32_t ws, uint32_t* keys,
                          float* energy, hipStream_t st) {
     int64_t maxn = 0;
@@ -813,7 +975,7 @@ static int launch_energy(const arctopk_plan* p, const float* sketch, int32_t ws,
     int gx = (int)std::min<int64_t>(1024, (maxn + 255) / 256);
     dim3 grid(gx, p->nseg);
     hipLaunchKernelGGL(k_energy, grid, dim3(256), 0, st, p->d_segs, p->nseg, sketch, p->r,
-                       (float)ws, keys, energy);
+                       make_scale(ws), keys, energy);
     return (int)hipGetLastError();
 }
 
@@ -828,9 +990,8 @@ extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_
     if (!p || !sketch || !rowlist || !slotmap || ws < 1) return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     if (p->n_small) {
-        hipLaunchKernelGGL(k_select_small, dim3(p->n_small), dim3(kSelThreads),
-                           (size_t)p->small_lds, st, p->d_segs, p->d_small, sketch, p->r, (float)ws,
-                           rowlist, slotmap);
+        hipLaunchKernelGGL(k_select_small, dim3(p->n_small), dim3(kST), (size_t)p->small_lds, st,
+                           p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
     }
     if (p->n_large) {
         int e = launch_energy(p, sketch, ws, p->d_keys, nullptr, st);
@@ -865,10 +1026,7 @@ extern "C" int arctopk_decode(const arctopk_plan* p, const float* packed, const 
     if (ef == ARCTOPK_EF21 && !gerr) return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid(p->n_dec), block(256);
-    Scale sc;
-    sc.ws = (float)ws;
-    sc.pow2 = (ws & (ws - 1)) == 0;
-    sc.inv = 1.0f / (float)ws;
+    const Scale sc = make_scale(ws);
     if (ef == ARCTOPK_EF21)
         hipLaunchKernelGGL(k_decode<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, p->d_dec, packed, slotmap, sc, gerr, out);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)

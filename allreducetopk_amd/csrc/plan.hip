@@ -162,7 +162,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     p->enc_lds_bytes = vlds ? lds : std::max(0, lds);
     p->n_small = (int)small_ids.size();
     p->n_large = (int)large_ids.size();
-    p->small_lds = (int)(small_rows * 4);
+    p->small_lds = (int)(((small_rows + 3) & ~3) * 4 + 16);
 #define ALLOC_COPY(dst, vec)                                                                  \
     do {                                                                                      \
         e = hipMalloc((void**)&dst, std::max<size_t>(1, vec.size() * sizeof(vec[0])));        \

@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-events", action="store_true")
+    ap.add_argument("--host-staged", action="store_true",
+                    help="D2H + H2D of the packed payload around the all-reduce (NIC model)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -120,6 +122,7 @@ def main():
     bucket = SyntheticBucket(buf, shapes, index=0, is_last=True)
     st = GroupTopKState(None, r=args.r, compress_ratio=args.ratio, start_compress_iter=0,
                         use_error_feedback=args.ef, seed=1234)
+    st.host_staged = args.host_staged
     # warm-up (EF14: first call creates E; EF21: first call is the dense init)
     for _ in range(max(args.warmup, 2 if args.ef == "ef21" else 1)):
         group_topk_hook(st, bucket)
@@ -143,6 +146,8 @@ def main():
     phase_ms = {}
     if st.phase_events:
         order = ["start"] + PHASES
+        if args.host_staged:
+            order = order[:5] + ["d2h", "h2d"] + order[5:]
         for a, b in zip(order[:-1], order[1:]):
             ds = [ev[a].elapsed_time(ev[b]) for ev in st.phase_events]
             phase_ms[b] = statistics.mean(ds)
@@ -170,7 +175,8 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (N(0,1) fp32 gradients, per-rank seed)",
-        "config": {"workload": f"arctopk_{args.ef}_bucket_16x2048x2048_fp32_256MiB",
+        "config": {"workload": f"arctopk_{args.ef}_bucket_16x2048x2048_fp32_256MiB"
+                               + ("_host_staged" if args.host_staged else ""),
                    "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
                    "bucket_bytes": bucket_bytes, "parallelism": f"dp{world}",
                    "collectives": "RCCL all_reduce x2 per bucket"},
