@@ -92,10 +92,40 @@ class BucketPlan:
         self.rowlist = torch.empty(max(1, info.sel_rows), dtype=torch.int32, device=dev)
         self.slotmap = torch.empty(max(1, info.rows_total), dtype=torch.int32, device=dev)
         self.V = torch.empty(max(1, info.v_len), dtype=torch.float32, device=dev)
+        self.groups = self._make_groups()
         bits = dtype_bits(dtype)
         # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
         self.bits_sum = sum(((s.n if s.kind == N.SEG_RAW else s.n * r) + s.k_rows * s.m) * bits
                             for s in self.segments)
+
+    PIPELINE_GROUPS = 4             # packed all-reduce split into up to this many pieces
+    PIPELINE_MIN_BYTES = 4 << 20    # ... each at least this large (RCCL efficiency)
+
+    def _make_groups(self):
+        """Contiguous segment ranges with roughly equal packed bytes: (b, e, lo, hi)."""
+        segs = self.segments
+        total = int(self.info.packed_len)
+        ng = max(1, min(self.PIPELINE_GROUPS, len(segs), (4 * total) // self.PIPELINE_MIN_BYTES))
+        groups, b, acc = [], 0, 0
+        for i, s in enumerate(segs):
+            acc += int(s.k_rows * s.m)
+            if acc * ng >= total * (len(groups) + 1) or i == len(segs) - 1:
+                lo = int(segs[b].packed_off)
+                hi = int(s.packed_off + s.k_rows * s.m)
+                groups.append((b, i + 1, lo, hi))
+                b = i + 1
+        return groups
+
+    def pack_range(self, b: int, e: int, grad, err, ef: int, stream: int):
+        N.check(N.lib().arctopk_pack_segments(self.handle, b, e, N.ptr(grad), N.ptr(err), ef,
+                                              self.rowlist.data_ptr(), self.packed.data_ptr(),
+                                              stream), "arctopk_pack_segments")
+
+    def decode_range(self, b: int, e: int, world_size: int, ef: int, gerr, out, stream: int):
+        N.check(N.lib().arctopk_decode_segments(self.handle, b, e, self.packed.data_ptr(),
+                                                self.slotmap.data_ptr(), world_size, ef,
+                                                N.ptr(gerr), out.data_ptr(), stream),
+                "arctopk_decode_segments")
 
     @property
     def sketch_view(self):
@@ -302,10 +332,12 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     plan = state._plan_for(bucket)
     stream = torch.cuda.current_stream(input_tensor.device)
     sid = stream.cuda_stream
-    host_v = state._proj.get(seed, plan.ms, input_tensor.dtype)
-    if plan.info.v_len:
-        plan.V[:plan.info.v_len].copy_(host_v[:plan.info.v_len], non_blocking=True)
-    state._proj.prefetch(state._upcoming_ms(bucket), input_tensor.dtype)
+    dtype = input_tensor.dtype
+    host_v = state._proj.get(seed, plan.ms, dtype)
+    V = plan.V
+    if plan.info.v_len:  # 512 KiB pinned H2D at headline, stream-ordered before encode
+        V[:plan.info.v_len].copy_(host_v[:plan.info.v_len], non_blocking=True)
+    state._proj.prefetch(state._upcoming_ms(bucket), dtype)
 
     evs = None
     if state.phase_events is not None:
@@ -321,16 +353,35 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             evs[name] = e
 
     mark("start")
-    plan.encode(input_tensor, err, ef, err_in, plan.V, sid)
+    plan.encode(input_tensor, err, ef, err_in, V, sid)
     mark("encode")
+
     if world_size > 1:  # a SUM over one rank is the identity: nothing to exchange
         dist.all_reduce(plan.sketch_view, group=group, async_op=False)
     mark("sketch_allreduce")
     plan.select(world_size, sid)
     mark("select")
+    state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum
+    if world_size > 1 and len(plan.groups) > 1 and not state.host_staged:
+        # pipelined exchange: pack group g, start its all-reduce (RCCL stream), pack g+1;
+        # then decode each group once its collective is done (the current stream waits
+        # on the collective's event, the host does not block)
+        works = []
+        for b_, e_, lo, hi in plan.groups:
+            plan.pack_range(b_, e_, input_tensor, err, ef, sid)
+            works.append(dist.all_reduce(plan.packed[lo:hi], group=group, async_op=True))
+        mark("pack")
+        mark("packed_allreduce")
+        for (b_, e_, lo, hi), w in zip(plan.groups, works):
+            w.wait()
+            plan.decode_range(b_, e_, world_size, ef, gerr, input_tensor, sid)
+        mark("decode")
+        state.maybe_increase_iter(bucket)
+        fut = torch.futures.Future()
+        fut.set_result(input_tensor)
+        return fut
     plan.pack(input_tensor, err, ef, sid)
     mark("pack")
-    state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum
     if state.host_staged:  # D2H to a pinned "NIC buffer" and back, stream-ordered
         pv = plan.packed_view
         if state._host_buf is None or state._host_buf.numel() < pv.numel():

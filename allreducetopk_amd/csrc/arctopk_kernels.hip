@@ -440,7 +440,7 @@ __device__ void select_rows(const KeyT* keys, int64_t n, int64_t k, int32_t* __r
             ++eq_seen;
         }
         if (sel) {
-            rl[slot] = (int32_t)i;
+            if (slot < k) rl[slot] = (int32_t)i;  // bound: never store past the row list
             sm[i] = (int32_t)slot;
             ++slot;
         } else {
@@ -570,6 +570,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
             const uint32_t key = keys[i];
             if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & dmask], 1u);
         }
+        __syncthreads();
         SEL_STAMP(5);
         if (wave == 0) {  // lane l owns digits 255-4l .. 252-4l (descending)
             uint32_t c[4], sum = 0;
@@ -612,6 +613,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
                 const uint32_t key = keys[i];
                 if ((key & mask) == prefix) sh.cand[atomicAdd(&sh.ncand, 1u)] = key;
             }
+            __syncthreads();
             SEL_STAMP(6);
             const int nc = (int)sh.ncand;
             for (int i = nc + tid; i < ((nc + 3) & ~3); i += kST) sh.cand[i] = 0u;  // pad to x4
@@ -633,6 +635,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
                     sh.need_eq = kk - gt;
                 }
             }
+            __syncthreads();
             SEL_STAMP(7);
             ranked = true;
             break;
@@ -685,7 +688,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
                     ++eq_seen;
                 }
                 if (sel) {
-                    rl[slot] = i + u;
+                    if (slot < s.k_rows) rl[slot] = i + u;  // bound: never store past the row list
                     sm[i + u] = (int32_t)slot;
                     ++slot;
                 } else {
@@ -1002,19 +1005,51 @@ extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_
     return (int)hipGetLastError();
 }
 
-extern "C" int arctopk_pack(const arctopk_plan* p, const float* grad, float* err, int32_t ef,
-                            const int32_t* rowlist, float* packed, void* stream) {
+extern "C" int arctopk_pack_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,
+                                     const float* grad, float* err, int32_t ef,
+                                     const int32_t* rowlist, float* packed, void* stream) {
     if (!p || !rowlist || !packed) return ARCTOPK_EINVAL;
+    if (seg_begin < 0 || seg_end > p->nseg || seg_begin > seg_end) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF_NONE ? !grad : !err) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF21 && !grad) return ARCTOPK_EINVAL;
+    const int c0 = p->h_pack_begin[seg_begin], c1 = p->h_pack_begin[seg_end];
+    if (c1 == c0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid(p->n_pack), block(256);
+    dim3 grid(c1 - c0), block(256);
+    const Chunk* ch = p->d_pack + c0;
     if (ef == ARCTOPK_EF_NONE)
-        hipLaunchKernelGGL(k_pack<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, p->d_pack, grad, err, rowlist, packed);
+        hipLaunchKernelGGL(k_pack<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
     else if (ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL(k_pack<ARCTOPK_EF14>, grid, block, 0, st, p->d_segs, p->d_pack, grad, err, rowlist, packed);
+        hipLaunchKernelGGL(k_pack<ARCTOPK_EF14>, grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
     else if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL(k_pack<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, p->d_pack, grad, err, rowlist, packed);
+        hipLaunchKernelGGL(k_pack<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
+    else
+        return ARCTOPK_EINVAL;
+    return (int)hipGetLastError();
+}
+
+extern "C" int arctopk_pack(const arctopk_plan* p, const float* grad, float* err, int32_t ef,
+                            const int32_t* rowlist, float* packed, void* stream) {
+    if (!p) return ARCTOPK_EINVAL;
+    return arctopk_pack_segments(p, 0, p->nseg, grad, err, ef, rowlist, packed, stream);
+}
+
+extern "C" int arctopk_decode_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,
+                                       const float* packed, const int32_t* slotmap, int32_t ws,
+                                       int32_t ef, float* gerr, float* out, void* stream) {
+    if (!p || !packed || !slotmap || !out || ws < 1) return ARCTOPK_EINVAL;
+    if (seg_begin < 0 || seg_end > p->nseg || seg_begin > seg_end) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF21 && !gerr) return ARCTOPK_EINVAL;
+    const int c0 = p->h_dec_begin[seg_begin], c1 = p->h_dec_begin[seg_end];
+    if (c1 == c0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid(c1 - c0), block(256);
+    const Chunk* ch = p->d_dec + c0;
+    const Scale sc = make_scale(ws);
+    if (ef == ARCTOPK_EF21)
+        hipLaunchKernelGGL(k_decode<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+    else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
+        hipLaunchKernelGGL(k_decode<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -1022,18 +1057,8 @@ extern "C" int arctopk_pack(const arctopk_plan* p, const float* grad, float* err
 
 extern "C" int arctopk_decode(const arctopk_plan* p, const float* packed, const int32_t* slotmap,
                               int32_t ws, int32_t ef, float* gerr, float* out, void* stream) {
-    if (!p || !packed || !slotmap || !out || ws < 1) return ARCTOPK_EINVAL;
-    if (ef == ARCTOPK_EF21 && !gerr) return ARCTOPK_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    dim3 grid(p->n_dec), block(256);
-    const Scale sc = make_scale(ws);
-    if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL(k_decode<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, p->d_dec, packed, slotmap, sc, gerr, out);
-    else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL(k_decode<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, p->d_dec, packed, slotmap, sc, gerr, out);
-    else
-        return ARCTOPK_EINVAL;
-    return (int)hipGetLastError();
+    if (!p) return ARCTOPK_EINVAL;
+    return arctopk_decode_segments(p, 0, p->nseg, packed, slotmap, ws, ef, gerr, out, stream);
 }
 
 extern "C" int arctopk_ef_apply(float* x, float* E, int64_t n, int32_t ef, int32_t err_in,

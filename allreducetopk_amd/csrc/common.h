@@ -76,6 +76,8 @@ struct arctopk_plan {
     int n_pack;
     arctopk::Chunk* d_dec;
     int n_dec;
+    int32_t* h_pack_begin;        // [nseg + 1]: first pack chunk of each segment
+    int32_t* h_dec_begin;         // [nseg + 1]: first decode chunk of each segment
     uint32_t* d_keys;             // select workspace: one key per row
     int32_t* d_small;             // segments selected by the fused one-block kernel
     int n_small;

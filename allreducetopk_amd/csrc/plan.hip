@@ -94,6 +94,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     int64_t small_rows = 0;
     std::vector<EncTile> enc;
     std::vector<Chunk> pack, dec;
+    std::vector<int32_t> pack_begin, dec_begin;
     int lds = 0;
     int vlds = 1;
     for (size_t i = 0; i < segs.size(); ++i) {
@@ -130,6 +131,8 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             else vlds = 0;
         }
         // ---- pack chunks: selected rows, ~kChunkElems elements each
+        pack_begin.push_back((int32_t)pack.size());
+        dec_begin.push_back((int32_t)dec.size());
         {
             int64_t per = std::max<int64_t>(1, kChunkElems / s.m);
             for (int64_t j = 0; j < s.k_rows; j += per)
@@ -158,6 +161,12 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     p->n_enc = (int)enc.size();
     p->n_pack = (int)pack.size();
     p->n_dec = (int)dec.size();
+    pack_begin.push_back((int32_t)pack.size());
+    dec_begin.push_back((int32_t)dec.size());
+    p->h_pack_begin = new int32_t[pack_begin.size()];
+    p->h_dec_begin = new int32_t[dec_begin.size()];
+    std::copy(pack_begin.begin(), pack_begin.end(), p->h_pack_begin);
+    std::copy(dec_begin.begin(), dec_begin.end(), p->h_dec_begin);
     p->enc_vlds = vlds;
     p->enc_lds_bytes = vlds ? lds : std::max(0, lds);
     p->n_small = (int)small_ids.size();
@@ -208,6 +217,8 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_small) (void)hipFree(p->d_small);
     if (p->d_large) (void)hipFree(p->d_large);
     delete[] p->h_segs;
+    delete[] p->h_pack_begin;
+    delete[] p->h_dec_begin;
     delete p;
     return 0;
 }

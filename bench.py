@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-events", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL (real runs); gloo lets N ranks share one GPU (rehearsal)")
     ap.add_argument("--host-staged", action="store_true",
                     help="D2H + H2D of the packed payload around the all-reduce (NIC model)")
     args = ap.parse_args()
@@ -108,11 +110,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks but {ndev} visible GPUs (RCCL needs one GPU per rank)")
+    local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     shapes = HEADLINE
     n = bucket_numel(shapes)
@@ -179,7 +188,8 @@ def main():
                                + ("_host_staged" if args.host_staged else ""),
                    "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
                    "bucket_bytes": bucket_bytes, "parallelism": f"dp{world}",
-                   "collectives": "RCCL all_reduce x2 per bucket"},
+                   "collectives": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
+                                  + " all_reduce: sketch + packed values (pipelined in groups)"},
         "per_gpu_value": round(value / world, 2),
         "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
         "roofline": roof,

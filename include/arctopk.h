@@ -152,6 +152,19 @@ int arctopk_pack(const arctopk_plan* plan, const float* grad, float* err, int32_
 int arctopk_decode(const arctopk_plan* plan, const float* packed, const int32_t* slotmap,
                    int32_t world_size, int32_t ef, float* gerr, float* out, void* stream);
 
+/*
+ * Segment-range forms of K3/K4 (segments [seg_begin, seg_end) only), so a caller can
+ * pipeline the packed all-reduce: pack group g, start its collective, pack g+1, ...
+ * and decode each group once its collective has completed.  Packed data of the
+ * segments in [b, e) occupy packed[seg(b).packed_off, seg(e-1).packed_off + k(e-1)).
+ */
+int arctopk_pack_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t seg_end,
+                          const float* grad, float* err, int32_t ef, const int32_t* rowlist,
+                          float* packed, void* stream);
+int arctopk_decode_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t seg_end,
+                            const float* packed, const int32_t* slotmap, int32_t world_size,
+                            int32_t ef, float* gerr, float* out, void* stream);
+
 /* ---- TopK / RandK baselines (comm_hooks/sparse_hook.py, sparse_hook_c4.py) ---------- */
 /*
  * Tensors of a bucket are described by host arrays of `ntensors` entries:

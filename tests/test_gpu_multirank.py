@@ -31,6 +31,9 @@ def _worker(rank, ws, port, td, ef, kind):
     from oracle import sparse as S
     dev = "cuda:0"
     n = bucket_numel(MIX)
+    if kind == "arc_pipe":  # force the pipelined pack / all-reduce / decode on this bucket
+        G.BucketPlan.PIPELINE_MIN_BYTES = 64
+        kind = "arc"
     if kind == "arc":
         st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                               use_error_feedback=ef, seed=77)
@@ -60,6 +63,8 @@ def _worker(rank, ws, port, td, ef, kind):
             plan = st._plans[0][1]
             rl = plan.rowlist.cpu()
             rows = [rl[s.sel_off:s.sel_off + s.k_rows].long() for s in plan.segments]
+            if G.BucketPlan.PIPELINE_MIN_BYTES == 64:
+                assert len(plan.groups) > 1, "pipelined path not exercised"
             other = [torch.empty_like(rl) for _ in range(ws)]
             dist.all_gather(other, rl)
             assert torch.equal(other[0], other[1]), "ranks selected different rows"
@@ -92,6 +97,7 @@ def _worker(rank, ws, port, td, ef, kind):
 
 
 @pytest.mark.parametrize("kind,ef", [("arc", "noef"), ("arc", "ef14"), ("arc", "ef21"),
+                                     ("arc_pipe", "ef14"), ("arc_pipe", "ef21"),
                                      ("topk", "ef14"), ("topk", "ef21"), ("randk", "ef14")])
 def test_two_ranks_one_gpu(kind, ef):
     from parity import free_port
