@@ -12,6 +12,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "mselect.h"
 
 using namespace arctopk;
 
@@ -329,126 +330,6 @@ __global__ void __launch_bounds__(256) k_energy(const SegDev* __restrict__ segs,
     }
 }
 
-constexpr int kSelThreads = 1024;
-constexpr int kSelWaves = kSelThreads / 64;
-
-// exclusive scan of one value per thread across the block; returns the block total
-__device__ __forceinline__ int64_t block_exscan(int64_t v, int64_t* wsum, int64_t& total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int64_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    if (wave == 0) {
-        int64_t w = lane < kSelWaves ? wsum[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int64_t y = __shfl_up(w, o, 64);
-            if (lane >= o) w += y;
-        }
-        if (lane < kSelWaves) wsum[lane] = w;  // inclusive
-    }
-    __syncthreads();
-    const int64_t before = (wave ? wsum[wave - 1] : 0) + x - v;
-    total = wsum[kSelWaves - 1];
-    __syncthreads();
-    return before;
-}
-
-struct SelShared {
-    uint32_t hist[256];
-    int64_t wsum[kSelWaves];
-    uint32_t digit;
-    int64_t kk;
-};
-
-// One block: MSB-first 8-bit radix select of the k-th largest of keys[0..n) (LDS or
-// global), then an index-ordered compaction (ties at the threshold: lowest rows
-// first) writing the ascending row list and every row's slot (or -1).
-template <typename KeyT>
-__device__ void select_rows(const KeyT* keys, int64_t n, int64_t k, int32_t* __restrict__ rl,
-                            int32_t* __restrict__ sm, SelShared& sh) {
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    uint32_t prefix = 0, mask = 0;
-    int64_t kk = k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int i = tid; i < 256; i += kSelThreads) sh.hist[i] = 0;
-        __syncthreads();
-        for (int64_t i = tid; i < n; i += kSelThreads) {
-            const uint32_t key = keys[i];
-            if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        if (tid < 64) {
-            uint32_t c[4];
-            uint32_t sum = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                c[q] = sh.hist[255 - 4 * lane - q];
-                sum += c[q];
-            }
-            uint32_t incl = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += y;
-            }
-            const uint32_t excl = incl - sum;
-            if ((uint64_t)excl < (uint64_t)kk && (uint64_t)incl >= (uint64_t)kk) {
-                uint32_t acc = excl;
-                int q = 0;
-                for (; q < 3; ++q) {
-                    if ((uint64_t)(acc + c[q]) >= (uint64_t)kk) break;
-                    acc += c[q];
-                }
-                sh.digit = 255 - 4 * lane - q;
-                sh.kk = kk - acc;
-            }
-        }
-        __syncthreads();
-        prefix |= sh.digit << shift;
-        mask |= 255u << shift;
-        kk = sh.kk;
-        __syncthreads();
-    }
-    const uint32_t T = prefix;
-    const int64_t need_eq = kk;
-    const int64_t per = (n + kSelThreads - 1) / kSelThreads;
-    const int64_t r0 = min<int64_t>(n, tid * per), r1 = min<int64_t>(n, r0 + per);
-    int64_t gt = 0, eq = 0;
-    for (int64_t i = r0; i < r1; ++i) {
-        const uint32_t key = keys[i];
-        gt += key > T;
-        eq += key == T;
-    }
-    int64_t tot;
-    const int64_t eq_before = block_exscan(eq, sh.wsum, tot);
-    int64_t take_eq = need_eq - eq_before;
-    take_eq = take_eq < 0 ? 0 : (take_eq > eq ? eq : take_eq);
-    int64_t slot = block_exscan(gt + take_eq, sh.wsum, tot);
-    int64_t eq_seen = 0;
-    for (int64_t i = r0; i < r1; ++i) {
-        const uint32_t key = keys[i];
-        bool sel = key > T;
-        if (key == T) {
-            sel = eq_seen < take_eq;
-            ++eq_seen;
-        }
-        if (sel) {
-            if (slot < k) rl[slot] = (int32_t)i;  // bound: never store past the row list
-            sm[i] = (int32_t)slot;
-            ++slot;
-        } else {
-            sm[i] = -1;
-        }
-    }
-}
-
 // Small segments (n <= kSmallSelRows): one 256-thread block per segment, keys in LDS.
 //  1. energies -> LDS keys; block OR/AND gives the keys' common leading bits, so the
 //     first 8-bit digit covers the most significant *varying* bits (energies of one
@@ -700,15 +581,32 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
     SEL_STAMP(4);
 }
 
-// Larger segments: keys precomputed by k_energy into global memory.
-__global__ void __launch_bounds__(kSelThreads) k_select(const SegDev* __restrict__ segs,
-                                                        const int32_t* __restrict__ seg_ids,
-                                                        const uint32_t* __restrict__ keys_all,
-                                                        int32_t* __restrict__ rowlist,
-                                                        int32_t* __restrict__ slotmap) {
-    __shared__ SelShared sh;
-    const SegDev s = segs[seg_ids[blockIdx.x]];
-    select_rows(keys_all + s.row_off, s.n, s.k_rows, rowlist + s.sel_off, slotmap + s.row_off, sh);
+// Larger segments: energy keys into global memory plus each segment's key OR / AND
+// (its common leading bits seed the multi-block radix select of mselect.hip).
+__global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ segs,
+                                                  const int32_t* __restrict__ ids, int first,
+                                                  const float* __restrict__ sketch, int R, Scale sc,
+                                                  uint32_t* __restrict__ keys, MWorkspace* ws) {
+    const int t = blockIdx.y;
+    const SegDev s = segs[ids[first + t]];
+    const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
+    uint32_t kor = 0u, kand = ~0u;
+    for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < s.n;
+         row += (int64_t)gridDim.x * 256) {
+        const uint32_t key = energy_key(row_energy(sketch + s.sketch_off + row * stride, R, sc, s.kind));
+        keys[s.row_off + row] = key;
+        kor |= key;
+        kand &= key;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicOr(&ws->st[t].kor, kor);
+        atomicAnd(&ws->st[t].kand, kand);
+    }
 }
 
 __device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m >= 256; }
@@ -784,6 +682,44 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                 }
             }
         }
+        return;
+    }
+    if (m >= 4 && m < 256) {  // small-m: row list staged in LDS, 32-bit mulhi division
+        __shared__ int32_t rs[kSmallTileRows];
+        const int nr = (int)ch.nrows;
+        for (int r = threadIdx.x; r < nr; r += 256) rs[r] = rl[r];
+        __syncthreads();
+        const uint32_t cnt = (uint32_t)(nr * m);
+        const int64_t dbase = s.packed_off + ch.row0 * m;
+        const int64_t pre = (4 - (dbase & 3)) & 3;
+        auto one = [&](uint32_t e) -> float {
+            const uint32_t r = div32(e, s.magic32);
+            const int64_t src = s.offset + (int64_t)rs[r] * m + (e - r * (uint32_t)m);
+            float v;
+            if constexpr (EF == ARCTOPK_EF_NONE) {
+                v = G[src];
+            } else if constexpr (EF == ARCTOPK_EF14) {
+                v = E[src];
+                E[src] = 0.f;
+            } else {
+                const float ev = E[src];
+                v = G[src] - ev;
+                E[src] = ev + v;
+            }
+            return v;
+        };
+        for (uint32_t e = threadIdx.x; e < (uint32_t)min<int64_t>(pre, cnt); e += 256) dst[e] = one(e);
+        const uint32_t body = cnt > pre ? (uint32_t)((cnt - pre) >> 2) : 0u;
+        for (uint32_t q = threadIdx.x; q < body; q += 256) {
+            const uint32_t e = (uint32_t)pre + (q << 2);
+            float4 v;
+            v.x = one(e);
+            v.y = one(e + 1);
+            v.z = one(e + 2);
+            v.w = one(e + 3);
+            *reinterpret_cast<float4*>(dst + e) = v;
+        }
+        for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256) dst[e] = one(e);
         return;
     }
     const uint32_t cnt = (uint32_t)(ch.nrows * m);
@@ -864,6 +800,37 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                 }
             }
         }
+        return;
+    }
+    if (m >= 4 && m < 256) {  // small-m tile: slots staged in LDS, 32-bit mulhi division
+        __shared__ int32_t sl[kSmallTileRows];
+        const int nr = (int)ch.nrows;
+        for (int r = threadIdx.x; r < nr; r += 256) sl[r] = sm[r];
+        __syncthreads();
+        const uint32_t cnt = (uint32_t)(nr * m);
+        const int64_t pre = (4 - (base & 3)) & 3;  // elements before the first 16-B boundary
+        auto one = [&](uint32_t e) -> float {
+            const uint32_t r = div32(e, s.magic32);
+            const int32_t slot = sl[r];
+            float v = slot >= 0 ? sc(pk[(int64_t)slot * m + (e - r * (uint32_t)m)]) : 0.f;
+            if constexpr (EF == ARCTOPK_EF21) {
+                v = gE[base + e] + v;
+                if (slot >= 0) gE[base + e] = v;
+            }
+            return v;
+        };
+        for (uint32_t e = threadIdx.x; e < (uint32_t)min<int64_t>(pre, cnt); e += 256) out[base + e] = one(e);
+        const uint32_t body = cnt > pre ? (uint32_t)((cnt - pre) >> 2) : 0u;
+        for (uint32_t q = threadIdx.x; q < body; q += 256) {
+            const uint32_t e = (uint32_t)pre + (q << 2);
+            float4 v;
+            v.x = one(e);
+            v.y = one(e + 1);
+            v.z = one(e + 2);
+            v.w = one(e + 3);
+            *reinterpret_cast<float4*>(out + base + e) = v;
+        }
+        for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256) out[base + e] = one(e);
         return;
     }
     const uint32_t cnt = (uint32_t)(ch.nrows * m);
@@ -996,11 +963,17 @@ extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_
         hipLaunchKernelGGL(k_select_small, dim3(p->n_small), dim3(kST), (size_t)p->small_lds, st,
                            p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
     }
-    if (p->n_large) {
-        int e = launch_energy(p, sketch, ws, p->d_keys, nullptr, st);
+    for (int bi = 0; bi < p->n_large_batches; ++bi) {
+        const MBatch& b = p->h_large_batches[bi];
+        int64_t maxn = 0;
+        for (int i = 0; i < b.cnt; ++i) maxn = std::max<int64_t>(maxn, b.it[i].n);
+        int e = ms_reset_orand(p->d_mws, b.cnt, st);
         if (e) return e;
-        hipLaunchKernelGGL(k_select, dim3(p->n_large), dim3(kSelThreads), 0, st, p->d_segs,
-                           p->d_large, p->d_keys, rowlist, slotmap);
+        const int gx = (int)std::min<int64_t>(512, (maxn + 255) / 256);
+        hipLaunchKernelGGL(k_arc_keys, dim3(gx, b.cnt), dim3(256), 0, st, p->d_segs, p->d_large,
+                           bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws);
+        e = ms_select(b, maxn, p->d_keys, nullptr, true, p->d_mws, rowlist, nullptr, slotmap, st);
+        if (e) return e;
     }
     return (int)hipGetLastError();
 }

@@ -39,7 +39,12 @@ struct SegDev {
     int32_t kind;
     int32_t vec;       // 1: m % 4 == 0 and offset % 4 == 0 and packed_off % 4 == 0
     FastDiv mdiv;      // division by m
+    uint32_t magic32;  // ceil(2^32 / m): exact quotient for x < 2^32 / m (in-tile indices)
+    uint32_t pad2;
 };
+
+__device__ __forceinline__ uint32_t div32(uint32_t x, uint32_t magic) { return __umulhi(x, magic); }
+constexpr int kSmallTileRows = 1024;  // rows of a small-m pack/decode chunk (LDS slot table)
 
 // encode tile modes
 enum : int32_t { ENC_ROW_VEC = 0, ENC_ROW_SCALAR = 1, ENC_TILE = 2, ENC_RAW = 3 };
@@ -59,6 +64,8 @@ struct Chunk {         // pack: selected-row range; decode: row range
 };
 
 }  // namespace arctopk
+
+namespace arctopk { struct MBatch; struct MWorkspace; }
 
 struct arctopk_plan {
     int device;
@@ -84,4 +91,7 @@ struct arctopk_plan {
     int small_lds;                // bytes of LDS keys for the largest small segment
     int32_t* d_large;             // segments whose keys go through global memory
     int n_large;
+    arctopk::MBatch* h_large_batches;   // multi-block select items (host, by value at launch)
+    int n_large_batches;
+    arctopk::MWorkspace* d_mws;         // multi-block select workspace
 };

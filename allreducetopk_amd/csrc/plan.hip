@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "common.h"
+#include "mselect.h"
 
 using namespace arctopk;
 
@@ -105,6 +106,8 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         g.row_off = s.row_off; g.sel_off = s.sel_off; g.kind = s.kind;
         g.vec = (s.m % 4 == 0 && s.offset % 4 == 0 && s.packed_off % 4 == 0) ? 1 : 0;
         g.mdiv = make_fastdiv((uint32_t)s.m);
+        g.magic32 = s.m > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)s.m - 1) / (uint64_t)s.m) : 0u;
+        g.pad2 = 0;
         if (s.n <= kSmallSelRows) {
             small_ids.push_back((int32_t)i);
             small_rows = std::max<int64_t>(small_rows, s.n);
@@ -130,17 +133,21 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             if (vbytes <= kVLdsMaxBytes) lds = std::max(lds, vbytes);
             else vlds = 0;
         }
-        // ---- pack chunks: selected rows, ~kChunkElems elements each
+        // ---- pack chunks: selected rows, ~kChunkElems elements each (small m: at most
+        //      kSmallTileRows rows, the size of the kernels' LDS row/slot table)
         pack_begin.push_back((int32_t)pack.size());
         dec_begin.push_back((int32_t)dec.size());
+        const bool small_tile = s.m >= 4 && s.m < 256;
         {
             int64_t per = std::max<int64_t>(1, kChunkElems / s.m);
+            if (small_tile) per = std::min<int64_t>(per, kSmallTileRows);
             for (int64_t j = 0; j < s.k_rows; j += per)
                 pack.push_back(Chunk{(int32_t)i, 0, j, std::min(per, s.k_rows - j)});
         }
         // ---- decode chunks: all rows
         {
             int64_t per = std::max<int64_t>(1, kChunkElems / s.m);
+            if (small_tile) per = std::min<int64_t>(per, kSmallTileRows);
             for (int64_t row = 0; row < s.n; row += per)
                 dec.push_back(Chunk{(int32_t)i, 0, row, std::min(per, s.n - row)});
         }
@@ -185,6 +192,20 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     ALLOC_COPY(p->d_dec, dec);
     ALLOC_COPY(p->d_small, small_ids);
     ALLOC_COPY(p->d_large, large_ids);
+    if (!large_ids.empty()) {
+        p->n_large_batches = (int)((large_ids.size() + kMB - 1) / kMB);
+        p->h_large_batches = new MBatch[p->n_large_batches];
+        for (int bi = 0; bi < p->n_large_batches; ++bi) {
+            MBatch& b = p->h_large_batches[bi];
+            b.cnt = (int32_t)std::min<size_t>(kMB, large_ids.size() - (size_t)bi * kMB);
+            for (int i = 0; i < b.cnt; ++i) {
+                const arctopk_segment& sg = segs[large_ids[(size_t)bi * kMB + i]];
+                b.it[i] = MItem{sg.row_off, sg.n, sg.k_rows, sg.sel_off, sg.row_off};
+            }
+        }
+        e = hipMalloc((void**)&p->d_mws, sizeof(MWorkspace));
+        if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
+    }
 #undef ALLOC_COPY
     e = hipMalloc((void**)&p->d_keys, std::max<size_t>(4, info.rows_total * sizeof(uint32_t)));
     if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
@@ -218,6 +239,8 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_large) (void)hipFree(p->d_large);
     delete[] p->h_segs;
     delete[] p->h_pack_begin;
+    delete[] p->h_large_batches;
+    if (p->d_mws) (void)hipFree(p->d_mws);
     delete[] p->h_dec_begin;
     delete p;
     return 0;

@@ -23,6 +23,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 MIX = [[10], [40, 16], [4, 3, 3, 3], [16, 8, 3, 3], [16, 8, 1, 1], [96, 40], [7], [256, 512],
        [33, 130], [1000], [64, 70], [8, 8, 5, 5], [130, 2048]]
+# Segments past the single-block select (> 15360 rows): multi-block radix select, and more
+# of them than one select batch holds (48).
+LARGE = [[20000, 8], [30], [512, 512, 3, 3], [16000, 3], [7, 9]] + [[15400, 2]] * 50
+SHAPE_SETS = {"mix": MIX, "large": LARGE}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -52,10 +56,11 @@ def test_plan_geometry_matches_oracle():
     assert plan.info.packed_len == sum(o.k for o in segs)
 
 
-@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
-def test_kernel_phases_bitexact(ef):
+@pytest.mark.parametrize("ef,which", [("noef", "mix"), ("ef14", "mix"), ("ef21", "mix"),
+                                      ("ef14", "large"), ("ef21", "large")])
+def test_kernel_phases_bitexact(ef, which):
     """encode -> select (fed the oracle's sketch) -> pack -> decode, phase by phase."""
-    shapes = MIX
+    shapes = SHAPE_SETS[which]
     segs = A.segments(shapes, 0.2)
     plan = BucketPlan([tuple(s) for s in shapes], 4, 0.2, torch.float32, DEV)
     G = _rand_bucket(shapes, 1)
@@ -128,9 +133,10 @@ def test_kernel_phases_bitexact(ef):
     assert_bitwise(out, ref_out, "decoded bucket")
 
 
-@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
-def test_hook_end_to_end_vs_oracle(ef):
-    shapes = MIX
+@pytest.mark.parametrize("ef,which", [("noef", "mix"), ("ef14", "mix"), ("ef21", "mix"),
+                                      ("ef14", "large")])
+def test_hook_end_to_end_vs_oracle(ef, which):
+    shapes = SHAPE_SETS[which]
     numel = bucket_numel(shapes)
     st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                         use_error_feedback=ef, seed=1234)

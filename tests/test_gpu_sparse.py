@@ -12,6 +12,9 @@ from parity import assert_bitwise, check_rows_tie_aware, ensure_group
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 SHAPES = [[10], [40, 16], [4, 3, 3, 3], [96, 40], [256, 512], [1000], [3, 7]]
+# more tensors than one select batch (48), and tensors large enough for many hist blocks
+LARGE = [[300000], [3, 5], [1000, 300], [512, 64, 3, 3]] + [[2000]] * 60
+SHAPE_SETS = {"small": SHAPES, "large": LARGE}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -25,19 +28,21 @@ def _rand(shapes, seed):
     return torch.randn(bucket_numel(shapes), generator=g)
 
 
-@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
-def test_topk_hook_vs_oracle(ef):
+@pytest.mark.parametrize("ef,which", [("noef", "small"), ("ef14", "small"), ("ef21", "small"),
+                                      ("ef14", "large"), ("ef21", "large")])
+def test_topk_hook_vs_oracle(ef, which):
+    shapes = SHAPE_SETS[which]
     st = sparse_hook.SparseState(None, compress_ratio=0.2, start_compress_iter=0,
                                  sparse_type="tensor", random=False, use_error_feedback=ef)
     E = gE = None
     for it in range(3):
-        G = _rand(SHAPES, 50 + it)
-        out = sparse_hook.sparse_hook_sync(st, SyntheticBucket(G.to(DEV), SHAPES)).wait()
+        G = _rand(shapes, 50 + it)
+        out = sparse_hook.sparse_hook_sync(st, SyntheticBucket(G.to(DEV), shapes)).wait()
         torch.cuda.synchronize()
         if ef == "ef21" and E is None:
             E, gE = G.clone(), G.clone()
             continue
-        res = S.simulate_step([G], [E if not (ef == "ef14" and E is None) else None], gE, SHAPES,
+        res = S.simulate_step([G], [E if not (ef == "ef14" and E is None) else None], gE, shapes,
                               0.2, ef, False, None)
         assert_bitwise(out, res["out"], f"it{it} out")
         if ef != "noef":
