@@ -53,7 +53,7 @@ _SIGS = {
                                         c_void_p, c_void_p, c_void_p]),
     "arctopk_decode_segments": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int32,
                                           c_int32, c_void_p, c_void_p, c_void_p]),
-    "arctopk_sparse_workspace_bytes": (c_int64, []),
+    "arctopk_sparse_workspace_bytes": (c_int64, [c_int32, POINTER(c_int64)]),
     "arctopk_topk_select": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
                                       POINTER(c_int64), POINTER(c_int64), c_void_p, c_void_p, c_void_p,
                                       c_void_p]),

@@ -201,6 +201,10 @@ class GroupTopKState(HookState):
         self.host_staged = False
         self._host_buf = None
 
+    def _after_load(self) -> None:
+        # prefetched projections were keyed on seeds of the old rng position
+        self._proj.reset()
+
     def _plan_for(self, bucket) -> BucketPlan:
         buf = bucket.buffer()
         grads = bucket.gradients()

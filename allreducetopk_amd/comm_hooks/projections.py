@@ -126,6 +126,13 @@ class ProjectionSource:
             for key in [k for k in self._pending if k not in live]:  # stale predictions
                 self._pending.pop(key)
 
+    def reset(self):
+        """Forget the seed look-ahead and pending draws (the rng was repositioned)."""
+        with self._lock:
+            self._pending.clear()
+        self._lookahead = None
+        self._future_seeds.clear()
+
     def close(self):
         if self._pool is not None:
             self._pool.shutdown(wait=False, cancel_futures=True)

@@ -70,6 +70,7 @@ class SparseState(HookState):
             raise ValueError("index_source must be 'torch' or 'hash'")
         self.index_source = index_source
         self._workspace = None
+        self._ws_bytes: Dict[tuple, int] = {}
 
     # ratio of this call; the c4 variant overrides (gradual compression)
     def _call_ratio(self) -> float:
@@ -79,10 +80,17 @@ class SparseState(HookState):
         pass
 
 
-def _workspace(state, device) -> torch.Tensor:
+def _workspace(state, device, numels) -> torch.Tensor:
+    """Select workspace for this bucket's tensor sizes (grown, never shrunk)."""
+    key = tuple(numels)
+    nbytes = state._ws_bytes.get(key)
+    if nbytes is None:
+        nbytes = int(N.lib().arctopk_sparse_workspace_bytes(len(numels), N.i64_array(numels)))
+        if nbytes < 0:
+            N.check(-nbytes, "arctopk_sparse_workspace_bytes")
+        state._ws_bytes[key] = nbytes
     ws = state._workspace
-    if ws is None or ws.device != device:
-        nbytes = int(N.lib().arctopk_sparse_workspace_bytes())
+    if ws is None or ws.device != device or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
         state._workspace = ws
     return ws
@@ -176,7 +184,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
                                         values.data_ptr(), stream), "arctopk_sparse_gather")
         bits_sum = sum_k * dtype_bits(dtype)
     else:
-        ws_buf = _workspace(state, device)
+        ws_buf = _workspace(state, device, numels)
         N.check(L.arctopk_topk_select(x, nt, a_off, a_n, a_k, a_ko, indices.data_ptr(),
                                       values.data_ptr(), ws_buf.data_ptr(), stream),
                 "arctopk_topk_select")

@@ -81,6 +81,46 @@ class HookState:
                 logger.info("Start to apply %s hook after %s iterations.", self.compressor_name,
                             self.start_compress_iter)
 
+    # -- checkpointing (not in the reference, which loses E / gE / rng on resume) --------
+    _CKPT_SCALARS = ("iter", "comm_bits_this_round", "total_bit_before_compression",
+                     "total_bit_after_compression", "adam_freeze_key")
+
+    def state_dict(self) -> dict:
+        """Everything a resumed run needs to continue bit-identically.
+
+        Scalars, the seed generator's state (``rng``, when the state has one) and the
+        per-bucket residuals ``error_dict`` / ``global_error_dict`` (EF14 / EF21), as
+        references to the live tensors -- ``torch.save`` copies them.  Loadable with
+        ``torch.load(..., weights_only=True)``.
+        """
+        out = {k: getattr(self, k) for k in self._CKPT_SCALARS}
+        rng = getattr(self, "rng", None)
+        if rng is not None:
+            out["rng_state"] = rng.get_state()
+        for name in ("error_dict", "global_error_dict"):
+            d = getattr(self, name, None)
+            if d is not None:
+                out[name] = {int(b): t for b, t in d.items()}
+        return out
+
+    def load_state_dict(self, sd: dict, device=None) -> None:
+        """Restore :meth:`state_dict`; residuals are copied to ``device`` when given."""
+        for k in self._CKPT_SCALARS:
+            if k in sd:
+                setattr(self, k, sd[k])
+        if "rng_state" in sd:
+            if getattr(self, "rng", None) is None:
+                raise KeyError("checkpoint holds an rng state but this hook state has no rng")
+            self.rng.set_state(sd["rng_state"])
+        for name in ("error_dict", "global_error_dict"):
+            if name in sd:
+                setattr(self, name, {int(b): (t.to(device) if device is not None else t).clone()
+                                     for b, t in sd[name].items()})
+        self._after_load()
+
+    def _after_load(self) -> None:
+        """Hook for subclasses holding derived state (look-ahead seeds etc.)."""
+
     def compression_bits_stats(self):
         rate = (self.total_bit_before_compression / self.total_bit_after_compression
                 if self.total_bit_after_compression > 0 else 0)

@@ -972,7 +972,8 @@ extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_
         const int gx = (int)std::min<int64_t>(512, (maxn + 255) / 256);
         hipLaunchKernelGGL(k_arc_keys, dim3(gx, b.cnt), dim3(256), 0, st, p->d_segs, p->d_large,
                            bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws);
-        e = ms_select(b, maxn, p->d_keys, nullptr, true, p->d_mws, rowlist, nullptr, slotmap, st);
+        e = ms_select(b, maxn, p->d_keys, nullptr, true, p->d_mws, p->mws_cap, rowlist, nullptr,
+                      slotmap, st);
         if (e) return e;
     }
     return (int)hipGetLastError();

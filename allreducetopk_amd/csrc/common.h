@@ -94,4 +94,5 @@ struct arctopk_plan {
     arctopk::MBatch* h_large_batches;   // multi-block select items (host, by value at launch)
     int n_large_batches;
     arctopk::MWorkspace* d_mws;         // multi-block select workspace
+    int64_t mws_cap;                    // its candidate slots
 };

@@ -8,20 +8,54 @@
 namespace arctopk {
 namespace {
 
+constexpr int kW1 = 12;  // first-pass digit width (kMBins = 1 << kW1)
+constexpr int kW2 = 10;  // refinement digit width (12 + 10 + 10 >= 32 key bits)
+constexpr int kPerLane = kMTile / 256;  // keys per lane of a tile (16)
+
 template <bool FROM_FLOAT>
-__device__ __forceinline__ uint32_t load_key(const uint32_t* __restrict__ keys,
-                                             const float* __restrict__ x, int64_t i) {
-    if constexpr (FROM_FLOAT) return __float_as_uint(x[i]) & 0x7FFFFFFFu;  // |x|; NaN above inf
+__device__ __forceinline__ uint32_t load_bits(const uint32_t* __restrict__ keys,
+                                              const float* __restrict__ x, int64_t i) {
+    if constexpr (FROM_FLOAT) return __float_as_uint(x[i]);
     else return keys[i];
 }
 
-// item start state.  FROM_FLOAT: |x| keys, only the sign bit is known.  Otherwise the
-// caller's key pass left the OR / AND of all keys in the state: their common leading
-// bits are fixed, so the first digit falls on varying bits.
+// |x| for TopK keys: NaN sorts above inf, as in the previous radix order
+template <bool FROM_FLOAT>
+__device__ __forceinline__ uint32_t key_of(uint32_t bits) {
+    if constexpr (FROM_FLOAT) return bits & 0x7FFFFFFFu;
+    else return bits;
+}
+
+__device__ __forceinline__ uint32_t popc64(uint64_t v) { return (uint32_t)__popcll(v); }
+
+// exclusive block scan of one uint32 per thread (NW waves); *total = block sum
+template <int NW>
+__device__ __forceinline__ uint32_t block_exscan_u32(uint32_t v, uint32_t* lds, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint32_t s = lds[w];
+        before += w < wave ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + x - v;
+}
+
 template <bool FROM_FLOAT>
 __global__ void k_ms_init(MBatch b, MWorkspace* ws) {
     const int t = blockIdx.x;
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) ws->hist[t][i] = 0;
+    for (int i = threadIdx.x; i < kMBins; i += blockDim.x) ws->hist[t][i] = 0;
     if (threadIdx.x == 0) {
         MState& s = ws->st[t];
         if constexpr (FROM_FLOAT) {
@@ -29,6 +63,7 @@ __global__ void k_ms_init(MBatch b, MWorkspace* ws) {
             s.mask = 0x80000000u;
             s.bit = 31;
         } else {
+            // common leading bits of all keys are decided from the start
             const uint32_t diff = s.kor ^ s.kand;
             const int bit = diff ? 32 - __clz(diff) : 0;
             const uint32_t low = bit == 32 ? 0xFFFFFFFFu : ((1u << bit) - 1u);
@@ -37,6 +72,10 @@ __global__ void k_ms_init(MBatch b, MWorkspace* ws) {
             s.bit = bit;
         }
         s.kk = b.it[t].k;
+        s.cand = 0;
+        s.ncand = 0;
+        s.p1 = s.prefix;
+        s.m1 = s.mask;
     }
 }
 
@@ -48,224 +87,358 @@ __global__ void k_ms_reset_orand(MWorkspace* ws, int cnt) {
     }
 }
 
-template <bool FROM_FLOAT>
+// Histogram of the next min(W, bit) undecided bits of the keys matching the prefix:
+// PASS 0 scans every key of the item; later passes scan the candidates when the item
+// has them.  LDS histogram, merged with one global atomic per non-empty bin.
+template <bool FROM_FLOAT, int PASS>
 __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __restrict__ keys,
-                                                 const float* __restrict__ x, MWorkspace* ws) {
-    __shared__ uint32_t h[4][256];  // one copy per wave: fewer same-address atomics
+                                                 const float* __restrict__ x, MWorkspace* ws,
+                                                 const uint32_t* __restrict__ ckey) {
+    constexpr int W = PASS == 0 ? kW1 : kW2;
+    __shared__ uint32_t h[1 << W];
     const int t = blockIdx.y;
     const MState s = ws->st[t];
     if (s.bit <= 0) return;
-    const int w = s.bit < 8 ? s.bit : 8;
+    const int w = s.bit < W ? s.bit : W;
     const int shift = s.bit - w;
     const uint32_t dmask = (1u << w) - 1u;
-    const int wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < 4 * 256; i += 256) (&h[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < (1 << W); i += 256) h[i] = 0;
     __syncthreads();
     const MItem it = b.it[t];
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < it.n; i += (int64_t)gridDim.x * 256) {
-        const uint32_t key = load_key<FROM_FLOAT>(keys, x, it.key_off + i);
-        if ((key & s.mask) == s.prefix) atomicAdd(&h[wave][(key >> shift) & dmask], 1u);
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (PASS > 0 && s.cand) {
+        const uint32_t* src = ckey + it.cand_off;
+        const int64_t n = s.ncand;
+        for (; i < n; i += stride) {
+            const uint32_t key = src[i];
+            if ((key & s.mask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
+        }
+    } else {
+        const int64_t n = it.n;
+        for (; i + 3 * stride < n; i += 4 * stride) {  // four loads in flight per lane
+            uint32_t k4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) k4[u] = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i + u * stride));
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if ((k4[u] & s.mask) == s.prefix) atomicAdd(&h[(k4[u] >> shift) & dmask], 1u);
+        }
+        for (; i < n; i += stride) {
+            const uint32_t key = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
+            if ((key & s.mask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
+        }
     }
     __syncthreads();
-    const uint32_t c = h[0][threadIdx.x] + h[1][threadIdx.x] + h[2][threadIdx.x] + h[3][threadIdx.x];
-    if (c) atomicAdd(&ws->hist[t][threadIdx.x], c);
+    for (int j = threadIdx.x; j <= (int)dmask; j += 256)
+        if (h[j]) atomicAdd(&ws->hist[t][j], h[j]);
 }
 
-__global__ void k_ms_digit(MBatch b, MWorkspace* ws) {
+// Pick the digit holding the kk-th largest key (bins scanned from the top), then clear
+// the histogram for the next pass.  PASS 0 also fixes the candidate bin and mode.
+template <int PASS>
+__global__ void __launch_bounds__(256) k_ms_digit(MBatch b, MWorkspace* ws) {
+    constexpr int W = PASS == 0 ? kW1 : kW2;
+    constexpr int PER = ((1 << W) + 255) / 256;
+    __shared__ uint32_t lds[4];
     const int t = blockIdx.x;
-    const int lane = threadIdx.x;
-    MState s = ws->st[t];
-    if (s.bit > 0) {
-        const int w = s.bit < 8 ? s.bit : 8;
-        const int shift = s.bit - w;
-        uint32_t c[4], sum = 0;
+    const MState s = ws->st[t];
+    if (s.bit <= 0) return;  // uniform per block
+    const int w = s.bit < W ? s.bit : W;
+    const int shift = s.bit - w;
+    const int nb = 1 << w;
+    const int per = (nb + 255) / 256;
+    uint32_t c[PER];
+    uint32_t sum = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            c[q] = ws->hist[t][255 - 4 * lane - q];
-            sum += c[q];
+    for (int q = 0; q < PER; ++q) {
+        const int bin = nb - 1 - ((int)threadIdx.x * per + q);
+        c[q] = (q < per && bin >= 0) ? ws->hist[t][bin] : 0u;
+        sum += c[q];
+    }
+    uint32_t total;
+    const uint32_t excl = block_exscan_u32<4>(sum, lds, &total);
+    const uint64_t kk = (uint64_t)s.kk;
+    if ((uint64_t)excl < kk && (uint64_t)excl + sum >= kk) {
+        uint64_t acc = excl;
+        int q = 0;
+        for (; q < per - 1; ++q) {
+            if (acc + c[q] >= kk) break;
+            acc += c[q];
         }
-        uint64_t incl = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        const uint64_t excl = incl - sum;
-        if (excl < (uint64_t)s.kk && incl >= (uint64_t)s.kk) {
-            uint64_t acc = excl;
-            int q = 0;
-            for (; q < 3; ++q) {
-                if (acc + c[q] >= (uint64_t)s.kk) break;
-                acc += c[q];
-            }
-            const uint32_t d = 255 - 4 * lane - q;
-            MState& g = ws->st[t];
-            g.prefix = s.prefix | (d << shift);
-            g.mask = s.mask | (((1u << w) - 1u) << shift);
-            g.kk = s.kk - (int64_t)acc;
-            g.bit = shift;
+        const uint32_t d = (uint32_t)(nb - 1 - ((int)threadIdx.x * per + q));
+        MState& g = ws->st[t];
+        const uint32_t prefix = s.prefix | (d << shift);
+        const uint32_t mask = s.mask | ((uint32_t)(nb - 1) << shift);
+        g.prefix = prefix;
+        g.mask = mask;
+        g.kk = s.kk - (int64_t)acc;
+        g.bit = shift;
+        if (PASS == 0) {
+            g.p1 = prefix;
+            g.m1 = mask;
+            g.cand = (int64_t)c[q] <= b.it[t].cand_cap ? 1 : 0;
         }
     }
-    __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ws->hist[t][4 * lane + q] = 0;
+    for (int q = 0; q < PER; ++q) {
+        const int bin = nb - 1 - ((int)threadIdx.x * per + q);
+        if (q < per && bin >= 0) ws->hist[t][bin] = 0u;
+    }
 }
 
+// One block per range: count of keys above the first-pass bin, and (candidate mode)
+// append the bin's keys + local indices to the item's candidate list.
 template <bool FROM_FLOAT>
-__global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __restrict__ keys,
-                                                  const float* __restrict__ x, MWorkspace* ws) {
-    __shared__ int64_t s_gt[4], s_eq[4];
+__global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __restrict__ keys,
+                                                    const float* __restrict__ x, MWorkspace* ws,
+                                                    uint32_t* __restrict__ ckey,
+                                                    uint32_t* __restrict__ cidx) {
+    __shared__ uint32_t lds[4];
     const int t = blockIdx.y;
     const MItem it = b.it[t];
-    const int64_t per = (it.n + kMRanges - 1) / kMRanges;
-    const int64_t r0 = min<int64_t>(it.n, blockIdx.x * per), r1 = min<int64_t>(it.n, r0 + per);
-    const uint32_t T = ws->st[t].prefix;
-    int64_t gt = 0, eq = 0;
-    for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
-        const uint32_t key = load_key<FROM_FLOAT>(keys, x, it.key_off + i);
-        gt += key > T;
-        eq += key == T;
-    }
+    const int r = blockIdx.x;
+    if (r >= it.nranges) return;
+    const MState s = ws->st[t];
+    const uint32_t hi = s.p1 | ~s.m1;  // largest key of the bin
+    const int64_t r0 = (int64_t)r * it.range;
+    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t gt = 0;
+    for (int64_t tile = r0; tile < r1; tile += kMTile) {
+        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
+        uint32_t kv[kPerLane];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        gt += __shfl_xor(gt, o, 64);
-        eq += __shfl_xor(eq, o, 64);
+        for (int j = 0; j < kPerLane; ++j)
+            kv[j] = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)));
+        uint32_t nin = 0;
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const bool valid = wb + j * 64 + lane < r1;
+            gt += (valid && kv[j] > hi) ? 1u : 0u;
+            if (s.cand) nin += popc64(__ballot(valid && (kv[j] & s.m1) == s.p1));
+        }
+        if (s.cand && nin) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&ws->st[t].ncand, nin);
+            base = __shfl(base, 0, 64);
+#pragma unroll
+            for (int j = 0; j < kPerLane; ++j) {
+                const int64_t i = wb + j * 64 + lane;
+                const bool in = i < r1 && (kv[j] & s.m1) == s.p1;
+                const uint64_t bm = __ballot(in);
+                if (in) {
+                    const uint32_t pos = base + popc64(bm & lt);
+                    ckey[it.cand_off + pos] = kv[j];
+                    cidx[it.cand_off + pos] = (uint32_t)i;
+                }
+                base += popc64(bm);
+            }
+        }
     }
-    if ((threadIdx.x & 63) == 0) {
-        s_gt[threadIdx.x >> 6] = gt;
-        s_eq[threadIdx.x >> 6] = eq;
-    }
-    __syncthreads();
+    uint32_t total;
+    (void)block_exscan_u32<4>(gt, lds, &total);
     if (threadIdx.x == 0) {
-        ws->cnt_gt[t][blockIdx.x] = s_gt[0] + s_gt[1] + s_gt[2] + s_gt[3];
-        ws->cnt_eq[t][blockIdx.x] = s_eq[0] + s_eq[1] + s_eq[2] + s_eq[3];
+        ws->cnt_gt[t][r] = total;
+        ws->cnt_eq[t][r] = 0u;
     }
 }
 
-__global__ void __launch_bounds__(kMRanges) k_ms_offsets(MBatch b, MWorkspace* ws) {
-    __shared__ int64_t buf[kMRanges];
+// Per-range counts of the bin's keys > T and == T (T = the final prefix): from the
+// candidates (atomics) or, in full mode, by rescanning each range's keys.
+template <bool FROM_FLOAT>
+__global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __restrict__ keys,
+                                                  const float* __restrict__ x, MWorkspace* ws,
+                                                  const uint32_t* __restrict__ ckey,
+                                                  const uint32_t* __restrict__ cidx) {
+    __shared__ uint32_t lds[4];
+    const int t = blockIdx.y;
+    const MItem it = b.it[t];
+    const MState s = ws->st[t];
+    const uint32_t T = s.prefix;
+    if (s.cand) {
+        const int64_t n = s.ncand;
+        for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < n; c += (int64_t)gridDim.x * 256) {
+            const uint32_t key = ckey[it.cand_off + c];
+            if (key >= T) {
+                const int r = (int)(cidx[it.cand_off + c] / (uint32_t)it.range);
+                atomicAdd(key > T ? &ws->cnt_gt[t][r] : &ws->cnt_eq[t][r], 1u);
+            }
+        }
+        return;
+    }
+    for (int r = blockIdx.x; r < it.nranges; r += gridDim.x) {
+        const int64_t r0 = (int64_t)r * it.range;
+        const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+        uint32_t gt = 0, eq = 0;
+        for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+            const uint32_t key = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
+            const bool in = (key & s.m1) == s.p1;
+            gt += (in && key > T) ? 1u : 0u;
+            eq += key == T ? 1u : 0u;
+        }
+        uint32_t tg, te;
+        (void)block_exscan_u32<4>(gt, lds, &tg);
+        (void)block_exscan_u32<4>(eq, lds, &te);
+        if (threadIdx.x == 0) {
+            ws->cnt_gt[t][r] += tg;
+            ws->cnt_eq[t][r] = te;
+        }
+    }
+}
+
+// Per item: T-equal allowance per range (lowest ranges first) and output offsets.
+__global__ void __launch_bounds__(kMMaxRanges) k_ms_offsets(MBatch b, MWorkspace* ws) {
+    __shared__ uint32_t lds[kMMaxRanges / 64];
     const int t = blockIdx.x;
     const int i = threadIdx.x;
-    const int64_t eq = ws->cnt_eq[t][i];
-    buf[i] = eq;
-    __syncthreads();
-    for (int o = 1; o < kMRanges; o <<= 1) {
-        const int64_t y = i >= o ? buf[i - o] : 0;
-        __syncthreads();
-        buf[i] += y;
-        __syncthreads();
-    }
-    const int64_t eq_before = buf[i] - eq;
+    const int nr = b.it[t].nranges;
+    const uint32_t eq = i < nr ? ws->cnt_eq[t][i] : 0u;
+    uint32_t tot;
+    const uint32_t eq_before = block_exscan_u32<kMMaxRanges / 64>(eq, lds, &tot);
     const int64_t need = ws->st[t].kk;
-    int64_t take = need - eq_before;
+    int64_t take = need - (int64_t)eq_before;
     take = take < 0 ? 0 : (take > eq ? eq : take);
-    ws->take_eq[t][i] = take;
-    const int64_t sel = ws->cnt_gt[t][i] + take;
-    __syncthreads();
-    buf[i] = sel;
-    __syncthreads();
-    for (int o = 1; o < kMRanges; o <<= 1) {
-        const int64_t y = i >= o ? buf[i - o] : 0;
-        __syncthreads();
-        buf[i] += y;
-        __syncthreads();
+    const uint32_t sel = (i < nr ? ws->cnt_gt[t][i] : 0u) + (uint32_t)take;
+    const uint32_t sel_before = block_exscan_u32<kMMaxRanges / 64>(sel, lds, &tot);
+    if (i < nr) {
+        ws->take_eq[t][i] = (uint32_t)take;
+        ws->sel_before[t][i] = sel_before;
     }
-    ws->sel_before[t][i] = buf[i] - sel;
 }
 
-// ARC: rows[out_off + slot] = i and slots[slot_off + i] = slot | -1 for every key.
-// TopK: idx[out_off + slot] = i, vals[out_off + slot] = x[key_off + i].
+// One block per range, 4096-key tiles (each wave a contiguous 1024 keys, 16 per lane):
+// ballot compaction in index order.  ARC: rows[out_off + slot] = i and the slot map for
+// every key; TopK: idx[out_off + slot] = i, vals[out_off + slot] = x[key_off + i].
 template <bool FROM_FLOAT, bool ARC>
 __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __restrict__ keys,
                                                   const float* __restrict__ x, MWorkspace* ws,
                                                   int32_t* __restrict__ out_idx,
                                                   float* __restrict__ out_val,
                                                   int32_t* __restrict__ out_slot) {
-    __shared__ uint32_t s_sel[4], s_eq[4];
+    __shared__ uint32_t s_eq[4], s_gt[4];
     const int t = blockIdx.y;
     const MItem it = b.it[t];
-    const int64_t per = (it.n + kMRanges - 1) / kMRanges;
-    const int64_t r0 = min<int64_t>(it.n, blockIdx.x * per), r1 = min<int64_t>(it.n, r0 + per);
+    const int r = blockIdx.x;
+    if (r >= it.nranges) return;
     const uint32_t T = ws->st[t].prefix;
-    const int64_t take_eq = ws->take_eq[t][blockIdx.x];
-    int64_t slot = ws->sel_before[t][blockIdx.x];
-    int64_t eq_seen = 0;
+    uint32_t take_left = ws->take_eq[t][r];
+    int64_t run = ws->sel_before[t][r];
+    const int64_t r0 = (int64_t)r * it.range;
+    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int64_t base = r0; base < r1; base += 256) {
-        const int64_t i = base + threadIdx.x;
-        const bool in = i < r1;
-        uint32_t key = 0;
-        float v = 0.f;
-        if (in) {
-            if constexpr (FROM_FLOAT) {
-                v = x[it.key_off + i];
-                key = __float_as_uint(v) & 0x7FFFFFFFu;
-            } else {
-                key = keys[it.key_off + i];
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int64_t tile = r0; tile < r1; tile += kMTile) {
+        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
+        uint32_t bits[kPerLane];
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j)
+            bits[j] = load_bits<FROM_FLOAT>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1));
+        uint32_t weq = 0, wgt = 0;
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const bool valid = wb + j * 64 + lane < r1;
+            const uint32_t key = key_of<FROM_FLOAT>(bits[j]);
+            weq += popc64(__ballot(valid && key == T));
+            wgt += popc64(__ballot(valid && key > T));
+        }
+        if (lane == 0) {
+            s_eq[wave] = weq;
+            s_gt[wave] = wgt;
+        }
+        __syncthreads();
+        uint32_t eqb = 0, gtb = 0, teq = 0, tgt = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            eqb += w < wave ? s_eq[w] : 0u;
+            gtb += w < wave ? s_gt[w] : 0u;
+            teq += s_eq[w];
+            tgt += s_gt[w];
+        }
+        __syncthreads();
+        uint32_t run_eq = eqb;
+        int64_t run_sel = run + gtb + min(eqb, take_left);
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const int64_t i = wb + j * 64 + lane;
+            const bool valid = i < r1;
+            const uint32_t key = key_of<FROM_FLOAT>(bits[j]);
+            const bool eq = valid && key == T;
+            const bool gt = valid && key > T;
+            const uint64_t beq = __ballot(eq);
+            const bool sel = gt || (eq && run_eq + popc64(beq & lt) < take_left);
+            const uint64_t bsel = __ballot(sel);
+            const int64_t my = run_sel + popc64(bsel & lt);
+            if (sel && my < it.k) {  // bound: never store past the item's k outputs
+                out_idx[it.out_off + my] = (int32_t)i;
+                if constexpr (!ARC) out_val[it.out_off + my] = __uint_as_float(bits[j]);
             }
+            if constexpr (ARC) {
+                if (valid) out_slot[it.slot_off + i] = sel ? (int32_t)my : -1;
+            }
+            run_eq += popc64(beq);
+            run_sel += popc64(bsel);
         }
-        const bool gt = in && key > T;
-        const bool eq = in && key == T;
-        const uint64_t beq = __ballot(eq);
-        if (lane == 0) s_eq[wave] = __popcll(beq);
-        __syncthreads();
-        uint32_t eq_rank = __popcll(beq & lt);
-        for (int w = 0; w < wave; ++w) eq_rank += s_eq[w];
-        const uint32_t eq_tile = s_eq[0] + s_eq[1] + s_eq[2] + s_eq[3];
-        const bool sel = gt || (eq && (eq_seen + eq_rank) < take_eq);
-        const uint64_t bsel = __ballot(sel);
-        if (lane == 0) s_sel[wave] = __popcll(bsel);
-        __syncthreads();
-        uint32_t sel_rank = __popcll(bsel & lt);
-        for (int w = 0; w < wave; ++w) sel_rank += s_sel[w];
-        const uint32_t sel_tile = s_sel[0] + s_sel[1] + s_sel[2] + s_sel[3];
-        const int64_t my = slot + sel_rank;
-        if (sel && my < it.k) {  // bound: never store past the item's k outputs
-            out_idx[it.out_off + my] = (int32_t)i;
-            if constexpr (!ARC) out_val[it.out_off + my] = v;
-        }
-        if constexpr (ARC) {
-            if (in) out_slot[it.slot_off + i] = sel ? (int32_t)my : -1;
-        }
-        slot += sel_tile;
-        eq_seen += eq_tile;
-        __syncthreads();
+        const uint32_t te = min(teq, take_left);
+        run += tgt + te;
+        take_left -= te;
     }
 }
 
 }  // namespace
 
+void ms_item_geometry(MItem& it) {
+    const int64_t tiles = (it.n + kMTile - 1) / kMTile;
+    const int64_t per = std::max<int64_t>(1, (tiles + kMMaxRanges - 1) / kMMaxRanges);
+    it.range = (int32_t)(per * kMTile);
+    it.nranges = (int32_t)((it.n + it.range - 1) / it.range);
+    // candidates: the k-th key's 12-bit bin; a few % of n on gradient-like data, all of
+    // n on degenerate data (e.g. a zero tensor) -> full mode past the cap
+    it.cand_cap = it.n <= 65536 ? it.n : std::max<int64_t>(65536, it.n / 8);
+}
+
+int64_t ms_workspace_bytes(int64_t cap_total) {
+    return (int64_t)sizeof(MWorkspace) + 8 * cap_total;
+}
+
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* x, bool arc,
-              MWorkspace* ws, int32_t* out_idx, float* out_val, int32_t* out_slot,
-              hipStream_t st) {
+              MWorkspace* ws, int64_t cap_total, int32_t* out_idx, float* out_val,
+              int32_t* out_slot, hipStream_t st) {
     const int cnt = b.cnt;
     if (cnt < 1) return 0;
-    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + 1023) / 1024));
-    if (arc) {
-        hipLaunchKernelGGL(k_ms_init<false>, dim3(cnt), dim3(256), 0, st, b, ws);
-    } else {
-        hipLaunchKernelGGL(k_ms_init<true>, dim3(cnt), dim3(256), 0, st, b, ws);
+    int gr = 1;
+    for (int i = 0; i < cnt; ++i) {
+        const MItem& it = b.it[i];
+        if (it.nranges < 1 || it.nranges > kMMaxRanges || it.cand_off < 0 ||
+            it.cand_off + it.cand_cap > cap_total || (int64_t)it.range * it.nranges < it.n)
+            return 1001;  // ARCTOPK_EINVAL: geometry not from ms_item_geometry
+        gr = std::max(gr, it.nranges);
     }
-    for (int pass = 0; pass < 4; ++pass) {
-        if (arc)
-            hipLaunchKernelGGL(k_ms_hist<false>, dim3(hb, cnt), dim3(256), 0, st, b, keys, x, ws);
-        else
-            hipLaunchKernelGGL(k_ms_hist<true>, dim3(hb, cnt), dim3(256), 0, st, b, keys, x, ws);
-        hipLaunchKernelGGL(k_ms_digit, dim3(cnt), dim3(64), 0, st, b, ws);
-    }
-    if (arc) {
-        hipLaunchKernelGGL(k_ms_count<false>, dim3(kMRanges, cnt), dim3(256), 0, st, b, keys, x, ws);
-    } else {
-        hipLaunchKernelGGL(k_ms_count<true>, dim3(kMRanges, cnt), dim3(256), 0, st, b, keys, x, ws);
-    }
-    hipLaunchKernelGGL(k_ms_offsets, dim3(cnt), dim3(kMRanges), 0, st, b, ws);
+    uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
+    uint32_t* cidx = ckey + cap_total;
+    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + kMTile - 1) / kMTile));
+    const dim3 gh(hb, cnt), gt(gr, cnt);
+#define MS_LAUNCH(FF, AR)                                                                              \
+    do {                                                                                               \
+        hipLaunchKernelGGL(k_ms_init<FF>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
+        hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
+        hipLaunchKernelGGL(k_ms_digit<0>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
+        hipLaunchKernelGGL(k_ms_compact<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);        \
+        hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
+        hipLaunchKernelGGL(k_ms_digit<1>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
+        hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
+        hipLaunchKernelGGL(k_ms_digit<2>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
+        hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);          \
+        hipLaunchKernelGGL(k_ms_offsets, dim3(cnt), dim3(kMMaxRanges), 0, st, b, ws);                  \
+        hipLaunchKernelGGL((k_ms_write<FF, AR>), gt, dim3(256), 0, st, b, keys, x, ws, out_idx,        \
+                           out_val, out_slot);                                                         \
+    } while (0)
     if (arc)
-        hipLaunchKernelGGL((k_ms_write<false, true>), dim3(kMRanges, cnt), dim3(256), 0, st, b, keys,
-                           x, ws, out_idx, out_val, out_slot);
+        MS_LAUNCH(false, true);
     else
-        hipLaunchKernelGGL((k_ms_write<true, false>), dim3(kMRanges, cnt), dim3(256), 0, st, b, keys,
-                           x, ws, out_idx, out_val, out_slot);
+        MS_LAUNCH(true, false);
+#undef MS_LAUNCH
     return (int)hipGetLastError();
 }
 

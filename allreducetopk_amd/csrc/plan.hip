@@ -198,12 +198,22 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         for (int bi = 0; bi < p->n_large_batches; ++bi) {
             MBatch& b = p->h_large_batches[bi];
             b.cnt = (int32_t)std::min<size_t>(kMB, large_ids.size() - (size_t)bi * kMB);
+            int64_t cap = 0;
             for (int i = 0; i < b.cnt; ++i) {
                 const arctopk_segment& sg = segs[large_ids[(size_t)bi * kMB + i]];
-                b.it[i] = MItem{sg.row_off, sg.n, sg.k_rows, sg.sel_off, sg.row_off};
+                MItem& it = b.it[i];
+                it.key_off = sg.row_off;
+                it.n = sg.n;
+                it.k = sg.k_rows;
+                it.out_off = sg.sel_off;
+                it.slot_off = sg.row_off;
+                ms_item_geometry(it);
+                it.cand_off = cap;
+                cap += it.cand_cap;
             }
+            p->mws_cap = std::max(p->mws_cap, cap);
         }
-        e = hipMalloc((void**)&p->d_mws, sizeof(MWorkspace));
+        e = hipMalloc((void**)&p->d_mws, (size_t)ms_workspace_bytes(p->mws_cap));
         if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
     }
 #undef ALLOC_COPY

@@ -145,8 +145,27 @@ inline int grid_for(int64_t work, int cap) {
 
 }  // namespace
 
-extern "C" int64_t arctopk_sparse_workspace_bytes(void) {
-    return (int64_t)sizeof(arctopk::MWorkspace);
+// candidate slots the TopK select needs: the largest per-batch sum of item capacities
+static int64_t topk_cap_total(int32_t nt, const int64_t* numels) {
+    int64_t best = 0;
+    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
+        int64_t cap = 0;
+        for (int32_t j = first; j < std::min<int32_t>(nt, first + arctopk::kMB); ++j) {
+            arctopk::MItem it{};
+            it.n = std::max<int64_t>(1, numels[j]);
+            arctopk::ms_item_geometry(it);
+            cap += it.cand_cap;
+        }
+        best = std::max(best, cap);
+    }
+    return best;
+}
+
+extern "C" int64_t arctopk_sparse_workspace_bytes(int32_t nt, const int64_t* numels) {
+    if (nt < 1 || !numels) return -(int64_t)ARCTOPK_EINVAL;
+    for (int32_t j = 0; j < nt; ++j)
+        if (numels[j] < 1 || numels[j] >= (1ll << 31)) return -(int64_t)ARCTOPK_EINVAL;
+    return arctopk::ms_workspace_bytes(topk_cap_total(nt, numels));
 }
 
 extern "C" int arctopk_topk_select(const float* x, int32_t nt, const int64_t* offsets,
@@ -154,20 +173,30 @@ extern "C" int arctopk_topk_select(const float* x, int32_t nt, const int64_t* of
                                    int32_t* idx, float* vals, void* workspace, void* stream) {
     if (!x || !offsets || !numels || !ks || !k_off || !idx || !vals || !workspace || nt < 1)
         return ARCTOPK_EINVAL;
+    for (int32_t j = 0; j < nt; ++j)
+        if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j])
+            return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     arctopk::MWorkspace* ws = (arctopk::MWorkspace*)workspace;
+    const int64_t cap_total = topk_cap_total(nt, numels);
     for (int32_t first = 0; first < nt; first += arctopk::kMB) {
         arctopk::MBatch b;
         b.cnt = std::min<int32_t>(arctopk::kMB, nt - first);
-        int64_t maxn = 0;
+        int64_t maxn = 0, cap = 0;
         for (int i = 0; i < b.cnt; ++i) {
             const int j = first + i;
-            if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j])
-                return ARCTOPK_EINVAL;
-            b.it[i] = arctopk::MItem{offsets[j], numels[j], ks[j], k_off[j], 0};
+            arctopk::MItem& it = b.it[i];
+            it.key_off = offsets[j];
+            it.n = numels[j];
+            it.k = ks[j];
+            it.out_off = k_off[j];
+            it.slot_off = 0;
+            arctopk::ms_item_geometry(it);
+            it.cand_off = cap;
+            cap += it.cand_cap;
             maxn = std::max(maxn, numels[j]);
         }
-        int e = arctopk::ms_select(b, maxn, nullptr, x, false, ws, idx, vals, nullptr, st);
+        int e = arctopk::ms_select(b, maxn, nullptr, x, false, ws, cap_total, idx, vals, nullptr, st);
         if (e) return e;
     }
     return 0;

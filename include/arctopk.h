@@ -175,8 +175,12 @@ int arctopk_decode_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t
  */
 #define ARCTOPK_SPARSE_MAX_BATCH 64
 
-/* bytes of `workspace` that arctopk_topk_select needs (independent of the tensors) */
-int64_t arctopk_sparse_workspace_bytes(void);
+/*
+ * Bytes of `workspace` that arctopk_topk_select needs for these tensor sizes (fixed
+ * tables plus a candidate list of ~n/8 per tensor of a launch batch), or
+ * -ARCTOPK_EINVAL for bad arguments.
+ */
+int64_t arctopk_sparse_workspace_bytes(int32_t ntensors, const int64_t* numels);
 
 /*
  * Exact element top-k of |x| per tensor by multi-block radix select; ties at the

@@ -62,7 +62,7 @@ kof = [sum(ks[:i]) for i in range(nt)]
 A_off, A_n, A_k, A_ko = N.i64_array(offs), N.i64_array(numel_t), N.i64_array(ks), N.i64_array(kof)
 sk_idx = torch.empty(sum(ks), dtype=torch.int32, device=dev)
 sk_val = torch.empty(sum(ks), device=dev)
-wsb = torch.empty(int(L.arctopk_sparse_workspace_bytes()), dtype=torch.uint8, device=dev)
+wsb = torch.empty(int(L.arctopk_sparse_workspace_bytes(len(ks), N.i64_array(numel_t))), dtype=torch.uint8, device=dev)
 KS = sum(ks)
 variants["sparse ef_apply ef14"] = (lambda: L.arctopk_ef_apply(a.data_ptr(), b.data_ptr(), n, N.EF14, 1, s), 12 * n)
 variants["topk_select (16 tensors)"] = (lambda: L.arctopk_topk_select(G.data_ptr(), nt, A_off, A_n, A_k, A_ko, sk_idx.data_ptr(), sk_val.data_ptr(), wsb.data_ptr(), s), 4 * 5 * n + 8 * KS)

@@ -33,7 +33,7 @@ kof = [sum(ks[:i]) for i in range(len(ks))]
 X = torch.randn(sum(numel_t), device=dev)
 idx = torch.empty(sum(ks), dtype=torch.int32, device=dev)
 val = torch.empty(sum(ks), device=dev)
-wsb = torch.empty(int(L.arctopk_sparse_workspace_bytes()), dtype=torch.uint8, device=dev)
+wsb = torch.empty(int(L.arctopk_sparse_workspace_bytes(len(ks), N.i64_array(numel_t))), dtype=torch.uint8, device=dev)
 for _ in range(REPS):
     N.check(L.arctopk_topk_select(X.data_ptr(), len(ks), N.i64_array(offs), N.i64_array(numel_t),
                                   N.i64_array(ks), N.i64_array(kof), idx.data_ptr(), val.data_ptr(),

@@ -258,3 +258,60 @@ def test_encode_rejects_bad_layout():
     st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0)
     with pytest.raises(RuntimeError):
         group_topk_hook(st, SyntheticBucket(buf, [[3, 5, 2], [70]]))  # 30 % 8 != 0
+
+
+@pytest.mark.parametrize("ef", ["ef14", "ef21"])
+def test_resume_from_state_dict_is_bit_identical(ef, tmp_path):
+    """Checkpoint the hook state after two calls, restore it into a fresh state (and a
+    fresh projection prefetcher) and continue: outputs and residuals match an
+    uninterrupted run bit for bit."""
+    shapes = MIX
+
+    def mk():
+        return GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                              use_error_feedback=ef, seed=55)
+
+    def call(st, it):
+        G = _rand_bucket(shapes, 300 + it).to(DEV)
+        out = group_topk_hook(st, SyntheticBucket(G, shapes, index=0, is_last=True)).wait()
+        torch.cuda.synchronize()
+        return out.clone()
+
+    ref = mk()
+    ref_outs = [call(ref, it) for it in range(4)]
+    a = mk()
+    for it in range(2):
+        call(a, it)
+    torch.save(a.state_dict(), tmp_path / "ck.pt")
+    b = mk()
+    b.load_state_dict(torch.load(tmp_path / "ck.pt", weights_only=True), device=DEV)
+    for it in range(2, 4):
+        assert_bitwise(call(b, it), ref_outs[it], f"resumed it{it}")
+    assert_bitwise(b.error_dict[0], ref.error_dict[0], "resumed E")
+    assert b.iter == ref.iter
+
+
+@pytest.mark.parametrize("fill", ["zero", "two_levels"])
+def test_select_degenerate_energies(fill):
+    """All-equal energies (zero gradients) and two energy levels on large segments: the
+    exact tie rule picks the lowest rows, through the full-rescan select path."""
+    shapes = [tuple(s) for s in LARGE[:5]]
+    segs = A.segments(shapes, 0.2)
+    plan = BucketPlan(shapes, 4, 0.2, torch.float32, DEV)
+    stream = torch.cuda.current_stream().cuda_stream
+    Ps = []
+    for s in segs:
+        if fill == "zero":
+            P = torch.zeros(s.n, 4)
+        else:
+            lv = (torch.arange(s.n) % 3 == 0).float() * 2.0 + 1.0
+            P = lv[:, None].expand(s.n, 4).contiguous()
+        Ps.append(P[:, 0].contiguous() if s.kind == A.RAW else P)
+    ref = torch.cat([p.flatten() for p in Ps])
+    plan.sketch[:ref.numel()].copy_(ref.to(DEV))
+    plan.select(1, stream)
+    torch.cuda.synchronize()
+    norms, _ = A.select(Ps, 1, segs)
+    for r_, nrm, s in zip(_gpu_rows(plan), norms, plan.segments):
+        assert check_rows_tie_aware(r_, nrm, int(s.k_rows), band=0.0) == 0
+        assert torch.all(r_[1:] > r_[:-1])

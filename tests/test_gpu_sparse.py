@@ -67,7 +67,8 @@ def test_topk_select_kernel_ties_and_order():
     xd = x.to(DEV)
     idx = torch.empty(k, dtype=torch.int32, device=DEV)
     vals = torch.empty(k, device=DEV)
-    ws = torch.empty(int(L.arctopk_sparse_workspace_bytes()), dtype=torch.uint8, device=DEV)
+    ws = torch.empty(int(L.arctopk_sparse_workspace_bytes(1, N.i64_array([n]))), dtype=torch.uint8,
+                     device=DEV)
     st = torch.cuda.current_stream().cuda_stream
     N.check(L.arctopk_topk_select(xd.data_ptr(), 1, N.i64_array([0]), N.i64_array([n]),
                                   N.i64_array([k]), N.i64_array([0]), idx.data_ptr(),
@@ -86,6 +87,44 @@ def test_topk_select_kernel_ties_and_order():
                                   vals2.data_ptr(), ws.data_ptr(), st), "topk_select")
     torch.cuda.synchronize()
     assert check_rows_tie_aware(idx2.cpu(), x.abs(), k2, band=0.0) == 0
+
+
+@pytest.mark.parametrize("case", ["constant", "mostly_zero", "two_values"])
+def test_topk_select_degenerate_large(case):
+    """Multi-range tensors whose k-th |x| bin is too full for the candidate list (the
+    select rescans the full tensor) and exact ties across many ranges."""
+    L = N.lib()
+    n = 3_000_000
+    g = torch.Generator().manual_seed(11)
+    if case == "constant":
+        x = torch.full((n,), -0.75)
+    elif case == "mostly_zero":
+        x = torch.zeros(n)
+        nz = torch.randperm(n, generator=g)[:200_000]
+        x[nz] = torch.randn(200_000, generator=g)
+    else:
+        x = torch.where(torch.rand(n, generator=g) < 0.5, torch.tensor(1.5), torch.tensor(-3.0))
+    k = 600_000
+    numels = [n, 5000]
+    ks = [k, 1000]
+    xd = torch.cat([x, torch.randn(5000, generator=g)]).to(DEV)
+    idx = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
+    vals = torch.empty(sum(ks), device=DEV)
+    ws = torch.empty(int(L.arctopk_sparse_workspace_bytes(2, N.i64_array(numels))), dtype=torch.uint8,
+                     device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    N.check(L.arctopk_topk_select(xd.data_ptr(), 2, N.i64_array([0, n]), N.i64_array(numels),
+                                  N.i64_array(ks), N.i64_array([0, k]), idx.data_ptr(),
+                                  vals.data_ptr(), ws.data_ptr(), st), "topk_select")
+    torch.cuda.synchronize()
+    i = idx.cpu().long()
+    xa = xd.cpu()
+    assert check_rows_tie_aware(i[:k], x.abs(), k, band=0.0) == 0
+    assert torch.all(i[1:k] > i[:k - 1])
+    assert torch.equal(vals.cpu()[:k], x[i[:k]])
+    assert check_rows_tie_aware(i[k:], xa[n:].abs(), 1000, band=0.0) == 0
+    if case == "constant":
+        assert torch.equal(i[:k], torch.arange(k))
 
 
 @pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])

@@ -180,3 +180,33 @@ def test_compressed_path_refuses_cpu_buckets():
         sparse_hook.sparse_hook_sync(sp, SyntheticBucket(torch.randn(640), [(40, 16)]))
     if owned:  # do not leak a CPU group into GPU tests collected in the same process
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("which", ["arc", "sparse"])
+def test_state_dict_roundtrip_weights_only(tmp_path, which):
+    """EF state checkpoint: scalars, rng position and residuals survive torch.save /
+    torch.load(weights_only=True); the restored rng continues the same seed sequence."""
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import GroupTopKState
+    from allreducetopk_amd.comm_hooks.sparse_hook import SparseState
+    mk = (lambda: GroupTopKState(None, r=4, compress_ratio=0.2, use_error_feedback="ef21", seed=9)) \
+        if which == "arc" else \
+        (lambda: SparseState(None, compress_ratio=0.2, use_error_feedback="ef21", random_seed=9))
+    st = mk()
+    st.iter = 17
+    st.comm_bits_this_round = 12345
+    st.error_dict = {0: torch.randn(100), 3: torch.randn(7)}
+    st.global_error_dict = {0: torch.randn(100)}
+    torch.randint(0, 10, (5,), generator=st.rng)  # move the rng
+    path = tmp_path / "hook.pt"
+    torch.save(st.state_dict(), path)
+    st2 = mk()
+    st2.load_state_dict(torch.load(path, weights_only=True))
+    assert st2.iter == 17 and st2.comm_bits_this_round == 12345
+    assert sorted(st2.error_dict) == [0, 3]
+    for b in st.error_dict:
+        assert torch.equal(st2.error_dict[b], st.error_dict[b])
+        assert st2.error_dict[b].data_ptr() != st.error_dict[b].data_ptr()
+    assert torch.equal(st2.global_error_dict[0], st.global_error_dict[0])
+    a = torch.randint(0, 1_000_000_000, (4,), generator=st.rng)
+    b = torch.randint(0, 1_000_000_000, (4,), generator=st2.rng)
+    assert torch.equal(a, b)
