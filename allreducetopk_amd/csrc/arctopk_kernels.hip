@@ -591,9 +591,30 @@ __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ seg
     const SegDev s = segs[ids[first + t]];
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
     uint32_t kor = 0u, kand = ~0u;
-    for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < s.n;
-         row += (int64_t)gridDim.x * 256) {
-        const uint32_t key = energy_key(row_energy(sketch + s.sketch_off + row * stride, R, sc, s.kind));
+    const int64_t gs = (int64_t)gridDim.x * 256;
+    int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const float* sk = sketch + s.sketch_off;
+    if (stride == 4) {  // r = 4: four rows' sketch loads in flight per lane
+        for (; row + 3 * gs < s.n; row += 4 * gs) {
+            float v[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[u][j] = sk[(row + u * gs) * 4 + j];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float a = sc(v[u][0]), b = sc(v[u][1]), c = sc(v[u][2]), d = sc(v[u][3]);
+                const float e = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(a, a), __fmul_rn(b, b)),
+                                                    __fmul_rn(c, c)), __fmul_rn(d, d));
+                const uint32_t key = energy_key(e);
+                keys[s.row_off + row + u * gs] = key;
+                kor |= key;
+                kand &= key;
+            }
+        }
+    }
+    for (; row < s.n; row += gs) {
+        const uint32_t key = energy_key(row_energy(sk + row * stride, R, sc, s.kind));
         keys[s.row_off + row] = key;
         kor |= key;
         kand &= key;
@@ -603,10 +624,41 @@ __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ seg
         kor |= __shfl_xor(kor, o, 64);
         kand &= __shfl_xor(kand, o, 64);
     }
+    // per-block partials (one memory-side store each: same-line atomics from every block
+    // would serialise); the last block of the segment reduces them and initialises the
+    // segment's select state
+    __shared__ uint32_t s_or[4], s_and[4];
     if ((threadIdx.x & 63) == 0) {
-        atomicOr(&ws->st[t].kor, kor);
-        atomicAnd(&ws->st[t].kand, kand);
+        s_or[threadIdx.x >> 6] = kor;
+        s_and[threadIdx.x >> 6] = kand;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_exchange(&ws->part_or[t][blockIdx.x], s_or[0] | s_or[1] | s_or[2] | s_or[3],
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_exchange(&ws->part_and[t][blockIdx.x], s_and[0] & s_and[1] & s_and[2] & s_and[3],
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!ms_arrive_last(&ws->done[t].v, gridDim.x)) return;
+    kor = 0u;
+    kand = ~0u;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
+        kor |= ms_take(&ws->part_or[t][i]);
+        kand &= ms_take(&ws->part_and[t][i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        s_or[threadIdx.x >> 6] = kor;
+        s_and[threadIdx.x >> 6] = kand;
+    }
+    __syncthreads();
+    ms_init_item(ws, t, s.k_rows, s_or[0] | s_or[1] | s_or[2] | s_or[3],
+                 s_and[0] & s_and[1] & s_and[2] & s_and[3]);
 }
 
 __device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m >= 256; }
@@ -802,35 +854,70 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
         }
         return;
     }
-    if (m >= 4 && m < 256) {  // small-m tile: slots staged in LDS, 32-bit mulhi division
-        __shared__ int32_t sl[kSmallTileRows];
+    if (m >= 4 && m < 256) {
+        // small m (3x3 / 1x1 convs): rows are too short for a wave each.  Selected rows
+        // of the chunk own consecutive slots (the row list is ascending), so their packed
+        // values are one contiguous range: stream-fill the chunk (zeros, or gE for EF21),
+        // then scatter that range row by row from a slot -> row table in LDS.
+        __shared__ int32_t rows_s[kSmallTileRows];
+        __shared__ int32_t s_first[4], s_cnt[4];
         const int nr = (int)ch.nrows;
-        for (int r = threadIdx.x; r < nr; r += 256) sl[r] = sm[r];
-        __syncthreads();
-        const uint32_t cnt = (uint32_t)(nr * m);
-        const int64_t pre = (4 - (base & 3)) & 3;  // elements before the first 16-B boundary
-        auto one = [&](uint32_t e) -> float {
-            const uint32_t r = div32(e, s.magic32);
-            const int32_t slot = sl[r];
-            float v = slot >= 0 ? sc(pk[(int64_t)slot * m + (e - r * (uint32_t)m)]) : 0.f;
-            if constexpr (EF == ARCTOPK_EF21) {
-                v = gE[base + e] + v;
-                if (slot >= 0) gE[base + e] = v;
+        int32_t first = 0x7FFFFFFF;
+        int32_t nsel = 0;
+        for (int r = threadIdx.x; r < nr; r += 256) {
+            const int32_t sl = sm[r];
+            if (sl >= 0) {
+                first = min(first, sl);
+                ++nsel;
             }
-            return v;
-        };
-        for (uint32_t e = threadIdx.x; e < (uint32_t)min<int64_t>(pre, cnt); e += 256) out[base + e] = one(e);
-        const uint32_t body = cnt > pre ? (uint32_t)((cnt - pre) >> 2) : 0u;
-        for (uint32_t q = threadIdx.x; q < body; q += 256) {
-            const uint32_t e = (uint32_t)pre + (q << 2);
-            float4 v;
-            v.x = one(e);
-            v.y = one(e + 1);
-            v.z = one(e + 2);
-            v.w = one(e + 3);
-            *reinterpret_cast<float4*>(out + base + e) = v;
         }
-        for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256) out[base + e] = one(e);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            first = min(first, __shfl_xor(first, o, 64));
+            nsel += __shfl_xor(nsel, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            s_first[threadIdx.x >> 6] = first;
+            s_cnt[threadIdx.x >> 6] = nsel;
+        }
+        __syncthreads();
+        first = min(min(s_first[0], s_first[1]), min(s_first[2], s_first[3]));
+        nsel = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        for (int r = threadIdx.x; r < nr; r += 256) {
+            const int32_t sl = sm[r];
+            if (sl >= 0) rows_s[sl - first] = r;
+        }
+        // fill
+        const uint32_t cnt = (uint32_t)(nr * m);
+        const int64_t pre = min<int64_t>((4 - (base & 3)) & 3, cnt);  // to the first 16-B boundary
+        const uint32_t body = (uint32_t)((cnt - pre) >> 2);
+        for (uint32_t e = threadIdx.x; e < (uint32_t)pre; e += 256)
+            out[base + e] = EF == ARCTOPK_EF21 ? gE[base + e] + 0.f : 0.f;
+        for (uint32_t q = threadIdx.x; q < body; q += 256) {
+            const int64_t e = base + pre + ((int64_t)q << 2);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (EF == ARCTOPK_EF21) {
+                const float4 g = *reinterpret_cast<const float4*>(gE + e);
+                v = make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f);
+            }
+            *reinterpret_cast<float4*>(out + e) = v;
+        }
+        for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256)
+            out[base + e] = EF == ARCTOPK_EF21 ? gE[base + e] + 0.f : 0.f;
+        __syncthreads();  // fill stores land before the selected rows overwrite them
+        // selected rows
+        const float* src = pk + (int64_t)first * m;
+        const uint32_t np = (uint32_t)(nsel * m);
+        for (uint32_t p = threadIdx.x; p < np; p += 256) {
+            const uint32_t j = div32(p, s.magic32);
+            const int64_t e = base + (int64_t)rows_s[j] * m + (p - j * (uint32_t)m);
+            float v = sc(src[p]);
+            if constexpr (EF == ARCTOPK_EF21) {
+                v = gE[e] + v;
+                gE[e] = v;
+            }
+            out[e] = v;
+        }
         return;
     }
     const uint32_t cnt = (uint32_t)(ch.nrows * m);
@@ -967,13 +1054,11 @@ extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_
         const MBatch& b = p->h_large_batches[bi];
         int64_t maxn = 0;
         for (int i = 0; i < b.cnt; ++i) maxn = std::max<int64_t>(maxn, b.it[i].n);
-        int e = ms_reset_orand(p->d_mws, b.cnt, st);
-        if (e) return e;
-        const int gx = (int)std::min<int64_t>(512, (maxn + 255) / 256);
+        const int gx = (int)std::min<int64_t>(kMHistBlocks, (maxn + 1023) / 1024);  // >= 4 rows per lane
         hipLaunchKernelGGL(k_arc_keys, dim3(gx, b.cnt), dim3(256), 0, st, p->d_segs, p->d_large,
                            bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws);
-        e = ms_select(b, maxn, p->d_keys, nullptr, true, p->d_mws, p->mws_cap, rowlist, nullptr,
-                      slotmap, st);
+        int e = ms_select(b, maxn, p->d_keys, nullptr, true, p->d_mws, p->mws_cap, rowlist, nullptr,
+                          slotmap, st);
         if (e) return e;
     }
     return (int)hipGetLastError();

@@ -48,15 +48,27 @@ struct MState {
     int32_t bit;            // bits [bit-1 .. 0] still undecided
     int32_t cand;           // 1: candidates were compacted, later passes read only them
     int64_t kk;             // keys still to take among those matching the prefix
-    uint32_t kor, kand;     // OR / AND of all keys (ARC start)
     uint32_t p1, m1;        // the first-pass bin (its keys are the candidates)
-    uint32_t ncand;         // candidates appended
-    uint32_t pad;
+    uint32_t ncand;         // candidates appended (copied from the padded counter)
+    uint32_t pad[7];        // 64 B
 };
 
+// Device-scope atomics run at the memory side and serialise per line: every
+// contended word gets a 128-B line of its own, and global histogram bins are
+// interleaved so neighbouring (equally hot) bins land on different lines.
+struct alignas(128) MCounter {
+    uint32_t v;
+    uint32_t pad[31];
+};
+__host__ __device__ constexpr int hist_slot(int bin) { return ((bin & 127) << 5) | (bin >> 7); }
+
 struct MWorkspace {
-    uint32_t hist[kMB][kMBins];
+    uint32_t hist[kMB][kMBins];  // indexed by hist_slot(bin)
     MState st[kMB];
+    MCounter ncand[kMB];
+    MCounter done[kMB];          // blocks of the running kernel that finished, per item
+    uint32_t part_or[kMB][kMHistBlocks];   // ARC key pass: per-block OR / AND partials
+    uint32_t part_and[kMB][kMHistBlocks];
     uint32_t cnt_gt[kMB][kMMaxRanges];
     uint32_t cnt_eq[kMB][kMMaxRanges];
     uint32_t take_eq[kMB][kMMaxRanges];
@@ -64,19 +76,67 @@ struct MWorkspace {
     // followed by the candidate lists: uint32 key[cap_total], uint32 index[cap_total]
 };
 
+// ---- device helpers shared with the producer of ARC keys (arctopk_kernels.hip) ----
+
+// True in exactly one block per counter: the last of `expected` blocks to arrive.  The
+// hand-over follows MI355X_MICROARCH.md's measured counter form: the payload is written
+// ONLY with device-scope atomics (performed at the memory side), every wave waits for
+// its own (vmcnt(0)) before a workgroup barrier, one lane then adds to the counter, the
+// block whose add returns expected-1 is last, and it reads the payload back ONLY with
+// device-scope atomics (ms_take) -- so no L2 line is trusted and no release fence (a
+// full L2 write-back per block) is needed.  The last block resets the counter.
+__device__ inline bool ms_arrive_last(uint32_t* counter, uint32_t expected) {
+    __shared__ uint32_t s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = prev + 1u == expected;
+        if (last) (void)__hip_atomic_exchange(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return s_last != 0u;
+}
+
+__device__ inline uint32_t ms_take(uint32_t* p) {  // read-and-clear at the memory side
+    return __hip_atomic_exchange(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Start state of item t (all threads of one block): histogram cleared, the keys' common
+// leading bits decided (kor / kand = OR / AND of all keys; TopK: |x| keys, kor = ~0).
+__device__ inline void ms_init_item(MWorkspace* ws, int t, int64_t k, uint32_t kor, uint32_t kand) {
+    for (int i = threadIdx.x; i < kMBins; i += blockDim.x) ws->hist[t][i] = 0;
+    if (threadIdx.x == 0) {
+        MState& s = ws->st[t];
+        const uint32_t diff = kor ^ kand;
+        const int bit = diff ? 32 - __clz(diff) : 0;
+        const uint32_t low = bit == 32 ? 0xFFFFFFFFu : ((1u << bit) - 1u);
+        s.prefix = kand & ~low;
+        s.mask = ~low;
+        s.bit = bit;
+        s.kk = k;
+        s.cand = 0;
+        s.ncand = 0;
+        s.p1 = s.prefix;
+        s.m1 = s.mask;
+        ws->ncand[t].v = 0;
+    }
+}
+
 // host-side geometry of one item: fills range / nranges / cand_cap (cand_off by caller)
 void ms_item_geometry(MItem& it);
 // workspace bytes for batches whose candidate capacities sum to <= cap_total
 int64_t ms_workspace_bytes(int64_t cap_total);
 
-// Launch the whole selection for one batch.  arc = true: keys come from `keys` and the
-// item states already hold the keys' OR / AND (ms_reset_orand before the key pass);
-// outputs are the ascending row list + per-key slot map.  arc = false: keys are |x| of
-// `x`; outputs are ascending indices + gathered values.  cap_total: candidate slots in
-// the workspace (the items' cand_off + cand_cap must fit).
+// Launch the whole selection for one batch.  arc: keys come from `keys`, whose producer
+// kernel already ran ms_init_item for every item (with the keys' OR / AND); outputs are
+// the ascending row list + per-key slot map.  !arc: keys are |x| of `x`; outputs are
+// ascending indices + gathered values.  cap_total: candidate slots in the workspace
+// (the items' cand_off + cand_cap must fit).  The workspace's `done` counters must be
+// zero before the first use (hipMemset once; every kernel leaves them zero).
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* x, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, float* out_val,
               int32_t* out_slot, hipStream_t st);
-int ms_reset_orand(MWorkspace* ws, int cnt, hipStream_t st);
 
 }  // namespace arctopk

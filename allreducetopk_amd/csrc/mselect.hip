@@ -1,4 +1,9 @@
 // Multi-block exact top-k selection (see mselect.h for the algorithm).
+//
+// Launches per batch: [init (TopK only; ARC's key producer initialises)] -> hist0 ->
+// compact -> hist1 -> hist2 -> count -> write.  Each histogram pass picks its digit in
+// the last block to finish (ms_arrive_last), the count pass computes the per-range
+// offsets the same way: no separate tiny kernels between the passes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -11,6 +16,7 @@ namespace {
 constexpr int kW1 = 12;  // first-pass digit width (kMBins = 1 << kW1)
 constexpr int kW2 = 10;  // refinement digit width (12 + 10 + 10 >= 32 key bits)
 constexpr int kPerLane = kMTile / 256;  // keys per lane of a tile (16)
+constexpr int kCandPerBlock = 2048;     // candidates per block of a refinement pass
 
 template <bool FROM_FLOAT>
 __device__ __forceinline__ uint32_t load_bits(const uint32_t* __restrict__ keys,
@@ -19,7 +25,7 @@ __device__ __forceinline__ uint32_t load_bits(const uint32_t* __restrict__ keys,
     else return keys[i];
 }
 
-// |x| for TopK keys: NaN sorts above inf, as in the previous radix order
+// |x| for TopK keys: NaN sorts above inf
 template <bool FROM_FLOAT>
 __device__ __forceinline__ uint32_t key_of(uint32_t bits) {
     if constexpr (FROM_FLOAT) return bits & 0x7FFFFFFFu;
@@ -52,100 +58,66 @@ __device__ __forceinline__ uint32_t block_exscan_u32(uint32_t v, uint32_t* lds, 
     return before + x - v;
 }
 
-template <bool FROM_FLOAT>
-__global__ void k_ms_init(MBatch b, MWorkspace* ws) {
+// TopK start state: |x| keys, only the sign bit is known
+__global__ void __launch_bounds__(256) k_ms_init(MBatch b, MWorkspace* ws) {
     const int t = blockIdx.x;
-    for (int i = threadIdx.x; i < kMBins; i += blockDim.x) ws->hist[t][i] = 0;
-    if (threadIdx.x == 0) {
-        MState& s = ws->st[t];
-        if constexpr (FROM_FLOAT) {
-            s.prefix = 0;
-            s.mask = 0x80000000u;
-            s.bit = 31;
-        } else {
-            // common leading bits of all keys are decided from the start
-            const uint32_t diff = s.kor ^ s.kand;
-            const int bit = diff ? 32 - __clz(diff) : 0;
-            const uint32_t low = bit == 32 ? 0xFFFFFFFFu : ((1u << bit) - 1u);
-            s.prefix = s.kand & ~low;
-            s.mask = ~low;
-            s.bit = bit;
-        }
-        s.kk = b.it[t].k;
-        s.cand = 0;
-        s.ncand = 0;
-        s.p1 = s.prefix;
-        s.m1 = s.mask;
-    }
-}
-
-__global__ void k_ms_reset_orand(MWorkspace* ws, int cnt) {
-    const int t = threadIdx.x;
-    if (t < cnt) {
-        ws->st[t].kor = 0u;
-        ws->st[t].kand = 0xFFFFFFFFu;
-    }
+    ms_init_item(ws, t, b.it[t].k, 0x7FFFFFFFu, 0u);
+    if (threadIdx.x == 0) ws->done[t].v = 0;
 }
 
 // Histogram of the next min(W, bit) undecided bits of the keys matching the prefix:
 // PASS 0 scans every key of the item; later passes scan the candidates when the item
-// has them.  LDS histogram, merged with one global atomic per non-empty bin.
+// has them.  LDS histogram, merged with one global atomic per non-empty bin; the last
+// block then reads (and clears) the global histogram and fixes the digit holding the
+// kk-th largest key.  PASS 0 also fixes the candidate bin and mode.
 template <bool FROM_FLOAT, int PASS>
 __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __restrict__ keys,
                                                  const float* __restrict__ x, MWorkspace* ws,
                                                  const uint32_t* __restrict__ ckey) {
     constexpr int W = PASS == 0 ? kW1 : kW2;
+    constexpr int PER = (1 << W) / 256;
     __shared__ uint32_t h[1 << W];
+    __shared__ uint32_t lds[4];
     const int t = blockIdx.y;
     const MState s = ws->st[t];
-    if (s.bit <= 0) return;
+    if (s.bit <= 0) return;  // every block: nothing left to decide
+    const bool from_cand = PASS > 0 && s.cand;
+    const int64_t ncand = from_cand ? (int64_t)ws->ncand[t].v : 0;
+    const int64_t nblk = from_cand
+        ? min<int64_t>(gridDim.x, max<int64_t>(1, (ncand + kCandPerBlock - 1) / kCandPerBlock))
+        : (int64_t)gridDim.x;
+    if (blockIdx.x >= nblk) return;  // uniform per block; not counted by the arrival
     const int w = s.bit < W ? s.bit : W;
     const int shift = s.bit - w;
     const uint32_t dmask = (1u << w) - 1u;
     for (int i = threadIdx.x; i < (1 << W); i += 256) h[i] = 0;
     __syncthreads();
     const MItem it = b.it[t];
-    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t stride = nblk * 256;
     int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (PASS > 0 && s.cand) {
-        const uint32_t* src = ckey + it.cand_off;
-        const int64_t n = s.ncand;
-        for (; i < n; i += stride) {
-            const uint32_t key = src[i];
-            if ((key & s.mask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
-        }
-    } else {
-        const int64_t n = it.n;
-        for (; i + 3 * stride < n; i += 4 * stride) {  // four loads in flight per lane
-            uint32_t k4[4];
+    const uint32_t* src = from_cand ? ckey + it.cand_off : nullptr;
+    const int64_t n = from_cand ? ncand : it.n;
+    for (; i + 3 * stride < n; i += 4 * stride) {  // four loads in flight per lane
+        uint32_t k4[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) k4[u] = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i + u * stride));
+        for (int u = 0; u < 4; ++u)
+            k4[u] = from_cand ? src[i + u * stride]
+                              : key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i + u * stride));
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if ((k4[u] & s.mask) == s.prefix) atomicAdd(&h[(k4[u] >> shift) & dmask], 1u);
-        }
-        for (; i < n; i += stride) {
-            const uint32_t key = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
-            if ((key & s.mask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
-        }
+        for (int u = 0; u < 4; ++u)
+            if ((k4[u] & s.mask) == s.prefix) atomicAdd(&h[(k4[u] >> shift) & dmask], 1u);
+    }
+    for (; i < n; i += stride) {
+        const uint32_t key = from_cand ? src[i]
+                                       : key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
+        if ((key & s.mask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
     }
     __syncthreads();
     for (int j = threadIdx.x; j <= (int)dmask; j += 256)
-        if (h[j]) atomicAdd(&ws->hist[t][j], h[j]);
-}
+        if (h[j]) atomicAdd(&ws->hist[t][hist_slot(j)], h[j]);
+    if (!ms_arrive_last(&ws->done[t].v, (uint32_t)nblk)) return;
 
-// Pick the digit holding the kk-th largest key (bins scanned from the top), then clear
-// the histogram for the next pass.  PASS 0 also fixes the candidate bin and mode.
-template <int PASS>
-__global__ void __launch_bounds__(256) k_ms_digit(MBatch b, MWorkspace* ws) {
-    constexpr int W = PASS == 0 ? kW1 : kW2;
-    constexpr int PER = ((1 << W) + 255) / 256;
-    __shared__ uint32_t lds[4];
-    const int t = blockIdx.x;
-    const MState s = ws->st[t];
-    if (s.bit <= 0) return;  // uniform per block
-    const int w = s.bit < W ? s.bit : W;
-    const int shift = s.bit - w;
+    // ---- last block: digit of the kk-th largest key (bins scanned from the top)
     const int nb = 1 << w;
     const int per = (nb + 255) / 256;
     uint32_t c[PER];
@@ -153,7 +125,7 @@ __global__ void __launch_bounds__(256) k_ms_digit(MBatch b, MWorkspace* ws) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int bin = nb - 1 - ((int)threadIdx.x * per + q);
-        c[q] = (q < per && bin >= 0) ? ws->hist[t][bin] : 0u;
+        c[q] = (q < per && bin >= 0) ? ms_take(&ws->hist[t][hist_slot(bin)]) : 0u;
         sum += c[q];
     }
     uint32_t total;
@@ -177,24 +149,20 @@ __global__ void __launch_bounds__(256) k_ms_digit(MBatch b, MWorkspace* ws) {
         if (PASS == 0) {
             g.p1 = prefix;
             g.m1 = mask;
-            g.cand = (int64_t)c[q] <= b.it[t].cand_cap ? 1 : 0;
+            g.cand = (int64_t)c[q] <= it.cand_cap ? 1 : 0;
         }
-    }
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int bin = nb - 1 - ((int)threadIdx.x * per + q);
-        if (q < per && bin >= 0) ws->hist[t][bin] = 0u;
     }
 }
 
 // One block per range: count of keys above the first-pass bin, and (candidate mode)
-// append the bin's keys + local indices to the item's candidate list.
+// append the bin's keys + local indices to the item's candidate list, one counter
+// atomic per block tile (a tile's candidates stay contiguous).
 template <bool FROM_FLOAT>
 __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __restrict__ keys,
                                                     const float* __restrict__ x, MWorkspace* ws,
                                                     uint32_t* __restrict__ ckey,
                                                     uint32_t* __restrict__ cidx) {
-    __shared__ uint32_t lds[4];
+    __shared__ uint32_t lds[4], s_cnt[4], s_base;
     const int t = blockIdx.y;
     const MItem it = b.it[t];
     const int r = blockIdx.x;
@@ -219,10 +187,17 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
             gt += (valid && kv[j] > hi) ? 1u : 0u;
             if (s.cand) nin += popc64(__ballot(valid && (kv[j] & s.m1) == s.p1));
         }
-        if (s.cand && nin) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&ws->st[t].ncand, nin);
-            base = __shfl(base, 0, 64);
+        if (s.cand) {  // uniform
+            if (lane == 0) s_cnt[wave] = nin;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+                s_base = tot ? atomicAdd(&ws->ncand[t].v, tot) : 0u;
+            }
+            __syncthreads();
+            uint32_t base = s_base;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) base += w < wave ? s_cnt[w] : 0u;
 #pragma unroll
             for (int j = 0; j < kPerLane; ++j) {
                 const int64_t i = wb + j * 64 + lane;
@@ -235,6 +210,7 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
                 }
                 base += popc64(bm);
             }
+            __syncthreads();  // s_cnt / s_base are rewritten by the next tile
         }
     }
     uint32_t total;
@@ -245,8 +221,10 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
     }
 }
 
-// Per-range counts of the bin's keys > T and == T (T = the final prefix): from the
-// candidates (atomics) or, in full mode, by rescanning each range's keys.
+// Per-range counts of the bin's keys > T and == T (T = the final prefix), added to the
+// compact pass's counts: from the candidates or, in full mode, by rescanning each
+// range.  The last block then turns them into per-range T-equal allowances (lowest
+// ranges first) and output offsets.
 template <bool FROM_FLOAT>
 __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __restrict__ keys,
                                                   const float* __restrict__ x, MWorkspace* ws,
@@ -257,54 +235,84 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
     const MItem it = b.it[t];
     const MState s = ws->st[t];
     const uint32_t T = s.prefix;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (s.cand) {
-        const int64_t n = s.ncand;
-        for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < n; c += (int64_t)gridDim.x * 256) {
-            const uint32_t key = ckey[it.cand_off + c];
-            if (key >= T) {
-                const int r = (int)(cidx[it.cand_off + c] / (uint32_t)it.range);
-                atomicAdd(key > T ? &ws->cnt_gt[t][r] : &ws->cnt_eq[t][r], 1u);
+        const int64_t n = ws->ncand[t].v;
+        for (int64_t c0 = (int64_t)blockIdx.x * 256 + wave * 64; c0 < n; c0 += (int64_t)gridDim.x * 256) {
+            const int64_t c = c0 + lane;
+            const bool valid = c < n;
+            const uint32_t key = valid ? ckey[it.cand_off + c] : 0u;
+            const int r = valid ? (int)(cidx[it.cand_off + c] / (uint32_t)it.range) : -1;
+            const bool gt = valid && key > T;
+            const bool eq = valid && key == T;
+            // segmented wave reduction: one atomic pair per distinct range in the wave
+            // (candidates are appended block tile by block tile: usually one or two)
+            uint64_t pending = __ballot(gt || eq);
+            while (pending) {
+                const int leader = __ffsll((long long)pending) - 1;
+                const int rl = __shfl(r, leader, 64);
+                const bool mine = valid && r == rl;
+                const uint32_t ng = popc64(__ballot(mine && gt)), ne = popc64(__ballot(mine && eq));
+                if (lane == leader) {
+                    if (ng) atomicAdd(&ws->cnt_gt[t][rl], ng);
+                    if (ne) atomicAdd(&ws->cnt_eq[t][rl], ne);
+                }
+                pending &= ~__ballot(mine);
             }
         }
-        return;
-    }
-    for (int r = blockIdx.x; r < it.nranges; r += gridDim.x) {
-        const int64_t r0 = (int64_t)r * it.range;
-        const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
-        uint32_t gt = 0, eq = 0;
-        for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
-            const uint32_t key = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
-            const bool in = (key & s.m1) == s.p1;
-            gt += (in && key > T) ? 1u : 0u;
-            eq += key == T ? 1u : 0u;
+    } else {
+        for (int r = blockIdx.x; r < it.nranges; r += gridDim.x) {
+            const int64_t r0 = (int64_t)r * it.range;
+            const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+            uint32_t gt = 0, eq = 0;
+            for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+                const uint32_t key = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
+                const bool in = (key & s.m1) == s.p1;
+                gt += (in && key > T) ? 1u : 0u;
+                eq += key == T ? 1u : 0u;
+            }
+            uint32_t tg, te;
+            (void)block_exscan_u32<4>(gt, lds, &tg);
+            (void)block_exscan_u32<4>(eq, lds, &te);
+            if (threadIdx.x == 0) {
+                if (tg) atomicAdd(&ws->cnt_gt[t][r], tg);
+                if (te) atomicAdd(&ws->cnt_eq[t][r], te);
+            }
         }
-        uint32_t tg, te;
-        (void)block_exscan_u32<4>(gt, lds, &tg);
-        (void)block_exscan_u32<4>(eq, lds, &te);
-        if (threadIdx.x == 0) {
-            ws->cnt_gt[t][r] += tg;
-            ws->cnt_eq[t][r] = te;
-        }
     }
-}
+    if (!ms_arrive_last(&ws->done[t].v, gridDim.x)) return;
 
-// Per item: T-equal allowance per range (lowest ranges first) and output offsets.
-__global__ void __launch_bounds__(kMMaxRanges) k_ms_offsets(MBatch b, MWorkspace* ws) {
-    __shared__ uint32_t lds[kMMaxRanges / 64];
-    const int t = blockIdx.x;
-    const int i = threadIdx.x;
-    const int nr = b.it[t].nranges;
-    const uint32_t eq = i < nr ? ws->cnt_eq[t][i] : 0u;
+    // ---- last block: offsets over the item's ranges (4 consecutive ranges per thread)
+    const int nr = it.nranges;
+    uint32_t eq[4], gt[4], se = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = threadIdx.x * 4 + q;
+        eq[q] = r < nr ? ms_take(&ws->cnt_eq[t][r]) : 0u;
+        gt[q] = r < nr ? ms_take(&ws->cnt_gt[t][r]) : 0u;
+        se += eq[q];
+    }
     uint32_t tot;
-    const uint32_t eq_before = block_exscan_u32<kMMaxRanges / 64>(eq, lds, &tot);
-    const int64_t need = ws->st[t].kk;
-    int64_t take = need - (int64_t)eq_before;
-    take = take < 0 ? 0 : (take > eq ? eq : take);
-    const uint32_t sel = (i < nr ? ws->cnt_gt[t][i] : 0u) + (uint32_t)take;
-    const uint32_t sel_before = block_exscan_u32<kMMaxRanges / 64>(sel, lds, &tot);
-    if (i < nr) {
-        ws->take_eq[t][i] = (uint32_t)take;
-        ws->sel_before[t][i] = sel_before;
+    uint32_t eq_before = block_exscan_u32<4>(se, lds, &tot);
+    const int64_t need = s.kk;
+    uint32_t take[4], ss = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int64_t tk = need - (int64_t)eq_before;
+        tk = tk < 0 ? 0 : (tk > eq[q] ? eq[q] : tk);
+        take[q] = (uint32_t)tk;
+        eq_before += eq[q];
+        ss += gt[q] + take[q];
+    }
+    uint32_t sel_before = block_exscan_u32<4>(ss, lds, &tot);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = threadIdx.x * 4 + q;
+        if (r < nr) {
+            ws->take_eq[t][r] = take[q];
+            ws->sel_before[t][r] = sel_before;
+        }
+        sel_before += gt[q] + take[q];
     }
 }
 
@@ -417,20 +425,16 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
     }
     uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
     uint32_t* cidx = ckey + cap_total;
-    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + kMTile - 1) / kMTile));
+    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + 8191) / 8192));
     const dim3 gh(hb, cnt), gt(gr, cnt);
 #define MS_LAUNCH(FF, AR)                                                                              \
     do {                                                                                               \
-        hipLaunchKernelGGL(k_ms_init<FF>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
+        if (!AR) hipLaunchKernelGGL(k_ms_init, dim3(cnt), dim3(256), 0, st, b, ws);                    \
         hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
-        hipLaunchKernelGGL(k_ms_digit<0>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
         hipLaunchKernelGGL(k_ms_compact<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);        \
         hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
-        hipLaunchKernelGGL(k_ms_digit<1>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
         hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
-        hipLaunchKernelGGL(k_ms_digit<2>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
         hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);          \
-        hipLaunchKernelGGL(k_ms_offsets, dim3(cnt), dim3(kMMaxRanges), 0, st, b, ws);                  \
         hipLaunchKernelGGL((k_ms_write<FF, AR>), gt, dim3(256), 0, st, b, keys, x, ws, out_idx,        \
                            out_val, out_slot);                                                         \
     } while (0)
@@ -439,11 +443,6 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
     else
         MS_LAUNCH(true, false);
 #undef MS_LAUNCH
-    return (int)hipGetLastError();
-}
-
-int ms_reset_orand(MWorkspace* ws, int cnt, hipStream_t st) {
-    hipLaunchKernelGGL(k_ms_reset_orand, dim3(1), dim3(64), 0, st, ws, cnt);
     return (int)hipGetLastError();
 }
 

@@ -215,6 +215,9 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         }
         e = hipMalloc((void**)&p->d_mws, (size_t)ms_workspace_bytes(p->mws_cap));
         if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
+        // arrival counters start at zero (each select kernel leaves them zero)
+        e = hipMemset(p->d_mws, 0, sizeof(MWorkspace));
+        if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
     }
 #undef ALLOC_COPY
     e = hipMalloc((void**)&p->d_keys, std::max<size_t>(4, info.rows_total * sizeof(uint32_t)));

@@ -37,16 +37,36 @@ from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import (GroupTopKSt
 METRIC = "compressed grad GB/s (device-resident) per GPU at k=0.2, r=4; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
 HEADLINE = [[2048, 2048]] * 16
+# secondary buckets: real DDP bucket shapes of the BASELINE configs
+WORKLOADS = {
+    "headline": ("bucket_16x2048x2048_fp32_256MiB", HEADLINE),
+    "llama_embed": ("bucket_llama1b_embed_32000x2048_fp32_250MiB", [[32000, 2048]]),
+    "roberta_embed": ("bucket_roberta_embed_50265x768_fp32_147MiB", [[50265, 768]]),
+    "resnet18_conv": ("bucket_28x512x512x3x3_fp32_252MiB", [[512, 512, 3, 3]] * 28),
+    "resnet50_mixed": ("bucket_resnet50_stage4_mixed_fp32",
+                       [[2048], [2048], [2048, 512, 1, 1], [512], [512], [512, 512, 3, 3], [512],
+                        [512], [512, 2048, 1, 1]] * 3 + [[2048, 1024, 1, 1]]),
+    "llama_layer_mixed": ("bucket_llama1b_layer_mixed_1d_fp32",
+                          [[2048], [5632, 2048], [2048, 5632], [5632, 2048], [2048]]
+                          + [[2048, 2048]] * 4 + [[2048]]),
+}
 PHASES = ["encode", "sketch_allreduce", "select", "pack", "packed_allreduce", "decode"]
 
 
 def algorithmic_bytes(ef: str, shapes, ratio: float, r: int):
-    """Minimum HBM bytes per call, per phase (fp32, fused design)."""
+    """Minimum HBM bytes per call, per phase (fp32, fused design).
+
+    1-D tensors are their own sketch (written by encode, read by select); 2-D/ND
+    tensors add an [n, r] sketch and read an [m, r] projection.
+    """
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import _geometry
     n_el = bucket_numel(shapes)
-    rows = sum(s[0] for s in shapes)
-    k_el = sum(max(1, int(s[0] * ratio)) * s[1] for s in shapes)
-    sk = rows * r * 4
-    vbytes = sum(s[1] for s in shapes) * r * 4
+    k_el = sk = vbytes = 0
+    for s_ in shapes:
+        kind, n, m = _geometry(s_)
+        k_el += max(1, int(n * ratio)) * m
+        sk += 4 * n * (1 if m == 1 and len(s_) == 1 else r)
+        vbytes += 0 if len(s_) == 1 else m * r * 4
     if ef == "noef":
         enc = 4 * n_el + sk + vbytes
         pack = 4 * k_el + 4 * k_el
@@ -63,12 +83,12 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int):
     return dict(encode=enc, select=sel, pack=pack, decode=dec, total=enc + sel + pack + dec)
 
 
-def cpu_baseline(ef: str, seconds: float, rank: int):
+def cpu_baseline(ef: str, seconds: float, rank: int, shapes, label: str):
     """Time the CPU oracle (a restatement of the reference hook) on the same bucket."""
     from oracle import arctopk as A
     threads = torch.get_num_threads()
     g = torch.Generator().manual_seed(1000 + rank)
-    n = bucket_numel(HEADLINE)
+    n = bucket_numel(shapes)
     G = torch.randn(n, generator=g)
     E = torch.randn(n, generator=g) * 0.1 if ef != "noef" else None
     gE = torch.zeros(n) if ef == "ef21" else None
@@ -78,13 +98,13 @@ def cpu_baseline(ef: str, seconds: float, rank: int):
     while time.perf_counter() < t_end or len(times) < 2:
         seed = st.next_seed()
         t0 = time.perf_counter()
-        A.simulate_step([G], [E], gE, HEADLINE, 0.2, 4, ef, seed)
+        A.simulate_step([G], [E], gE, shapes, 0.2, 4, ef, seed)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round(4 * n / med / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "port",
             "sample": f"{len(times)} oracle calls (torch-CPU restatement of group_topk_hook, "
-                      f"ws=1, {ef}) on one 16x[2048,2048] fp32 bucket, median {med * 1e3:.1f} ms, "
+                      f"ws=1, {ef}) on one {label} bucket, median {med * 1e3:.1f} ms, "
                       f"{os.cpu_count()} host CPUs visible"}
 
 
@@ -94,6 +114,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ef", default="ef14", choices=["noef", "ef14", "ef21"])
+    ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS),
+                    help="bucket shape set (headline = the BASELINE metric's bucket)")
     ap.add_argument("--ratio", type=float, default=0.2)
     ap.add_argument("--r", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -123,7 +145,7 @@ def main():
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    shapes = HEADLINE
+    label, shapes = WORKLOADS[args.workload]
     n = bucket_numel(shapes)
     bucket_bytes = 4 * n
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -184,7 +206,7 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (N(0,1) fp32 gradients, per-rank seed)",
-        "config": {"workload": f"arctopk_{args.ef}_bucket_16x2048x2048_fp32_256MiB"
+        "config": {"workload": f"arctopk_{args.ef}_{label}"
                                + ("_host_staged" if args.host_staged else ""),
                    "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
                    "bucket_bytes": bucket_bytes, "parallelism": f"dp{world}",
@@ -196,7 +218,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, rank)
+        out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, rank, shapes, label)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.barrier()
