@@ -25,7 +25,7 @@ STATUS = {1001: "invalid argument", 1002: "ND tensor numel not divisible by 2*t^
 class PlanInfo(ctypes.Structure):
     _fields_ = [("numel", c_int64), ("sketch_len", c_int64), ("v_len", c_int64),
                 ("packed_len", c_int64), ("sel_rows", c_int64), ("rows_total", c_int64),
-                ("nseg", c_int32), ("r", c_int32)]
+                ("nseg", c_int32), ("r", c_int32), ("values_len", c_int64)]
 
 
 class Segment(ctypes.Structure):

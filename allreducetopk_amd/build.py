@@ -37,19 +37,22 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
+    """Compile the HIP sources into one shared library (gfx950).  `out` / `defines`
+    build tuning variants (e.g. -DARCTOPK_ENC_WAVES=4) next to the product library."""
+    if out == LIB and not defines and not force and not _stale():
         return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}", *srcs, "-o", tmp]
+           "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], f"-I{INCLUDE}", f"-I{CSRC}",
+           *srcs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -88,7 +88,9 @@ class BucketPlan:
         self.ms = tuple(int(s.m) for s in self.segments if s.kind == N.SEG_SKETCH)
         dev = self.device
         self.sketch = torch.empty(max(1, info.sketch_len), dtype=torch.float32, device=dev)
-        self.packed = torch.empty(max(1, info.packed_len), dtype=torch.float32, device=dev)
+        # zero-filled: the <= 3 alignment pad floats between segments ride the
+        # all-reduce as zeros and are never decoded
+        self.packed = torch.zeros(max(1, info.packed_len), dtype=torch.float32, device=dev)
         self.rowlist = torch.empty(max(1, info.sel_rows), dtype=torch.int32, device=dev)
         self.slotmap = torch.empty(max(1, info.rows_total), dtype=torch.int32, device=dev)
         self.V = torch.empty(max(1, info.v_len), dtype=torch.float32, device=dev)
@@ -130,6 +132,12 @@ class BucketPlan:
     @property
     def sketch_view(self):
         return self.sketch[:self.info.sketch_len]
+
+    def packed_values(self) -> torch.Tensor:
+        """The selected values in the reference's values_memory layout (segments back to
+        back, no alignment pads) -- for inspection and tests."""
+        return torch.cat([self.packed[int(s.packed_off):int(s.packed_off + s.k_rows * s.m)]
+                          for s in self.segments])
 
     @property
     def packed_view(self):
@@ -337,10 +345,11 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     stream = torch.cuda.current_stream(input_tensor.device)
     sid = stream.cuda_stream
     dtype = input_tensor.dtype
-    host_v = state._proj.get(seed, plan.ms, dtype)
+    slot = state._proj.get(seed, plan.ms, dtype)
     V = plan.V
     if plan.info.v_len:  # 512 KiB pinned H2D at headline, stream-ordered before encode
-        V[:plan.info.v_len].copy_(host_v[:plan.info.v_len], non_blocking=True)
+        V[:plan.info.v_len].copy_(slot.host[:plan.info.v_len], non_blocking=True)
+    state._proj.release(slot, stream)  # refilled only after this copy completed
     state._proj.prefetch(state._upcoming_ms(bucket), dtype)
 
     evs = None

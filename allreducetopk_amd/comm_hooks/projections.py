@@ -25,21 +25,19 @@ from typing import Dict, Optional, Sequence, Tuple
 import torch
 
 
-def draw_host(seed: int, ms: Sequence[int], r: int, dtype: torch.dtype, pin: bool) -> torch.Tensor:
-    """Concatenated [m_i][r] projections for one call, on the host (pinned if asked).
+def _fill_plan(host: torch.Tensor, ms: Sequence[int], r: int, dtype: torch.dtype):
+    """Views of `host` that one generator pass fills in the reference's stream order.
 
-    Consecutive tensors whose m*r is a multiple of 16 are drawn by ONE randn call:
-    torch's CPU normal fill draws all uniforms in stream order and transforms them in
-    independent 16-value blocks, so the concatenation is bit-identical to per-tensor
-    calls (tests/test_host_logic.py checks it); other tensors get their own call,
-    exactly as the reference's per-tensor ``torch.randn(m, r)``.
+    Consecutive tensors whose m*r is a multiple of 16 share ONE view: torch's CPU normal
+    fill draws all uniforms in stream order and transforms them in independent 16-value
+    blocks, so one fill of the concatenation is bit-identical to per-tensor calls
+    (tests/test_host_logic.py checks it); other tensors get their own [m, r] view, as the
+    reference's per-tensor ``torch.randn(m, r)``.  ``Tensor.normal_`` on a view draws
+    exactly what ``torch.randn`` of that shape draws, at a third of the Python overhead.
     """
-    total = sum(int(m) * r for m in ms)
-    host = torch.empty(max(total, 1), dtype=dtype, pin_memory=pin)
-    g = torch.Generator().manual_seed(int(seed))
+    views = []
     fast = dtype == torch.float32
-    off = 0
-    run_start = run_len = 0
+    off = run_start = run_len = 0
     for m in ms:
         n = int(m) * r
         if fast and n >= 16 and n % 16 == 0:
@@ -48,17 +46,54 @@ def draw_host(seed: int, ms: Sequence[int], r: int, dtype: torch.dtype, pin: boo
             run_len += n
         else:
             if run_len:
-                torch.randn(run_len, generator=g, dtype=dtype, out=host[run_start:run_start + run_len])
+                views.append(host[run_start:run_start + run_len])
                 run_len = 0
-            torch.randn(int(m), r, generator=g, dtype=dtype, out=host[off:off + n].view(int(m), r))
+            views.append(host[off:off + n].view(int(m), r))
         off += n
     if run_len:
-        torch.randn(run_len, generator=g, dtype=dtype, out=host[run_start:run_start + run_len])
+        views.append(host[run_start:run_start + run_len])
+    return views
+
+
+def draw_host(seed: int, ms: Sequence[int], r: int, dtype: torch.dtype, pin: bool) -> torch.Tensor:
+    """Concatenated [m_i][r] projections for one call, on the host (pinned if asked)."""
+    total = sum(int(m) * r for m in ms)
+    host = torch.empty(max(total, 1), dtype=dtype, pin_memory=pin)
+    g = torch.Generator().manual_seed(int(seed))
+    for v in _fill_plan(host, ms, r, dtype):
+        v.normal_(generator=g)
     return host
 
 
+class Slot:
+    """A reusable pinned host buffer for one column list, with its fill views."""
+
+    __slots__ = ("key", "host", "views", "event")
+
+    def __init__(self, key, ms, r, dtype, pin):
+        self.key = key
+        total = sum(int(m) * r for m in ms)
+        self.host = torch.empty(max(total, 1), dtype=dtype, pin_memory=pin)
+        self.views = _fill_plan(self.host, ms, r, dtype)
+        self.event = None  # set when an async copy out of `host` was enqueued
+
+    def fill(self, seed: int):
+        if self.event is not None:  # the previous H2D copy from this buffer must be done
+            self.event.synchronize()
+            self.event = None
+        g = torch.Generator().manual_seed(int(seed))
+        for v in self.views:
+            v.normal_(generator=g)
+        return self
+
+
 class ProjectionSource:
-    """Per-state projection provider with look-ahead prefetch."""
+    """Per-state projection provider with look-ahead prefetch into pooled pinned slots.
+
+    ``get`` returns a filled :class:`Slot`; the caller copies ``slot.host`` to the device
+    and hands the slot back with :meth:`release` (recording the copy's stream, so the
+    buffer is refilled only after that copy completed).
+    """
 
     def __init__(self, r: int, depth: int = 8, workers: int = 8):
         self.r = r
@@ -66,6 +101,7 @@ class ProjectionSource:
         self._pool: Optional[ThreadPoolExecutor] = None
         self._workers = workers
         self._pending: Dict[Tuple, object] = {}
+        self._free: Dict[Tuple, list] = collections.defaultdict(list)
         self._lock = threading.Lock()
         self._lookahead: Optional[torch.Generator] = None
         self._future_seeds: collections.deque = collections.deque()
@@ -96,8 +132,26 @@ class ProjectionSource:
             self._sync_lookahead(rng)
         return seed
 
+    # -- slots --------------------------------------------------------------
+    def _slot(self, ms: Tuple[int, ...], dtype: torch.dtype) -> Slot:
+        key = (tuple(ms), dtype)
+        with self._lock:
+            free = self._free[key]
+            if free:
+                return free.pop()
+        return Slot(key, ms, self.r, dtype, pin=torch.cuda.is_available())
+
+    def release(self, slot: Slot, stream=None):
+        """Return a slot; with `stream`, after the work enqueued on it so far (the copy)."""
+        if stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            slot.event = ev
+        with self._lock:
+            self._free[slot.key].append(slot)
+
     # -- drawing ------------------------------------------------------------
-    def get(self, seed: int, ms: Tuple[int, ...], dtype: torch.dtype) -> torch.Tensor:
+    def get(self, seed: int, ms: Tuple[int, ...], dtype: torch.dtype) -> Slot:
         key = (seed, ms, dtype)
         with self._lock:
             fut = self._pending.pop(key, None)
@@ -105,7 +159,7 @@ class ProjectionSource:
             self.hits += 1
             return fut.result()
         self.misses += 1
-        return draw_host(seed, ms, self.r, dtype, pin=torch.cuda.is_available())
+        return self._slot(ms, dtype).fill(seed)
 
     def prefetch(self, upcoming_ms: Sequence[Tuple[int, ...]], dtype: torch.dtype):
         """Schedule the projections of the next ``len(upcoming_ms)`` calls."""
@@ -115,16 +169,20 @@ class ProjectionSource:
             self._pool = ThreadPoolExecutor(max_workers=self._workers,
                                             thread_name_prefix="arctopk-proj")
         seeds = self._peek_seeds(min(self.depth, len(upcoming_ms)))
-        pin = torch.cuda.is_available()
+        stale = []
         with self._lock:
             live = set()
             for seed, ms in zip(seeds, upcoming_ms):
                 key = (seed, ms, dtype)
                 live.add(key)
                 if key not in self._pending:
-                    self._pending[key] = self._pool.submit(draw_host, seed, ms, self.r, dtype, pin)
+                    self._pending[key] = self._pool.submit(
+                        lambda sd=seed, m_=ms: self._slot(m_, dtype).fill(sd))
             for key in [k for k in self._pending if k not in live]:  # stale predictions
-                self._pending.pop(key)
+                stale.append(self._pending.pop(key))
+        for fut in stale:  # recycle their slots once drawn
+            fut.add_done_callback(lambda f: self.release(f.result()) if not f.cancelled()
+                                  and f.exception() is None else None)
 
     def reset(self):
         """Forget the seed look-ahead and pending draws (the rng was repositioned)."""

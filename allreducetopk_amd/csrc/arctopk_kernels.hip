@@ -78,7 +78,8 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                                                 const EncTile* __restrict__ tiles,
                                                 const float* __restrict__ G, float* __restrict__ E,
                                                 const float* __restrict__ V,
-                                                float* __restrict__ sketch) {
+                                                float* __restrict__ sketch,
+                                                float* __restrict__ part_buf) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const EncTile t = tiles[blockIdx.x];
     const SegDev s = segs[t.seg];
@@ -131,25 +132,30 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         return;
     }
 
-    // wave-per-row modes: stage V^T ([R][m]) in LDS when it fits (conflict-free writes:
-    // consecutive lanes take consecutive columns c of one j)
+    // wave-per-row modes over the tile's columns [c0, c0 + cl): stage that slice of V^T
+    // ([R][cl]) in LDS (conflict-free writes: consecutive lanes take consecutive columns
+    // of one j).  Column-split tensors write per-part partial sketches, summed in fixed
+    // part order by k_sketch_combine.
+    const int c0 = t.c0, cl = t.clen;
     if constexpr (VLDS) {
         if constexpr (R == 4) {
-            const float4* v4 = reinterpret_cast<const float4*>(Vs);
-            for (int c = tid; c < m; c += 256) {
+            const float4* v4 = reinterpret_cast<const float4*>(Vs) + c0;
+            for (int c = tid; c < cl; c += 256) {
                 const float4 v = v4[c];
                 lds[c] = v.x;
-                lds[m + c] = v.y;
-                lds[2 * m + c] = v.z;
-                lds[3 * m + c] = v.w;
+                lds[cl + c] = v.y;
+                lds[2 * cl + c] = v.z;
+                lds[3 * cl + c] = v.w;
             }
         } else {
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                for (int c = tid; c < m; c += 256) lds[j * m + c] = Vs[c * R + j];
+                for (int c = tid; c < cl; c += 256) lds[j * cl + c] = Vs[(int64_t)(c0 + c) * R + j];
         }
         __syncthreads();
     }
+    float* const out_base = t.part < 0 ? sketch + s.sketch_off
+                                       : part_buf + s.part_off + (int64_t)t.part * s.n * R;
     const int64_t row_end = t.row0 + t.nrows;
     if (t.mode == ENC_ROW_VEC) {
         // Software-pipelined stream: a wave walks its rows in steps of 64*U float4
@@ -159,7 +165,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         // the compiler never orders an LDS read behind the prefetched global loads.
         constexpr int U = 4;
         constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
-        const int m4 = m >> 2;
+        const int m4 = cl >> 2;  // float4 columns of this tile
         const int steps = (m4 + 64 * U - 1) / (64 * U);
         const float4* vt4 = reinterpret_cast<const float4*>(lds);
         float4 ga[U], ea[U], gb[U], eb[U];
@@ -168,8 +174,8 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         for (int j = 0; j < R; ++j) acc[j] = 0.f;
 
         auto issue = [&](float4 (&gx)[U], float4 (&ex)[U], int64_t r_, int st_) {
-            const float4* g4 = reinterpret_cast<const float4*>(G + s.offset + r_ * m);
-            const float4* e4 = reinterpret_cast<const float4*>(E + s.offset + r_ * m);
+            const float4* g4 = reinterpret_cast<const float4*>(G + s.offset + r_ * m + c0);
+            const float4* e4 = reinterpret_cast<const float4*>(E + s.offset + r_ * m + c0);
 #pragma unroll
             for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: no exec-masked blocks
                 const int c = min(st_ * 64 * U + u * 64 + lane, m4 - 1);
@@ -178,7 +184,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
             }
         };
         auto consume = [&](float4 (&gx)[U], float4 (&ex)[U], int64_t r_, int st_) {
-            float4* e4 = reinterpret_cast<float4*>(E + s.offset + r_ * m);
+            float4* e4 = reinterpret_cast<float4*>(E + s.offset + r_ * m + c0);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int cu = st_ * 64 * U + u * 64 + lane;
@@ -194,13 +200,24 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                     if (ok) e4[c] = x;
                 }
                 if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 vq[4];  // !VLDS, R = 4: the 4 columns' V rows, 16-B loads from L2
+                if constexpr (!VLDS && R == 4) {
+                    const float4* vr = reinterpret_cast<const float4*>(Vs) + c0 + 4 * c;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) vq[q] = vr[q];
+                }
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     float4 v;
                     if constexpr (VLDS) {
                         v = vt4[j * m4 + c];
+                    } else if constexpr (R == 4) {
+                        v = make_float4(vq[0].x, vq[1].x, vq[2].x, vq[3].x);
+                        if (j == 1) v = make_float4(vq[0].y, vq[1].y, vq[2].y, vq[3].y);
+                        if (j == 2) v = make_float4(vq[0].z, vq[1].z, vq[2].z, vq[3].z);
+                        if (j == 3) v = make_float4(vq[0].w, vq[1].w, vq[2].w, vq[3].w);
                     } else {
-                        const float* vp = Vs + (int64_t)(4 * c) * R + j;
+                        const float* vp = Vs + (int64_t)(c0 + 4 * c) * R + j;
                         v = make_float4(vp[0], vp[R], vp[2 * R], vp[3 * R]);
                     }
                     float a = acc[j];
@@ -219,7 +236,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                     for (int j = 1; j < R; ++j)
                         if (lane == j) v = acc[j];
-                    sketch[s.sketch_off + r_ * R + lane] = v;
+                    out_base[r_ * R + lane] = v;
                 }
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = 0.f;
@@ -244,18 +261,18 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         }
     } else {  // ENC_ROW_SCALAR
         for (int64_t row = t.row0 + wave; row < row_end; row += 4) {
-            const int64_t base = s.offset + row * m;
+            const int64_t base = s.offset + row * m + c0;
             float acc[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[j] = 0.f;
-            for (int c = lane; c < m; c += 64) {
+            for (int c = lane; c < cl; c += 64) {
                 const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, c);
                 if constexpr (WRITE_E) E[base + c] = x;
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     float v;
-                    if constexpr (VLDS) v = lds[j * m + c];
-                    else v = Vs[(int64_t)c * R + j];
+                    if constexpr (VLDS) v = lds[j * cl + c];
+                    else v = Vs[(int64_t)(c0 + c) * R + j];
                     acc[j] = fmaf(x, v, acc[j]);
                 }
             }
@@ -266,7 +283,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int j = 1; j < R; ++j)
                     if (lane == j) v = acc[j];
-                sketch[s.sketch_off + row * R + lane] = v;
+                out_base[row * R + lane] = v;
             }
         }
     }
@@ -972,27 +989,50 @@ __global__ void __launch_bounds__(256) k_ef_apply(float* __restrict__ x, float* 
     }
 }
 
+// sketch of column-split tensors: the parts' partial sketches summed in part order
+__global__ void __launch_bounds__(256) k_sketch_combine(const SegDev* __restrict__ segs,
+                                                        const int32_t* __restrict__ ids, int R,
+                                                        const float* __restrict__ part_buf,
+                                                        float* __restrict__ sketch) {
+    const SegDev s = segs[ids[blockIdx.y]];
+    const int64_t cnt = s.n * R;
+    const float* pb = part_buf + s.part_off;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
+        float v = pb[i];
+        for (int q = 1; q < s.nparts; ++q) v = __fadd_rn(v, pb[(int64_t)q * cnt + i]);
+        sketch[s.sketch_off + i] = v;
+    }
+}
+
 template <int R, bool VLDS>
-int launch_encode_rv(const arctopk_plan* p, const float* G, float* E, int ef, int err_in,
-                     const float* V, float* sk, hipStream_t st) {
-    dim3 grid(p->n_enc), block(256);
-    const size_t lds = p->enc_lds_bytes;
+int launch_encode_rv(const arctopk_plan* p, int t0, int t1, size_t lds, const float* G, float* E,
+                     int ef, int err_in, const float* V, float* sk, hipStream_t st) {
+    if (t1 <= t0) return 0;
+    dim3 grid(t1 - t0), block(256);
+    const EncTile* tiles = p->d_enc + t0;
+    float* pb = p->d_part;
     if (ef == ARCTOPK_EF_NONE)
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF_NONE, false, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF_NONE, false, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
     else if (ef == ARCTOPK_EF14 && err_in)
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, true, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, true, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
     else if (ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, false, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, false, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
     else
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF21, true, VLDS>), grid, block, lds, st, p->d_segs, p->d_enc, G, E, V, sk);
+        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF21, true, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
     return (int)hipGetLastError();
 }
 
+// one launch (every tile's V slice fits in LDS), then the partial-sketch sums of
+// column-split tensors
 template <int R>
 int launch_encode_r(const arctopk_plan* p, const float* G, float* E, int ef, int err_in,
                     const float* V, float* sk, hipStream_t st) {
-    return p->enc_vlds ? launch_encode_rv<R, true>(p, G, E, ef, err_in, V, sk, st)
-                       : launch_encode_rv<R, false>(p, G, E, ef, err_in, V, sk, st);
+    int e = launch_encode_rv<R, true>(p, 0, p->n_enc, (size_t)p->enc_lds_bytes, G, E, ef, err_in, V, sk, st);
+    if (e || p->n_split == 0) return e;
+    const int gx = (int)std::min<int64_t>(256, (p->split_rows_max * R + 255) / 256);
+    hipLaunchKernelGGL(k_sketch_combine, dim3(gx, p->n_split), dim3(256), 0, st, p->d_segs, p->d_split, R,
+                       p->d_part, sk);
+    return (int)hipGetLastError();
 }
 
 }  // namespace

@@ -12,6 +12,8 @@ constexpr int kTileRows = 256;     // rows of one small-m encode tile (thread pe
 constexpr int kSmallM = 64;        // m below this: thread-per-row tiles; else wave-per-row
 constexpr int kVLdsMaxBytes = 64 * 1024;  // V staged in LDS up to this size, else read from L2
 constexpr int kChunkElems = 16384; // target elements per pack/decode work chunk
+constexpr int kEncTargetBlocks = 2048;  // encode blocks a bucket's wave-per-row work aims at
+                                        // (measured: 2048 beats 1024 on 256 CUs at 3 blocks/CU)
 constexpr int kSmallSelRows = 15360;  // rows up to this: keys in LDS (60 KiB + statics < 64 KiB)
 
 // 32-bit quotient by a runtime divisor: q = mulhi64(x, ceil(2^64/d)) is exact for
@@ -40,7 +42,8 @@ struct SegDev {
     int32_t vec;       // 1: m % 4 == 0 and offset % 4 == 0 and packed_off % 4 == 0
     FastDiv mdiv;      // division by m
     uint32_t magic32;  // ceil(2^32 / m): exact quotient for x < 2^32 / m (in-tile indices)
-    uint32_t pad2;
+    int32_t nparts;    // encode column parts (V slice of each fits in LDS); 1 = unsplit
+    int64_t part_off;  // nparts > 1: partial sketches at part_buf[part_off + (p * n + row) * r]
 };
 
 __device__ __forceinline__ uint32_t div32(uint32_t x, uint32_t magic) { return __umulhi(x, magic); }
@@ -54,6 +57,9 @@ struct EncTile {
     int32_t mode;
     int64_t row0;      // first row (RAW: first element)
     int64_t nrows;     // rows (RAW: elements)
+    int32_t c0, clen;  // row modes: column range (multiple of 4 apart when vectorised)
+    int32_t part;      // -1: whole rows -> sketch; else column part -> partial sketch
+    int32_t pad;
 };
 
 struct Chunk {         // pack: selected-row range; decode: row range
@@ -77,8 +83,11 @@ struct arctopk_plan {
     arctopk::SegDev* d_segs;
     arctopk::EncTile* d_enc;
     int n_enc;
-    int enc_lds_bytes;
-    int enc_vlds;                 // every wave-per-row segment's V fits in LDS
+    int enc_lds_bytes;            // dynamic LDS of the encode launch
+    float* d_part;                // partial sketches of column-split segments
+    int32_t* d_split;             // ids of column-split segments
+    int n_split;
+    int64_t split_rows_max;
     arctopk::Chunk* d_pack;
     int n_pack;
     arctopk::Chunk* d_dec;

@@ -2,6 +2,7 @@
 // buffer offsets, and the work tables of the encode / pack / decode kernels.
 // Built once per bucket layout; nothing here runs per call.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -15,7 +16,7 @@ namespace {
 
 int build_segments(const int64_t* dims, const int32_t* ndims, int32_t ntensors, int r, double ratio,
                    std::vector<arctopk_segment>& segs, arctopk_plan_info& info) {
-    int64_t off = 0, sk = 0, vo = 0, po = 0, ro = 0, so = 0;
+    int64_t off = 0, sk = 0, vo = 0, po = 0, ro = 0, so = 0, vals = 0;
     const int64_t* d = dims;
     for (int i = 0; i < ntensors; ++i) {
         const int nd = ndims[i];
@@ -54,6 +55,8 @@ int build_segments(const int64_t* dims, const int32_t* ndims, int32_t ntensors, 
         if (s.kind == ARCTOPK_SEG_SKETCH) vo += s.m * r;
         s.packed_off = po;
         po += k * s.m;
+        vals += k * s.m;
+        po = (po + 3) & ~int64_t(3);  // 16-B aligned segments: vector pack / decode paths
         s.row_off = ro;
         ro += s.n;
         s.sel_off = so;
@@ -66,6 +69,7 @@ int build_segments(const int64_t* dims, const int32_t* ndims, int32_t ntensors, 
     info.sketch_len = sk;
     info.v_len = vo;
     info.packed_len = po;
+    info.values_len = vals;
     info.sel_rows = so;
     info.rows_total = ro;
     info.nseg = ntensors;
@@ -91,23 +95,34 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     if (st) return st;
 
     std::vector<SegDev> dsegs(segs.size());
-    std::vector<int32_t> small_ids, large_ids;
+    std::vector<int32_t> small_ids, large_ids, split_ids;
     int64_t small_rows = 0;
     std::vector<EncTile> enc;
     std::vector<Chunk> pack, dec;
     std::vector<int32_t> pack_begin, dec_begin;
     int lds = 0;
-    int vlds = 1;
+    // Encode work sizing: tiles of wave-per-row segments hold enough rows that the
+    // bucket yields ~kEncTargetBlocks blocks (a bucket may hold ONE tensor: a DDP bucket
+    // of a 46 MB MLP weight must still fill 256 CUs), within [8K, 64K] elements per block.
+    int64_t row_work = 0;
+    for (const arctopk_segment& s : segs)
+        if (s.kind != ARCTOPK_SEG_RAW && !(s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536))
+            row_work += s.n * s.m;
+    int64_t target = kEncTargetBlocks;
+    if (const char* env = std::getenv("ARCTOPK_ENC_TARGET_BLOCKS")) target = std::max(1, std::atoi(env));  // tuning
+    const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(8192, row_work / target));
+    int64_t part_len = 0, split_rows_max = 0;
     for (size_t i = 0; i < segs.size(); ++i) {
         const arctopk_segment& s = segs[i];
         SegDev& g = dsegs[i];
         g.offset = s.offset; g.n = s.n; g.m = s.m; g.k_rows = s.k_rows;
         g.sketch_off = s.sketch_off; g.v_off = s.v_off; g.packed_off = s.packed_off;
         g.row_off = s.row_off; g.sel_off = s.sel_off; g.kind = s.kind;
-        g.vec = (s.m % 4 == 0 && s.offset % 4 == 0 && s.packed_off % 4 == 0) ? 1 : 0;
+        g.vec = (s.m % 4 == 0 && s.offset % 4 == 0) ? 1 : 0;  // packed_off is 4-aligned
         g.mdiv = make_fastdiv((uint32_t)s.m);
         g.magic32 = s.m > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)s.m - 1) / (uint64_t)s.m) : 0u;
-        g.pad2 = 0;
+        g.nparts = 1;
+        g.part_off = 0;
         if (s.n <= kSmallSelRows) {
             small_ids.push_back((int32_t)i);
             small_rows = std::max<int64_t>(small_rows, s.n);
@@ -118,35 +133,52 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         if (s.kind == ARCTOPK_SEG_RAW) {
             const int64_t per = 4096;
             for (int64_t e = 0; e < s.n; e += per)
-                enc.push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e)});
+                enc.push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e), 0, 1, -1, 0});
         } else if (s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536) {
             for (int64_t row = 0; row < s.n; row += kTileRows)
-                enc.push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(kTileRows, s.n - row)});
+                enc.push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(kTileRows, s.n - row),
+                                      0, (int32_t)s.m, -1, 0});
             lds = std::max<int>(lds, (int)(kTileRows * s.m * 4 + s.m * r * 4));
         } else {
-            // rows per tile: ~64K elements per block (4 waves), at least 4 rows
-            int64_t per = std::max<int64_t>(4, (64 * 1024) / s.m);
             const int mode = g.vec ? ENC_ROW_VEC : ENC_ROW_SCALAR;
-            for (int64_t row = 0; row < s.n; row += per)
-                enc.push_back(EncTile{(int32_t)i, mode, row, std::min(per, s.n - row)});
-            const int vbytes = (int)(s.m * r * 4);
-            if (vbytes <= kVLdsMaxBytes) lds = std::max(lds, vbytes);
-            else vlds = 0;
+            // columns per part: V^T slice [r][clen] within kVLdsMaxBytes (multiple of 4)
+            const int64_t max_cols = (kVLdsMaxBytes / (4 * r)) & ~int64_t(3);
+            const int nparts = (int)((s.m + max_cols - 1) / max_cols);
+            int64_t clen = (s.m + nparts - 1) / nparts;
+            clen = (clen + 3) & ~int64_t(3);
+            if (nparts > 1) {
+                g.nparts = nparts;
+                g.part_off = part_len;
+                part_len += (int64_t)nparts * s.n * r;
+                split_ids.push_back((int32_t)i);
+                split_rows_max = std::max<int64_t>(split_rows_max, s.n);
+            }
+            const int64_t per = std::max<int64_t>(4, tile_elems / std::min<int64_t>(clen, s.m));
+            for (int part = 0; part < nparts; ++part) {
+                const int64_t c0 = part * clen;
+                const int64_t cl = std::min<int64_t>(clen, s.m - c0);
+                for (int64_t row = 0; row < s.n; row += per)
+                    enc.push_back(EncTile{(int32_t)i, mode, row, std::min(per, s.n - row), (int32_t)c0,
+                                          (int32_t)cl, nparts > 1 ? part : -1, 0});
+                lds = std::max<int>(lds, (int)(cl * r * 4));
+            }
         }
         // ---- pack chunks: selected rows, ~kChunkElems elements each (small m: at most
         //      kSmallTileRows rows, the size of the kernels' LDS row/slot table)
         pack_begin.push_back((int32_t)pack.size());
         dec_begin.push_back((int32_t)dec.size());
         const bool small_tile = s.m >= 4 && s.m < 256;
+        // (rows of >= 256 elements go one per wave: at least 4 rows per chunk)
+        const int64_t min_rows = s.m >= 256 ? 4 : 1;
         {
-            int64_t per = std::max<int64_t>(1, kChunkElems / s.m);
+            int64_t per = std::max<int64_t>(min_rows, kChunkElems / s.m);
             if (small_tile) per = std::min<int64_t>(per, kSmallTileRows);
             for (int64_t j = 0; j < s.k_rows; j += per)
                 pack.push_back(Chunk{(int32_t)i, 0, j, std::min(per, s.k_rows - j)});
         }
         // ---- decode chunks: all rows
         {
-            int64_t per = std::max<int64_t>(1, kChunkElems / s.m);
+            int64_t per = std::max<int64_t>(min_rows, kChunkElems / s.m);
             if (small_tile) per = std::min<int64_t>(per, kSmallTileRows);
             for (int64_t row = 0; row < s.n; row += per)
                 dec.push_back(Chunk{(int32_t)i, 0, row, std::min(per, s.n - row)});
@@ -174,8 +206,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     p->h_dec_begin = new int32_t[dec_begin.size()];
     std::copy(pack_begin.begin(), pack_begin.end(), p->h_pack_begin);
     std::copy(dec_begin.begin(), dec_begin.end(), p->h_dec_begin);
-    p->enc_vlds = vlds;
-    p->enc_lds_bytes = vlds ? lds : std::max(0, lds);
+    p->enc_lds_bytes = lds;
     p->n_small = (int)small_ids.size();
     p->n_large = (int)large_ids.size();
     p->small_lds = (int)(((small_rows + 3) & ~3) * 4 + 16);
@@ -192,6 +223,13 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     ALLOC_COPY(p->d_dec, dec);
     ALLOC_COPY(p->d_small, small_ids);
     ALLOC_COPY(p->d_large, large_ids);
+    ALLOC_COPY(p->d_split, split_ids);
+    p->n_split = (int)split_ids.size();
+    p->split_rows_max = split_rows_max;
+    if (part_len > 0) {
+        e = hipMalloc((void**)&p->d_part, (size_t)part_len * sizeof(float));
+        if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
+    }
     if (!large_ids.empty()) {
         p->n_large_batches = (int)((large_ids.size() + kMB - 1) / kMB);
         p->h_large_batches = new MBatch[p->n_large_batches];
@@ -250,6 +288,8 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_keys) (void)hipFree(p->d_keys);
     if (p->d_small) (void)hipFree(p->d_small);
     if (p->d_large) (void)hipFree(p->d_large);
+    if (p->d_split) (void)hipFree(p->d_split);
+    if (p->d_part) (void)hipFree(p->d_part);
     delete[] p->h_segs;
     delete[] p->h_pack_begin;
     delete[] p->h_large_batches;

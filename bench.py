@@ -83,6 +83,22 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int):
     return dict(encode=enc, select=sel, pack=pack, decode=dec, total=enc + sel + pack + dec)
 
 
+def pmc_traffic(workload: str, ef: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC profile of this
+    workload (profiles/<round>/pmc_<workload>_<ef>.json, written by
+    scripts/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of
+    this same bench command; FETCH_SIZE doubled per the gfx950 correction)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_{workload}_{ef}.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as fh:
+        ent = json.load(fh)["kernels"].get(kernel)
+    if not ent:
+        return None, None
+    return ent["bytes_per_launch"], os.path.relpath(paths[-1], REPO)
+
+
 def cpu_baseline(ef: str, seconds: float, rank: int, shapes, label: str):
     """Time the CPU oracle (a restatement of the reference hook) on the same bucket."""
     from oracle import arctopk as A
@@ -201,6 +217,8 @@ def main():
         roof["hook"] = {"algorithmic_bytes": alg["total"], "device_us": round(hook_s * 1e6, 1),
                         "achieved": round(alg["total"] / hook_s / 1e9, 1),
                         "frac": round(alg["total"] / hook_s / 1e9 / HBM_PEAK_GBS, 4)}
+    if roof is not None:
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.workload, args.ef, "k_encode")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),

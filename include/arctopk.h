@@ -59,11 +59,13 @@ typedef struct {
     int64_t numel;       /* bucket elements (bucket.buffer().numel())                  */
     int64_t sketch_len;  /* floats of the concatenated sketch: sum n*r (SKETCH) + d (RAW) */
     int64_t v_len;       /* floats of the concatenated projections: sum m*r over SKETCH   */
-    int64_t packed_len;  /* sum_k: selected elements (ref values_memory length, :261-263)  */
+    int64_t packed_len;  /* floats of the packed buffer: every segment's k_rows*m values,
+                            each segment starting 16-B aligned (<= 3 pad floats between)  */
     int64_t sel_rows;    /* sum of selected rows (length of the row list)                 */
     int64_t rows_total;  /* sum n (length of the slot map)                                */
     int32_t nseg;        /* gradient views in the bucket                                  */
     int32_t r;           /* sketch rank                                                   */
+    int64_t values_len;  /* sum_k: selected elements (ref values_memory length, :261-263)  */
 } arctopk_plan_info;
 
 /* Per-segment geometry (for the host-side mirror and tests). */

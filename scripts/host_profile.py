@@ -15,7 +15,9 @@ from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import GroupTopKSta
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29511")
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
-shapes = [[2048, 2048]] * 16
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import WORKLOADS  # noqa: E402
+shapes = WORKLOADS[os.environ.get("WORKLOAD", "headline")][1]
 buf = torch.randn(bucket_numel(shapes), device="cuda:0")
 b = SyntheticBucket(buf, shapes)
 st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback="ef14", seed=1)

@@ -20,7 +20,7 @@ if os.environ.get("SHAPES") == "resnet18":
 dev = "cuda:0"
 plan = BucketPlan(shapes, 4, 0.2, torch.float32, dev)
 n = plan.info.numel
-K = plan.info.packed_len
+K = plan.info.values_len
 G = torch.randn(n, device=dev)
 E = torch.randn(n, device=dev) * 0.1
 gE = torch.randn(n, device=dev)

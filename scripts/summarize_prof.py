@@ -3,6 +3,7 @@ from FETCH_SIZE (x2: gfx950 reports half of a wide coalesced stream, MI355X_MICR
 HBM section) and WRITE_SIZE (both counters in KiB)."""
 import csv
 import glob
+import json
 import os
 import sys
 from collections import defaultdict
@@ -43,3 +44,23 @@ for k in sorted(set(fetch) | set(write)):
     wa = 1024 * sum(w) / len(w) if w else float("nan")
     print(f"{k[:60]:60s} launches {len(f):5d}  read {fa/1e6:10.2f} MB  write {wa/1e6:10.2f} MB  "
           f"total {(fa + wa)/1e6:10.2f} MB")
+
+# machine-readable per-launch traffic for bench.py's roofline.traffic
+out = {}
+for k in sorted(set(fetch) | set(write)):
+    f = fetch.get(k, [])
+    w = write.get(k, [])
+    name = k.split("(")[0].split("<")[0].replace("void ", "").strip()
+    if f and w:
+        ent = out.setdefault(name, {"launches": 0, "read_bytes": 0.0, "write_bytes": 0.0})
+        ent["launches"] += len(f)
+        ent["read_bytes"] += 2 * 1024 * sum(f)
+        ent["write_bytes"] += 1024 * sum(w)
+for ent in out.values():
+    ent["read_bytes"] = round(ent["read_bytes"] / ent["launches"])
+    ent["write_bytes"] = round(ent["write_bytes"] / ent["launches"])
+    ent["bytes_per_launch"] = ent["read_bytes"] + ent["write_bytes"]
+with open(os.path.join(root, "pmc_per_launch.json"), "w") as fh:
+    json.dump({"note": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads) + WRITE_SIZE, "
+                       "KiB -> bytes, averaged per launch; separate --pmc passes",
+               "kernels": out}, fh, indent=1)

@@ -74,7 +74,7 @@ def test_plan_geometry_matches_oracle(lib, shapes, ratio):
     st, segs, info = _describe(lib, shapes, 4, ratio)
     assert st == 0
     ref = A.segments(shapes, ratio)
-    sk = pk = 0
+    sk = pk = vals = 0
     for s, o in zip(segs, ref):
         assert (s.offset, s.n, s.m, s.k_rows) == (o.offset, o.n, o.m, o.k_rows)
         assert s.kind == o.kind
@@ -82,8 +82,11 @@ def test_plan_geometry_matches_oracle(lib, shapes, ratio):
         assert s.sketch_off == sk and s.packed_off == pk
         sk += s.n if s.kind == N.SEG_RAW else s.n * 4
         pk += s.k_rows * s.m
+        vals += s.k_rows * s.m
+        pk = (pk + 3) // 4 * 4  # segments start 16-B aligned in the packed buffer
     assert info.numel == sum(o.numel for o in ref)
     assert info.packed_len == pk and info.sketch_len == sk
+    assert info.values_len == vals == sum(A.cal_k(o.shape, ratio) for o in ref)
 
 
 def test_plan_errors(lib):

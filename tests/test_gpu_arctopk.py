@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 MIX = [[10], [40, 16], [4, 3, 3, 3], [16, 8, 3, 3], [16, 8, 1, 1], [96, 40], [7], [256, 512],
-       [33, 130], [1000], [64, 70], [8, 8, 5, 5], [130, 2048]]
+       [33, 130], [1000], [64, 70], [8, 8, 5, 5], [130, 2048], [9, 5632], [6, 4101]]
 # Segments past the single-block select (> 15360 rows): multi-block radix select, and more
 # of them than one select batch holds (48).
 LARGE = [[20000, 8], [30], [512, 512, 3, 3], [16000, 3], [7, 9]] + [[15400, 2]] * 50
@@ -53,7 +53,7 @@ def test_plan_geometry_matches_oracle():
     segs = A.segments(MIX, 0.2)
     for s, o in zip(plan.segments, segs):
         assert (s.offset, s.n, s.m, s.k_rows) == (o.offset, o.n, o.m, o.k_rows)
-    assert plan.info.packed_len == sum(o.k for o in segs)
+    assert plan.info.values_len == sum(o.k for o in segs)
 
 
 @pytest.mark.parametrize("ef,which", [("noef", "mix"), ("ef14", "mix"), ("ef21", "mix"),
@@ -112,7 +112,7 @@ def test_kernel_phases_bitexact(ef, which):
     vals = A.pack(Xo, rows, segs, ef)
     plan.pack(g_d, e_d, N.EF_CODE[ef], stream)
     torch.cuda.synchronize()
-    assert_bitwise(plan.packed_view, vals, "packed values")
+    assert_bitwise(plan.packed_values(), vals, "packed values")
     if ef == "ef14":
         assert_bitwise(e_d, Xo, "EF14 residual")
     elif ef == "ef21":
@@ -224,7 +224,7 @@ def test_headline_bucket_properties(ef):
     torch.cuda.synchronize()
     plan = st._plans[0][1]
     k_rows = plan.segments[0].k_rows
-    assert k_rows == 409 and plan.info.packed_len == 13_402_112
+    assert k_rows == 409 and plan.info.values_len == 13_402_112
     rows = _gpu_rows(plan)
     energy = torch.empty(plan.info.rows_total, device=DEV)
     plan.row_energy(1, energy, torch.cuda.current_stream().cuda_stream)

@@ -141,4 +141,4 @@ def test_hook_inside_ddp_rccl():
         segs = A.segments(shapes, 0.2)
         ref_k = sum(s.k for s in segs)
         plan = st._plans[b][1]
-        assert plan.info.packed_len == ref_k
+        assert plan.info.values_len == ref_k

@@ -76,7 +76,9 @@ def test_projection_prefetch_is_transparent():
     vals = []
     for _ in range(6):
         seed = ps.consume_seed(rng)
-        vals.append((seed, ps.get(seed, ms, torch.float32).clone()))
+        slot = ps.get(seed, ms, torch.float32)
+        vals.append((seed, slot.host.clone()))
+        ps.release(slot)
         ps.prefetch([ms] * 4, torch.float32)
     ps.close()
     assert ps.hits >= 4
