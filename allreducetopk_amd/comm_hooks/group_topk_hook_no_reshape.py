@@ -93,7 +93,13 @@ class BucketPlan:
         self.packed = torch.zeros(max(1, info.packed_len), dtype=torch.float32, device=dev)
         self.rowlist = torch.empty(max(1, info.sel_rows), dtype=torch.int32, device=dev)
         self.slotmap = torch.empty(max(1, info.rows_total), dtype=torch.int32, device=dev)
-        self.V = torch.empty(max(1, info.v_len), dtype=torch.float32, device=dev)
+        # projections: a ring of device slots filled by H2D copies on a side stream, so the
+        # copy for call i+1 overlaps call i's kernels instead of sitting between them
+        self.V_ring = [torch.empty(max(1, info.v_len), dtype=torch.float32, device=dev)
+                       for _ in range(self.V_RING)]
+        self._v_used = [None] * self.V_RING  # event after the encode that last read the slot
+        self._v_streams = [None] * self.V_RING
+        self._v_next = 0
         self.groups = self._make_groups()
         bits = dtype_bits(dtype)
         # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
@@ -102,6 +108,31 @@ class BucketPlan:
 
     PIPELINE_GROUPS = 4             # packed all-reduce split into up to this many pieces
     PIPELINE_MIN_BYTES = 4 << 20    # ... each at least this large (RCCL efficiency)
+    V_RING = 3                      # projection slots in flight per bucket
+
+    def stage_projection(self, host: torch.Tensor, copy_stream, stream):
+        """Copy this call's projections `host` (pinned) into the next ring slot on
+        `copy_stream`; `stream` waits for the copy.  Returns (slot index, device buffer)."""
+        i = self._v_next
+        self._v_next = (i + 1) % len(self.V_ring)
+        buf = self.V_ring[i]
+        if self._v_streams[i] is not copy_stream:  # allocator: the slot is also used there
+            buf.record_stream(copy_stream)
+            self._v_streams[i] = copy_stream
+        if self._v_used[i] is not None:  # the encode that read this slot must be done
+            copy_stream.wait_event(self._v_used[i])
+        n = int(self.info.v_len)
+        with torch.cuda.stream(copy_stream):
+            buf[:n].copy_(host[:n], non_blocking=True)
+        ready = torch.cuda.Event()
+        ready.record(copy_stream)
+        stream.wait_event(ready)
+        return i, buf
+
+    def projection_consumed(self, i: int, stream) -> None:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._v_used[i] = ev
 
     def _make_groups(self):
         """Contiguous segment ranges with roughly equal packed bytes: (b, e, lo, hi)."""
@@ -208,6 +239,36 @@ class GroupTopKState(HookState):
         # the packed payload device -> pinned host -> device around the all-reduce
         self.host_staged = False
         self._host_buf = None
+        # multi-GPU overlap (not in the reference, which blocks per collective): at world
+        # size > 1 each bucket's packed all-reduce and decode leave the caller's stream
+        # (decode on a side stream, returned Future carries its event), so the next
+        # bucket's encode runs while this one is on the wire; sketches use a second
+        # communicator so they never queue behind a packed all-reduce
+        self.async_exchange = True
+        self._copy_streams: Dict[int, torch.cuda.Stream] = {}
+        self._decode_streams: Dict[int, torch.cuda.Stream] = {}
+        self._pending: Dict[int, torch.cuda.Event] = {}  # bucket -> its decode-done event
+        self._sketch_groups: Dict[object, object] = {}
+
+    def _side_stream(self, table: Dict[int, "torch.cuda.Stream"], device) -> "torch.cuda.Stream":
+        idx = torch.device(device).index or 0
+        s = table.get(idx)
+        if s is None:
+            s = torch.cuda.Stream(device=device)
+            table[idx] = s
+        return s
+
+    def _sketch_group(self, group):
+        """A second communicator over the same ranks for the sketch all-reduces (created
+        collectively on the first compressed call; only for the world group, whose every
+        rank runs this hook)."""
+        if group is not dist.group.WORLD and group.size() != dist.get_world_size():
+            return group
+        g = self._sketch_groups.get(group)
+        if g is None:
+            g = dist.new_group(ranks=list(range(dist.get_world_size())))
+            self._sketch_groups[group] = g
+        return g
 
     def _after_load(self) -> None:
         # prefetched projections were keyed on seeds of the old rng position
@@ -342,14 +403,21 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     _reseed_global(seed)
 
     plan = state._plan_for(bucket)
-    stream = torch.cuda.current_stream(input_tensor.device)
+    dev = input_tensor.device
+    stream = torch.cuda.current_stream(dev)
     sid = stream.cuda_stream
+    pend = state._pending.pop(b, None)
+    if pend is not None:  # this bucket's previous decode (side stream) must be done
+        stream.wait_event(pend)
     dtype = input_tensor.dtype
     slot = state._proj.get(seed, plan.ms, dtype)
-    V = plan.V
-    if plan.info.v_len:  # 512 KiB pinned H2D at headline, stream-ordered before encode
-        V[:plan.info.v_len].copy_(slot.host[:plan.info.v_len], non_blocking=True)
-    state._proj.release(slot, stream)  # refilled only after this copy completed
+    vslot, V = -1, plan.V_ring[0]
+    if plan.info.v_len:  # 512 KiB pinned H2D at headline, on a side stream, ahead of encode
+        cs = state._side_stream(state._copy_streams, dev)
+        vslot, V = plan.stage_projection(slot.host, cs, stream)
+        state._proj.release(slot, cs)  # refilled only after this copy completed
+    else:
+        state._proj.release(slot)
     state._proj.prefetch(state._upcoming_ms(bucket), dtype)
 
     evs = None
@@ -359,26 +427,54 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             evs = {}
             state.phase_events.append(evs)
 
-    def mark(name):
+    def mark(name, on=None):
         if evs is not None:
             e = torch.cuda.Event(enable_timing=True)
-            e.record(stream)
+            e.record(on if on is not None else stream)
             evs[name] = e
 
     mark("start")
     plan.encode(input_tensor, err, ef, err_in, V, sid)
+    if vslot >= 0:
+        plan.projection_consumed(vslot, stream)
     mark("encode")
 
+    overlap = world_size > 1 and state.async_exchange and not state.host_staged
     if world_size > 1:  # a SUM over one rank is the identity: nothing to exchange
-        dist.all_reduce(plan.sketch_view, group=group, async_op=False)
+        sk_group = state._sketch_group(group) if overlap else group
+        dist.all_reduce(plan.sketch_view, group=sk_group, async_op=False)
     mark("sketch_allreduce")
     plan.select(world_size, sid)
     mark("select")
     state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum
+    if overlap:
+        # pack group g, start its all-reduce (RCCL stream), pack g+1 ...; decode runs on a
+        # side stream that waits for each group's collective, so the caller's stream is
+        # free for the next bucket's encode while this bucket is on the wire
+        works = []
+        for b_, e_, lo, hi in plan.groups:
+            plan.pack_range(b_, e_, input_tensor, err, ef, sid)
+            works.append(dist.all_reduce(plan.packed[lo:hi], group=group, async_op=True))
+        mark("pack")
+        ds = state._side_stream(state._decode_streams, dev)
+        ds.wait_stream(stream)  # select's slot map, the packed buffer's pack
+        input_tensor.record_stream(ds)
+        with torch.cuda.stream(ds):
+            for (b_, e_, lo, hi), w in zip(plan.groups, works):
+                w.wait()  # the side stream (current here) waits for the collective
+                plan.decode_range(b_, e_, world_size, ef, gerr, input_tensor, ds.cuda_stream)
+            mark("decode", ds)
+            done = torch.cuda.Event()
+            done.record(ds)
+            state._pending[b] = done
+            state.maybe_increase_iter(bucket)
+            # a device-aware Future: wait()/value() make the waiter's stream wait for decode
+            fut = torch.futures.Future(devices=[dev])
+            fut.set_result(input_tensor)
+        return fut
     if world_size > 1 and len(plan.groups) > 1 and not state.host_staged:
-        # pipelined exchange: pack group g, start its all-reduce (RCCL stream), pack g+1;
-        # then decode each group once its collective is done (the current stream waits
-        # on the collective's event, the host does not block)
+        # pipelined exchange on the caller's stream: pack group g, start its all-reduce,
+        # pack g+1; decode each group once its collective is done
         works = []
         for b_, e_, lo, hi in plan.groups:
             plan.pack_range(b_, e_, input_tensor, err, ef, sid)

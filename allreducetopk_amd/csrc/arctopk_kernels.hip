@@ -54,11 +54,11 @@ __device__ __forceinline__ float4 ef_apply4(const float4* __restrict__ g4, float
 template <int EF, bool ERR_IN>
 __device__ __forceinline__ float ef_apply1(const float* __restrict__ g, const float* __restrict__ e,
                                            int64_t i) {
-    float x = g[i];
+    float x = __builtin_nontemporal_load(g + i);
     if constexpr (EF == ARCTOPK_EF14) {
-        if constexpr (ERR_IN) x += e[i];
+        if constexpr (ERR_IN) x += __builtin_nontemporal_load(e + i);
     } else if constexpr (EF == ARCTOPK_EF21) {
-        x -= e[i];
+        x -= __builtin_nontemporal_load(e + i);
     }
     return x;
 }
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         float* out = sketch + s.sketch_off + t.row0;
         for (int64_t i = tid; i < t.nrows; i += 256) {
             const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, i);
-            if constexpr (WRITE_E) E[base + i] = x;
+            if constexpr (WRITE_E) __builtin_nontemporal_store(x, E + base + i);
             out[i] = x;
         }
         return;
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         const int cnt = (int)t.nrows * m;
         for (int i = tid; i < cnt; i += 256) {
             const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, i);
-            if constexpr (WRITE_E) E[base + i] = x;
+            if constexpr (WRITE_E) __builtin_nontemporal_store(x, E + base + i);
             tile[i] = x;
         }
         __syncthreads();
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     }
     float* const out_base = t.part < 0 ? sketch + s.sketch_off
                                        : part_buf + s.part_off + (int64_t)t.part * s.n * R;
-    const int64_t row_end = t.row0 + t.nrows;
+    const int64_t rs = t.rstride;
     if (t.mode == ENC_ROW_VEC) {
         // Software-pipelined stream: a wave walks its rows in steps of 64*U float4
         // (U per lane) with two register buffers: the loads of the next step are in
@@ -179,8 +179,8 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
             for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: no exec-masked blocks
                 const int c = min(st_ * 64 * U + u * 64 + lane, m4 - 1);
-                gx[u] = g4[c];
-                if constexpr (LOAD_E) ex[u] = e4[c];
+                gx[u] = ld_stream(g4 + c);
+                if constexpr (LOAD_E) ex[u] = ld_stream(e4 + c);
             }
         };
         auto consume = [&](float4 (&gx)[U], float4 (&ex)[U], int64_t r_, int st_) {
@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                     x.x -= ex[u].x; x.y -= ex[u].y; x.z -= ex[u].z; x.w -= ex[u].w;
                 }
                 if constexpr (WRITE_E) {
-                    if (ok) e4[c] = x;
+                    if (ok) st_stream(e4 + c, x);
                 }
                 if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
                 float4 vq[4];  // !VLDS, R = 4: the 4 columns' V rows, 16-B loads from L2
@@ -242,32 +242,34 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                 for (int j = 0; j < R; ++j) acc[j] = 0.f;
             }
         };
-        // cursor over (row, step) pairs of this wave: rows row0+wave, +4, ...
-        int64_t ra = t.row0 + wave;
+        // cursor over (tile row q, step) pairs of this wave: q = wave, wave + 4, ...
+        const int64_t nq = t.nrows;
+        int64_t qa = wave;
         int sa = 0;
-        if (ra < row_end) issue(ga, ea, ra, sa);
-        while (ra < row_end) {
-            int64_t rb = ra;
+        if (qa < nq) issue(ga, ea, t.row0 + qa * rs, sa);
+        while (qa < nq) {
+            int64_t qb = qa;
             int sb = sa + 1;
-            if (sb == steps) { sb = 0; rb += 4; }
-            if (rb < row_end) issue(gb, eb, rb, sb);
-            consume(ga, ea, ra, sa);
-            if (rb >= row_end) break;
-            ra = rb;
+            if (sb == steps) { sb = 0; qb += 4; }
+            if (qb < nq) issue(gb, eb, t.row0 + qb * rs, sb);
+            consume(ga, ea, t.row0 + qa * rs, sa);
+            if (qb >= nq) break;
+            qa = qb;
             sa = sb + 1;
-            if (sa == steps) { sa = 0; ra += 4; }
-            if (ra < row_end) issue(ga, ea, ra, sa);
-            consume(gb, eb, rb, sb);
+            if (sa == steps) { sa = 0; qa += 4; }
+            if (qa < nq) issue(ga, ea, t.row0 + qa * rs, sa);
+            consume(gb, eb, t.row0 + qb * rs, sb);
         }
     } else {  // ENC_ROW_SCALAR
-        for (int64_t row = t.row0 + wave; row < row_end; row += 4) {
+        for (int64_t q = wave; q < t.nrows; q += 4) {
+            const int64_t row = t.row0 + q * rs;
             const int64_t base = s.offset + row * m + c0;
             float acc[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[j] = 0.f;
             for (int c = lane; c < cl; c += 64) {
                 const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, c);
-                if constexpr (WRITE_E) E[base + c] = x;
+                if constexpr (WRITE_E) __builtin_nontemporal_store(x, E + base + c);
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     float v;
@@ -727,9 +729,9 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int c = min(c0 + u * 64 + lane, m4 - 1);
-                    if constexpr (EF == ARCTOPK_EF_NONE) a[u] = g4[c];
-                    else if constexpr (EF == ARCTOPK_EF14) a[u] = e4[c];
-                    else { a[u] = g4[c]; b[u] = e4[c]; }
+                    if constexpr (EF == ARCTOPK_EF_NONE) a[u] = ld4<kNtPack>(g4 + c);
+                    else if constexpr (EF == ARCTOPK_EF14) a[u] = ld4<kNtPack>(e4 + c);
+                    else { a[u] = ld4<kNtPack>(g4 + c); b[u] = ld4<kNtPack>(e4 + c); }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -739,13 +741,13 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                             d4[c] = a[u];
                         } else if constexpr (EF == ARCTOPK_EF14) {
                             d4[c] = a[u];
-                            e4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                            st4<kNtPack>(e4 + c, make_float4(0.f, 0.f, 0.f, 0.f));
                         } else {
                             const float4 dv = make_float4(a[u].x - b[u].x, a[u].y - b[u].y,
                                                           a[u].z - b[u].z, a[u].w - b[u].w);
                             d4[c] = dv;
-                            e4[c] = make_float4(b[u].x + dv.x, b[u].y + dv.y, b[u].z + dv.z,
-                                                b[u].w + dv.w);
+                            st4<kNtPack>(e4 + c, make_float4(b[u].x + dv.x, b[u].y + dv.y,
+                                                             b[u].z + dv.z, b[u].w + dv.w));
                         }
                     }
                 }
@@ -848,12 +850,13 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                 if constexpr (EF == ARCTOPK_EF21) {
 #pragma unroll 4
                     for (int c = lane; c < m4; c += 64) {
-                        const float4 g = g4[c];
-                        o4[c] = make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f);
+                        const float4 g = ld4<kNtDecode>(g4 + c);
+                        st4<kNtDecode>(o4 + c, make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f));
                     }
                 } else {
 #pragma unroll 8
-                    for (int c = lane; c < m4; c += 64) o4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    for (int c = lane; c < m4; c += 64)
+                        st4<kNtDecode>(o4 + c, make_float4(0.f, 0.f, 0.f, 0.f));
                 }
             } else {
                 const float4* p4 = reinterpret_cast<const float4*>(pk + (int64_t)slot * m);
@@ -861,11 +864,11 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                 for (int c = lane; c < m4; c += 64) {
                     float4 v = sc(p4[c]);
                     if constexpr (EF == ARCTOPK_EF21) {
-                        const float4 g = g4[c];
+                        const float4 g = ld4<kNtDecode>(g4 + c);
                         v = make_float4(g.x + v.x, g.y + v.y, g.z + v.z, g.w + v.w);
-                        g4[c] = v;
+                        st4<kNtDecode>(g4 + c, v);
                     }
-                    o4[c] = v;
+                    st4<kNtDecode>(o4 + c, v);
                 }
             }
         }

@@ -111,6 +111,8 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     int64_t target = kEncTargetBlocks;
     if (const char* env = std::getenv("ARCTOPK_ENC_TARGET_BLOCKS")) target = std::max(1, std::atoi(env));  // tuning
     const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(8192, row_work / target));
+    bool interleave = true;  // tuning switch (A/B): interleaved row tiles vs contiguous ranges
+    if (const char* env = std::getenv("ARCTOPK_ENC_INTERLEAVE")) interleave = std::atoi(env) != 0;
     int64_t part_len = 0, split_rows_max = 0;
     for (size_t i = 0; i < segs.size(); ++i) {
         const arctopk_segment& s = segs[i];
@@ -133,11 +135,11 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         if (s.kind == ARCTOPK_SEG_RAW) {
             const int64_t per = 4096;
             for (int64_t e = 0; e < s.n; e += per)
-                enc.push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e), 0, 1, -1, 0});
+                enc.push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e), 0, 1, -1, 1});
         } else if (s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536) {
             for (int64_t row = 0; row < s.n; row += kTileRows)
                 enc.push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(kTileRows, s.n - row),
-                                      0, (int32_t)s.m, -1, 0});
+                                      0, (int32_t)s.m, -1, 1});
             lds = std::max<int>(lds, (int)(kTileRows * s.m * 4 + s.m * r * 4));
         } else {
             const int mode = g.vec ? ENC_ROW_VEC : ENC_ROW_SCALAR;
@@ -154,12 +156,19 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 split_rows_max = std::max<int64_t>(split_rows_max, s.n);
             }
             const int64_t per = std::max<int64_t>(4, tile_elems / std::min<int64_t>(clen, s.m));
+            const int64_t ntiles = (s.n + per - 1) / per;
             for (int part = 0; part < nparts; ++part) {
                 const int64_t c0 = part * clen;
                 const int64_t cl = std::min<int64_t>(clen, s.m - c0);
-                for (int64_t row = 0; row < s.n; row += per)
-                    enc.push_back(EncTile{(int32_t)i, mode, row, std::min(per, s.n - row), (int32_t)c0,
-                                          (int32_t)cl, nparts > 1 ? part : -1, 0});
+                for (int64_t ti = 0; ti < ntiles; ++ti) {
+                    if (interleave)  // rows ti, ti + ntiles, ...: consecutive blocks, adjacent rows
+                        enc.push_back(EncTile{(int32_t)i, mode, ti, (s.n - ti + ntiles - 1) / ntiles,
+                                              (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1,
+                                              (int32_t)ntiles});
+                    else
+                        enc.push_back(EncTile{(int32_t)i, mode, ti * per, std::min(per, s.n - ti * per),
+                                              (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1, 1});
+                }
                 lds = std::max<int>(lds, (int)(cl * r * 4));
             }
         }

@@ -132,6 +132,9 @@ def main():
     ap.add_argument("--ef", default="ef14", choices=["noef", "ef14", "ef21"])
     ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS),
                     help="bucket shape set (headline = the BASELINE metric's bucket)")
+    ap.add_argument("--buckets", type=int, default=4,
+                    help="buckets per step (a backward's worth, hooked in order as DDP does); "
+                         "each is one workload bucket")
     ap.add_argument("--ratio", type=float, default=0.2)
     ap.add_argument("--r", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -164,25 +167,33 @@ def main():
     label, shapes = WORKLOADS[args.workload]
     n = bucket_numel(shapes)
     bucket_bytes = 4 * n
+    nb = args.buckets
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    buf = torch.randn(n, device=dev, generator=g)
-    bucket = SyntheticBucket(buf, shapes, index=0, is_last=True)
+    # one step = one backward's worth of buckets, hooked in bucket order as DDP does
+    buckets = [SyntheticBucket(torch.randn(n, device=dev, generator=g), shapes, index=i,
+                               is_last=(i == nb - 1)) for i in range(nb)]
     st = GroupTopKState(None, r=args.r, compress_ratio=args.ratio, start_compress_iter=0,
                         use_error_feedback=args.ef, seed=1234)
     st.host_staged = args.host_staged
+
+    def step():
+        futs = [group_topk_hook(st, bk) for bk in buckets]
+        for f in futs:  # DDP's finalize: the caller's stream waits for every bucket's future
+            f.wait()
+
     # warm-up (EF14: first call creates E; EF21: first call is the dense init)
     for _ in range(max(args.warmup, 2 if args.ef == "ef21" else 1)):
-        group_topk_hook(st, bucket)
+        step()
     torch.cuda.synchronize()
     if not args.no_phase_events:
         st.phase_events = []
-        st.phase_event_every = 4  # sample HIP events on every 4th timed call
+        st.phase_event_every = 8  # sample HIP events on every 8th timed hook call
 
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        group_topk_hook(st, bucket)
+        step()
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -192,16 +203,15 @@ def main():
 
     phase_ms = {}
     if st.phase_events:
-        order = ["start"] + PHASES
-        if args.host_staged:
-            order = order[:5] + ["d2h", "h2d"] + order[5:]
+        order = [p for p in ["start", "encode", "sketch_allreduce", "select", "pack", "d2h", "h2d",
+                             "packed_allreduce", "decode"] if p in st.phase_events[0]]
         for a, b in zip(order[:-1], order[1:]):
             ds = [ev[a].elapsed_time(ev[b]) for ev in st.phase_events]
             phase_ms[b] = statistics.mean(ds)
         phase_ms["hook_device_total"] = statistics.mean(
             ev["start"].elapsed_time(ev["decode"]) for ev in st.phase_events)
 
-    value = world * args.steps * bucket_bytes / elapsed / 1e9
+    value = world * args.steps * nb * bucket_bytes / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     alg = algorithmic_bytes(args.ef, shapes, args.ratio, args.r)
     roof = None
@@ -224,13 +234,17 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (N(0,1) fp32 gradients, per-rank seed)",
-        "config": {"workload": f"arctopk_{args.ef}_{label}"
+        "config": {"workload": f"arctopk_{args.ef}_{nb}x_{label}"
                                + ("_host_staged" if args.host_staged else ""),
                    "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
-                   "bucket_bytes": bucket_bytes, "parallelism": f"dp{world}",
+                   "bucket_bytes": bucket_bytes, "buckets_per_step": nb,
+                   "parallelism": f"dp{world}",
                    "collectives": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
-                                  + " all_reduce: sketch + packed values (pipelined in groups)"},
+                                  + " all_reduce: sketch (own communicator) + packed values "
+                                    "(pipelined in groups, decode overlapped with the next "
+                                    "bucket)"},
         "per_gpu_value": round(value / world, 2),
+        "ms_per_bucket": round(ms_per_step / nb, 4),
         "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
         "roofline": roof,
         "cpu_baseline": None,
