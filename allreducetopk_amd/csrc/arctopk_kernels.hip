@@ -109,7 +109,42 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         for (int i = tid; i < m * R; i += 256) vl[i] = Vs[i];
         const int64_t base = s.offset + t.row0 * m;
         const int cnt = (int)t.nrows * m;
-        for (int i = tid; i < cnt; i += 256) {
+        int done = 0;
+        if ((base & 3) == 0) {
+            // 16-B streams, all of a thread's loads issued before its stores (a store to E
+            // may not be reordered above a later load from E by the compiler)
+            constexpr int Q = 4;
+            constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
+            const int cnt4 = cnt >> 2;
+            const float4* g4 = reinterpret_cast<const float4*>(G + base);
+            float4* e4 = reinterpret_cast<float4*>(E + base);
+            float4* t4 = reinterpret_cast<float4*>(tile);
+            for (int q0 = tid; q0 < cnt4; q0 += 256 * Q) {
+                float4 gv[Q], ev[Q];
+#pragma unroll
+                for (int u = 0; u < Q; ++u) {
+                    const int q = min(q0 + u * 256, cnt4 - 1);
+                    gv[u] = ld_stream(g4 + q);
+                    if constexpr (LOAD_E) ev[u] = ld_stream(e4 + q);
+                }
+#pragma unroll
+                for (int u = 0; u < Q; ++u) {
+                    const int q = q0 + u * 256;
+                    if (q < cnt4) {
+                        float4 x = gv[u];
+                        if constexpr (EF == ARCTOPK_EF14 && ERR_IN) {
+                            x.x += ev[u].x; x.y += ev[u].y; x.z += ev[u].z; x.w += ev[u].w;
+                        } else if constexpr (EF == ARCTOPK_EF21) {
+                            x.x -= ev[u].x; x.y -= ev[u].y; x.z -= ev[u].z; x.w -= ev[u].w;
+                        }
+                        if constexpr (WRITE_E) st_stream(e4 + q, x);
+                        t4[q] = x;
+                    }
+                }
+            }
+            done = cnt4 << 2;
+        }
+        for (int i = done + tid; i < cnt; i += 256) {
             const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, i);
             if constexpr (WRITE_E) __builtin_nontemporal_store(x, E + base + i);
             tile[i] = x;
@@ -509,9 +544,17 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
             // rank the few keys of the threshold bin directly
             if (tid == 0) sh.ncand = 0;
             __syncthreads();
-            for (int i = tid; i < n; i += kST) {
-                const uint32_t key = keys[i];
-                if ((key & mask) == prefix) sh.cand[atomicAdd(&sh.ncand, 1u)] = key;
+            // wave-aggregated append: one LDS atomic per wave and round, not per key
+            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+            for (int b0 = 0; b0 < n; b0 += kST) {
+                const int i = b0 + tid;
+                const uint32_t key = i < n ? keys[i] : 0u;
+                const bool in = i < n && (key & mask) == prefix;
+                const uint64_t bm = __ballot(in);
+                uint32_t wb = 0;
+                if (lane == 0 && bm) wb = atomicAdd(&sh.ncand, (uint32_t)__popcll(bm));
+                wb = __shfl(wb, 0, 64);
+                if (in) sh.cand[wb + (uint32_t)__popcll(bm & lt)] = key;
             }
             __syncthreads();
             SEL_STAMP(6);
@@ -781,14 +824,51 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
         };
         for (uint32_t e = threadIdx.x; e < (uint32_t)min<int64_t>(pre, cnt); e += 256) dst[e] = one(e);
         const uint32_t body = cnt > pre ? (uint32_t)((cnt - pre) >> 2) : 0u;
-        for (uint32_t q = threadIdx.x; q < body; q += 256) {
-            const uint32_t e = (uint32_t)pre + (q << 2);
-            float4 v;
-            v.x = one(e);
-            v.y = one(e + 1);
-            v.z = one(e + 2);
-            v.w = one(e + 3);
-            *reinterpret_cast<float4*>(dst + e) = v;
+        // body: Q float4 of the packed output per thread and round, every gather load of the
+        // round issued before any residual store (the compiler may not move a load from E
+        // above a store to E; the elements of a chunk are distinct, so nothing aliases)
+        constexpr int Q = 4;
+        for (uint32_t q0 = threadIdx.x; q0 < body; q0 += 256 * Q) {
+            int64_t src[Q][4];
+            float va[Q][4], vb[Q][4];
+#pragma unroll
+            for (int u = 0; u < Q; ++u) {
+                const uint32_t e = (uint32_t)pre + (min(q0 + u * 256, body - 1) << 2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t r = div32(e + j, s.magic32);
+                    src[u][j] = s.offset + (int64_t)rs[r] * m + (e + j - r * (uint32_t)m);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < Q; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if constexpr (EF == ARCTOPK_EF_NONE) va[u][j] = G[src[u][j]];
+                    else if constexpr (EF == ARCTOPK_EF14) va[u][j] = E[src[u][j]];
+                    else { va[u][j] = G[src[u][j]]; vb[u][j] = E[src[u][j]]; }
+                }
+#pragma unroll
+            for (int u = 0; u < Q; ++u) {
+                const uint32_t q = q0 + u * 256;
+                if (q < body) {
+                    const uint32_t e = (uint32_t)pre + (q << 2);
+                    float vp[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if constexpr (EF == ARCTOPK_EF_NONE) {
+                            vp[j] = va[u][j];
+                        } else if constexpr (EF == ARCTOPK_EF14) {
+                            vp[j] = va[u][j];
+                            E[src[u][j]] = 0.f;
+                        } else {
+                            vp[j] = va[u][j] - vb[u][j];
+                            E[src[u][j]] = vb[u][j] + vp[j];
+                        }
+                    }
+                    *reinterpret_cast<float4*>(dst + e) = make_float4(vp[0], vp[1], vp[2], vp[3]);
+                }
+            }
         }
         for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256) dst[e] = one(e);
         return;
@@ -833,6 +913,7 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                                                 const float* __restrict__ packed,
                                                 const int32_t* __restrict__ slotmap, Scale sc,
                                                 float* __restrict__ gE, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float dlds[];  // small-m chunk tile
     const Chunk ch = chunks[blockIdx.x];
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
@@ -875,10 +956,11 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
         return;
     }
     if (m >= 4 && m < 256) {
-        // small m (3x3 / 1x1 convs): rows are too short for a wave each.  Selected rows
-        // of the chunk own consecutive slots (the row list is ascending), so their packed
-        // values are one contiguous range: stream-fill the chunk (zeros, or gE for EF21),
-        // then scatter that range row by row from a slot -> row table in LDS.
+        // small m (3x3 / 1x1 convs): rows are too short for a wave each.  The chunk is
+        // composed in LDS -- fill (zeros, or gE for EF21), then the selected rows, whose
+        // packed values are one contiguous range (the row list is ascending) -- and then
+        // written once with 16-B streaming stores: no partial-line double writes to HBM.
+        // Tile index t = e + a, a = base mod 4, so 16-B output groups are 16-B LDS groups.
         __shared__ int32_t rows_s[kSmallTileRows];
         __shared__ int32_t s_first[4], s_cnt[4];
         const int nr = (int)ch.nrows;
@@ -907,36 +989,57 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
             const int32_t sl = sm[r];
             if (sl >= 0) rows_s[sl - first] = r;
         }
-        // fill
-        const uint32_t cnt = (uint32_t)(nr * m);
-        const int64_t pre = min<int64_t>((4 - (base & 3)) & 3, cnt);  // to the first 16-B boundary
-        const uint32_t body = (uint32_t)((cnt - pre) >> 2);
-        for (uint32_t e = threadIdx.x; e < (uint32_t)pre; e += 256)
-            out[base + e] = EF == ARCTOPK_EF21 ? gE[base + e] + 0.f : 0.f;
-        for (uint32_t q = threadIdx.x; q < body; q += 256) {
-            const int64_t e = base + pre + ((int64_t)q << 2);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (EF == ARCTOPK_EF21) {
-                const float4 g = *reinterpret_cast<const float4*>(gE + e);
-                v = make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f);
+        const int cnt = nr * m;
+        const int a = (int)(base & 3);
+        const int ngroups = (a + cnt + 3) >> 2;
+        float* const ob = out - a + base;  // ob[t] = out[base + e]: 16-B aligned at t % 4 == 0
+        // 1. fill
+        for (int gi = threadIdx.x; gi < ngroups; gi += 256) {
+            const int t0 = gi << 2;
+            if (t0 >= a && t0 + 4 <= a + cnt) {
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (EF == ARCTOPK_EF21) {
+                    const float4 g = ld4<kNtDecode>(reinterpret_cast<const float4*>(gE - a + base + t0));
+                    v = make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f);
+                }
+                *reinterpret_cast<float4*>(dlds + t0) = v;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = t0 + j;
+                    if (t >= a && t < a + cnt)
+                        dlds[t] = EF == ARCTOPK_EF21 ? gE[base + t - a] + 0.f : 0.f;
+                }
             }
-            *reinterpret_cast<float4*>(out + e) = v;
         }
-        for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256)
-            out[base + e] = EF == ARCTOPK_EF21 ? gE[base + e] + 0.f : 0.f;
-        __syncthreads();  // fill stores land before the selected rows overwrite them
-        // selected rows
+        __syncthreads();
+        // 2. the selected rows
         const float* src = pk + (int64_t)first * m;
         const uint32_t np = (uint32_t)(nsel * m);
         for (uint32_t p = threadIdx.x; p < np; p += 256) {
             const uint32_t j = div32(p, s.magic32);
-            const int64_t e = base + (int64_t)rows_s[j] * m + (p - j * (uint32_t)m);
+            const int le = rows_s[j] * m + (int)(p - j * (uint32_t)m);
             float v = sc(src[p]);
             if constexpr (EF == ARCTOPK_EF21) {
-                v = gE[e] + v;
-                gE[e] = v;
+                v = gE[base + le] + v;
+                gE[base + le] = v;
             }
-            out[e] = v;
+            dlds[le + a] = v;
+        }
+        __syncthreads();
+        // 3. one streaming write of the chunk
+        for (int gi = threadIdx.x; gi < ngroups; gi += 256) {
+            const int t0 = gi << 2;
+            if (t0 >= a && t0 + 4 <= a + cnt) {
+                st4<kNtDecode>(reinterpret_cast<float4*>(ob + t0),
+                               *reinterpret_cast<const float4*>(dlds + t0));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = t0 + j;
+                    if (t >= a && t < a + cnt) ob[t] = dlds[t];
+                }
+            }
         }
         return;
     }
@@ -1149,9 +1252,9 @@ extern "C" int arctopk_decode_segments(const arctopk_plan* p, int32_t seg_begin,
     const Chunk* ch = p->d_dec + c0;
     const Scale sc = make_scale(ws);
     if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL(k_decode<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+        hipLaunchKernelGGL(k_decode<ARCTOPK_EF21>, grid, block, (size_t)p->dec_lds_bytes, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL(k_decode<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+        hipLaunchKernelGGL(k_decode<ARCTOPK_EF_NONE>, grid, block, (size_t)p->dec_lds_bytes, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();

@@ -11,7 +11,8 @@ constexpr int kMaxR = 8;           // sketch rank supported by the kernels
 constexpr int kTileRows = 256;     // rows of one small-m encode tile (thread per row)
 constexpr int kSmallM = 64;        // m below this: thread-per-row tiles; else wave-per-row
 constexpr int kVLdsMaxBytes = 64 * 1024;  // V staged in LDS up to this size, else read from L2
-constexpr int kChunkElems = 16384; // target elements per pack/decode work chunk
+constexpr int kChunkElems = 8192;  // target elements per pack/decode work chunk (8192 beat
+                                   // 16384 by 3 % on the headline, one 2048-row per wave)
 constexpr int kEncTargetBlocks = 2048;  // encode blocks a bucket's wave-per-row work aims at
                                         // (measured: 2048 beats 1024 on 256 CUs at 3 blocks/CU)
 constexpr int kSmallSelRows = 15360;  // rows up to this: keys in LDS (60 KiB + statics < 64 KiB)
@@ -127,6 +128,7 @@ struct arctopk_plan {
     int n_dec;
     int32_t* h_pack_begin;        // [nseg + 1]: first pack chunk of each segment
     int32_t* h_dec_begin;         // [nseg + 1]: first decode chunk of each segment
+    int dec_lds_bytes;            // dynamic LDS of the decode launch (small-m chunk tiles)
     uint32_t* d_keys;             // select workspace: one key per row
     int32_t* d_small;             // segments selected by the fused one-block kernel
     int n_small;

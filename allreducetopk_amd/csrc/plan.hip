@@ -101,6 +101,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     std::vector<Chunk> pack, dec;
     std::vector<int32_t> pack_begin, dec_begin;
     int lds = 0;
+    int64_t dec_lds = 0;
     // Encode work sizing: tiles of wave-per-row segments hold enough rows that the
     // bucket yields ~kEncTargetBlocks blocks (a bucket may hold ONE tensor: a DDP bucket
     // of a 46 MB MLP weight must still fill 256 CUs), within [8K, 64K] elements per block.
@@ -111,6 +112,9 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     int64_t target = kEncTargetBlocks;
     if (const char* env = std::getenv("ARCTOPK_ENC_TARGET_BLOCKS")) target = std::max(1, std::atoi(env));  // tuning
     const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(8192, row_work / target));
+    int64_t pack_elems = kChunkElems, dec_elems = kChunkElems;  // tuning switches (A/B)
+    if (const char* env = std::getenv("ARCTOPK_PACK_CHUNK")) pack_elems = std::max(64, std::atoi(env));
+    if (const char* env = std::getenv("ARCTOPK_DEC_CHUNK")) dec_elems = std::max(64, std::atoi(env));
     bool interleave = true;  // tuning switch (A/B): interleaved row tiles vs contiguous ranges
     if (const char* env = std::getenv("ARCTOPK_ENC_INTERLEAVE")) interleave = std::atoi(env) != 0;
     int64_t part_len = 0, split_rows_max = 0;
@@ -180,17 +184,19 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         // (rows of >= 256 elements go one per wave: at least 4 rows per chunk)
         const int64_t min_rows = s.m >= 256 ? 4 : 1;
         {
-            int64_t per = std::max<int64_t>(min_rows, kChunkElems / s.m);
+            int64_t per = std::max<int64_t>(min_rows, pack_elems / s.m);
             if (small_tile) per = std::min<int64_t>(per, kSmallTileRows);
             for (int64_t j = 0; j < s.k_rows; j += per)
                 pack.push_back(Chunk{(int32_t)i, 0, j, std::min(per, s.k_rows - j)});
         }
         // ---- decode chunks: all rows
         {
-            int64_t per = std::max<int64_t>(min_rows, kChunkElems / s.m);
-            if (small_tile) per = std::min<int64_t>(per, kSmallTileRows);
+            int64_t per = std::max<int64_t>(min_rows, dec_elems / s.m);
+            if (small_tile)  // the chunk tile lives in LDS: <= 64 KiB
+                per = std::min<int64_t>(std::min<int64_t>(per, kSmallTileRows), 16000 / s.m);
             for (int64_t row = 0; row < s.n; row += per)
                 dec.push_back(Chunk{(int32_t)i, 0, row, std::min(per, s.n - row)});
+            if (small_tile) dec_lds = std::max<int64_t>(dec_lds, (std::min(per, s.n) * s.m + 4) * 4);
         }
     }
 
@@ -216,6 +222,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     std::copy(pack_begin.begin(), pack_begin.end(), p->h_pack_begin);
     std::copy(dec_begin.begin(), dec_begin.end(), p->h_dec_begin);
     p->enc_lds_bytes = lds;
+    p->dec_lds_bytes = (int)dec_lds;
     p->n_small = (int)small_ids.size();
     p->n_large = (int)large_ids.size();
     p->small_lds = (int)(((small_rows + 3) & ~3) * 4 + 16);

@@ -53,6 +53,40 @@ WORKLOADS = {
 PHASES = ["encode", "sketch_allreduce", "select", "pack", "packed_allreduce", "decode"]
 
 
+def resnet18_cifar_shapes():
+    """Parameter shapes of the CIFAR ResNet-18 of configs[1] in definition order (the
+    reference's cifar10/resnet.py: 3x3 stem, BasicBlock [2, 2, 2, 2], 1x1 shortcuts,
+    BatchNorm weight + bias, Linear(512, 10)); 62 tensors, 11.17 M parameters."""
+    shapes = [[64, 3, 3, 3], [64], [64]]
+    cin = 64
+    for planes, stride in ((64, 1), (128, 2), (256, 2), (512, 2)):
+        for b in range(2):
+            s_ = stride if b == 0 else 1
+            shapes += [[planes, cin, 3, 3], [planes], [planes], [planes, planes, 3, 3], [planes], [planes]]
+            if s_ != 1 or cin != planes:
+                shapes += [[planes, cin, 1, 1], [planes], [planes]]
+            cin = planes
+    return shapes + [[10, 512], [10]]
+
+
+def ddp_buckets(shapes, first_cap=1 << 20, cap=25 << 20, elem_bytes=4):
+    """DDP's bucketing as the Reducer sees it: parameters in reverse definition order (the
+    order gradients become ready), a first bucket of <= 1 MiB, then <= 25 MiB buckets
+    (DistributedDataParallel defaults; a tensor larger than the cap gets its own bucket)."""
+    out, cur, size = [], [], 0
+    for s_ in reversed(shapes):
+        nbytes = elem_bytes * bucket_numel([s_])
+        limit = first_cap if not out else cap
+        if cur and size + nbytes > limit:
+            out.append(cur)
+            cur, size = [], 0
+        cur.append(s_)
+        size += nbytes
+    if cur:
+        out.append(cur)
+    return out
+
+
 def algorithmic_bytes(ef: str, shapes, ratio: float, r: int):
     """Minimum HBM bytes per call, per phase (fp32, fused design).
 
@@ -99,9 +133,10 @@ def pmc_traffic(workload: str, ef: str, kernel: str):
     return ent["bytes_per_launch"], os.path.relpath(paths[-1], REPO)
 
 
-def cpu_baseline(ef: str, seconds: float, rank: int, shapes, label: str):
+def cpu_baseline(ef: str, seconds: float, rank: int, shapes, label: str, hook: str = "arc"):
     """Time the CPU oracle (a restatement of the reference hook) on the same bucket."""
     from oracle import arctopk as A
+    from oracle import sparse as S
     threads = torch.get_num_threads()
     g = torch.Generator().manual_seed(1000 + rank)
     n = bucket_numel(shapes)
@@ -114,12 +149,16 @@ def cpu_baseline(ef: str, seconds: float, rank: int, shapes, label: str):
     while time.perf_counter() < t_end or len(times) < 2:
         seed = st.next_seed()
         t0 = time.perf_counter()
-        A.simulate_step([G], [E], gE, shapes, 0.2, 4, ef, seed)
+        if hook == "arc":
+            A.simulate_step([G], [E], gE, shapes, 0.2, 4, ef, seed)
+        else:
+            S.simulate_step([G], [E], gE, shapes, 0.2, ef, hook == "randk", seed)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
+    fn = "group_topk_hook" if hook == "arc" else f"sparse_hook_sync ({hook})"
     return {"value": round(4 * n / med / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "port",
-            "sample": f"{len(times)} oracle calls (torch-CPU restatement of group_topk_hook, "
+            "sample": f"{len(times)} oracle calls (torch-CPU restatement of {fn}, "
                       f"ws=1, {ef}) on one {label} bucket, median {med * 1e3:.1f} ms, "
                       f"{os.cpu_count()} host CPUs visible"}
 
@@ -130,8 +169,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ef", default="ef14", choices=["noef", "ef14", "ef21"])
-    ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS),
+    ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS) + ["resnet18_ddp"],
                     help="bucket shape set (headline = the BASELINE metric's bucket)")
+    ap.add_argument("--hook", default="arc", choices=["arc", "topk", "randk"],
+                    help="arc = ARC-TopK (the metric's codec); topk / randk = the reference's "
+                         "baselines (sparse_hook.py; RandK with the device index source)")
     ap.add_argument("--buckets", type=int, default=4,
                     help="buckets per step (a backward's worth, hooked in order as DDP does); "
                          "each is one workload bucket")
@@ -164,20 +206,35 @@ def main():
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    label, shapes = WORKLOADS[args.workload]
+    if args.workload == "resnet18_ddp":  # configs[1]'s model, as its DDP buckets
+        label = "resnet18_cifar_ddp_buckets_fp32_44.7MB"
+        layouts = ddp_buckets(resnet18_cifar_shapes())
+        shapes = layouts[0]
+    else:
+        label, shapes = WORKLOADS[args.workload]
+        layouts = [shapes] * args.buckets
+    nb = len(layouts)
+    bytes_per_step = sum(4 * bucket_numel(sh) for sh in layouts)
     n = bucket_numel(shapes)
-    bucket_bytes = 4 * n
-    nb = args.buckets
+    bucket_bytes = bytes_per_step // nb
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     # one step = one backward's worth of buckets, hooked in bucket order as DDP does
-    buckets = [SyntheticBucket(torch.randn(n, device=dev, generator=g), shapes, index=i,
-                               is_last=(i == nb - 1)) for i in range(nb)]
-    st = GroupTopKState(None, r=args.r, compress_ratio=args.ratio, start_compress_iter=0,
-                        use_error_feedback=args.ef, seed=1234)
-    st.host_staged = args.host_staged
+    buckets = [SyntheticBucket(torch.randn(bucket_numel(sh), device=dev, generator=g), sh, index=i,
+                               is_last=(i == nb - 1)) for i, sh in enumerate(layouts)]
+    if args.hook == "arc":
+        st = GroupTopKState(None, r=args.r, compress_ratio=args.ratio, start_compress_iter=0,
+                            use_error_feedback=args.ef, seed=1234)
+        st.host_staged = args.host_staged
+        hook = group_topk_hook
+    else:  # the reference's TopK / RandK baselines on the same buckets (sparse_hook.py)
+        from allreducetopk_amd.comm_hooks.sparse_hook import SparseState, sparse_hook_sync
+        st = SparseState(None, compress_ratio=args.ratio, start_compress_iter=0,
+                         sparse_type="tensor", random=(args.hook == "randk"),
+                         use_error_feedback=args.ef, random_seed=1234, index_source="hash")
+        hook = sparse_hook_sync
 
     def step():
-        futs = [group_topk_hook(st, bk) for bk in buckets]
+        futs = [hook(st, bk) for bk in buckets]
         for f in futs:  # DDP's finalize: the caller's stream waits for every bucket's future
             f.wait()
 
@@ -185,7 +242,7 @@ def main():
     for _ in range(max(args.warmup, 2 if args.ef == "ef21" else 1)):
         step()
     torch.cuda.synchronize()
-    if not args.no_phase_events:
+    if not args.no_phase_events and args.hook == "arc":
         st.phase_events = []
         st.phase_event_every = 8  # sample HIP events on every 8th timed hook call
 
@@ -202,7 +259,7 @@ def main():
     elapsed = float(t.item())
 
     phase_ms = {}
-    if st.phase_events:
+    if getattr(st, "phase_events", None):
         order = [p for p in ["start", "encode", "sketch_allreduce", "select", "pack", "d2h", "h2d",
                              "packed_allreduce", "decode"] if p in st.phase_events[0]]
         for a, b in zip(order[:-1], order[1:]):
@@ -211,9 +268,10 @@ def main():
         phase_ms["hook_device_total"] = statistics.mean(
             ev["start"].elapsed_time(ev["decode"]) for ev in st.phase_events)
 
-    value = world * args.steps * nb * bucket_bytes / elapsed / 1e9
+    value = world * args.steps * bytes_per_step / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
-    alg = algorithmic_bytes(args.ef, shapes, args.ratio, args.r)
+    per_bucket = [algorithmic_bytes(args.ef, sh, args.ratio, args.r) for sh in layouts]
+    alg = {k: sum(d[k] for d in per_bucket) / nb for k in per_bucket[0]}  # mean over the step's buckets
     roof = None
     if phase_ms:
         enc_s = phase_ms["encode"] / 1e3
@@ -234,7 +292,7 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (N(0,1) fp32 gradients, per-rank seed)",
-        "config": {"workload": f"arctopk_{args.ef}_{nb}x_{label}"
+        "config": {"workload": f"{'arctopk' if args.hook == 'arc' else args.hook}_{args.ef}_{nb}x_{label}"
                                + ("_host_staged" if args.host_staged else ""),
                    "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
                    "bucket_bytes": bucket_bytes, "buckets_per_step": nb,
@@ -250,7 +308,8 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, rank, shapes, label)
+        out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, rank, shapes, label,
+                                           args.hook)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.barrier()

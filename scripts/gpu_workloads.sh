@@ -1,15 +1,31 @@
 #!/bin/bash
-# bench.py on every workload (EF14) and on the headline bucket in all EF modes.
+# bench.py on every workload (EF14), the headline bucket in all EF modes, the TopK / RandK
+# baselines and the host-staged (NIC model) exchange.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/wl
 : > gpurun_out/wl/all.jsonl
-for spec in "headline ef14" "headline ef21" "headline noef" "llama_embed ef14" "roberta_embed ef14" \
-            "resnet18_conv ef14" "resnet50_mixed ef14" "llama_layer_mixed ef14" ${EXTRA_WL}; do
-  set -- $spec
-  timeout -k 10 240 python bench.py --workload $1 --ef $2 --steps 30 --warmup 5 --no-cpu-baseline \
-      > gpurun_out/wl/$1_$2.log 2>&1 || { echo "bench $1 $2 failed"; tail -20 gpurun_out/wl/$1_$2.log; exit 1; }
-  tail -1 gpurun_out/wl/$1_$2.log >> gpurun_out/wl/all.jsonl
-  echo "$1 $2 done"
-done
+i=0
+while read -r args; do
+  [ -z "$args" ] && continue
+  i=$((i+1))
+  timeout -k 10 240 python bench.py $args --steps 20 --warmup 3 --no-cpu-baseline \
+      > gpurun_out/wl/w$i.log 2>&1 || { echo "bench [$args] failed"; tail -20 gpurun_out/wl/w$i.log; exit 1; }
+  tail -1 gpurun_out/wl/w$i.log >> gpurun_out/wl/all.jsonl
+  echo "[$args] done"
+done <<LIST
+--workload headline --ef ef14
+--workload headline --ef ef21
+--workload headline --ef noef
+--workload headline --ef ef14 --host-staged
+--workload llama_embed --ef ef14
+--workload roberta_embed --ef ef14
+--workload resnet18_conv --ef ef14
+--workload resnet50_mixed --ef ef14
+--workload llama_layer_mixed --ef ef14
+--workload headline --ef ef14 --hook topk
+--workload headline --ef ef14 --hook randk
+${EXTRA_WL}
+LIST
+python scripts/wl_table.py gpurun_out/wl/all.jsonl

@@ -69,6 +69,35 @@ __global__ void __launch_bounds__(256) k_r2w1_chunk(const v4f* __restrict__ g, v
     }
 }
 
+// flat grid-stride: E := G + E and G := 0 (EF14 encode that also clears the bucket)
+template <int U>
+__global__ void __launch_bounds__(256) k_r2w2(v4f* __restrict__ g, v4f* __restrict__ e, size_t n4) {
+    const size_t stride = (size_t)gridDim.x * 256 * U;
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < n4; base += stride) {
+        v4f a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = min(base + (size_t)u * 256, n4 - 1);
+            a[u] = ld<true>(g + i);
+            b[u] = ld<true>(e + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * 256;
+            if (i < n4) {
+                st<true>(e + i, a[u] + b[u]);
+                st<true>(g + i, v4f{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+    }
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(256) k_zero(v4f* __restrict__ x, size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
+        st<NT>(x + i, v4f{0.f, 0.f, 0.f, 0.f});
+}
+
 __global__ void __launch_bounds__(256) k_fill(v4f* __restrict__ x, size_t n4, float v) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
         x[i] = v4f{v, v, v, v};
@@ -153,6 +182,13 @@ int main() {
             snprintf(nm, sizeof nm, "chunk R2W1 U4 %zu f4/blk nt both", per);
             timed(nm, pre, [&] { hipLaunchKernelGGL((k_r2w1_chunk<4, true, true>), dim3(grid), dim3(256), 0, 0, (const v4f*)G, (v4f*)E, n4, per); }, enc_bytes);
         }
+        for (int bpc : {4, 8}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "flat R2W2 (E=G+E, G=0) nt %d/CU", bpc);
+            timed(nm, pre, [&] { hipLaunchKernelGGL((k_r2w2<4>), dim3(256 * bpc), dim3(256), 0, 0, (v4f*)G, (v4f*)E, n4); }, 16.0 * N);
+        }
+        timed("zero G (decode-like) plain", pre, [&] { hipLaunchKernelGGL(k_zero<false>, dim3(2048), dim3(256), 0, 0, (v4f*)G, n4); }, 4.0 * N);
+        timed("zero G (decode-like) nt", pre, [&] { hipLaunchKernelGGL(k_zero<true>, dim3(2048), dim3(256), 0, 0, (v4f*)G, n4); }, 4.0 * N);
         timed("library k_encode EF14", pre, [&] { arctopk_encode(plan, G, E, ARCTOPK_EF14, 1, V, S, 0); }, enc_bytes);
         timed("library k_encode noef (read G)", pre, [&] { arctopk_encode(plan, G, E, ARCTOPK_EF_NONE, 0, V, S, 0); }, 4.0 * N);
         timed("library k_encode EF21 (read G, E)", pre, [&] { arctopk_encode(plan, G, E, ARCTOPK_EF21, 1, V, S, 0); }, 8.0 * N);
