@@ -353,6 +353,34 @@ def _check_bucket_layout(buf: torch.Tensor, grads) -> None:
         raise RuntimeError("bucket gradient views do not cover the buffer")
 
 
+def _stage_through_host(state: GroupTopKState, pv: torch.Tensor, stream, dev,
+                        chunks: int = 8) -> None:
+    """Move the packed payload device -> pinned host -> device as a NIC-staged exchange
+    would, in `chunks` pieces: D2H of piece i+1 runs while piece i goes back H2D (PCIe is
+    full duplex), so the pair costs about one direction plus one piece.  `stream` waits
+    for the last piece."""
+    n = pv.numel()
+    if state._host_buf is None or state._host_buf.numel() < n:
+        state._host_buf = torch.empty(n, dtype=pv.dtype, pin_memory=True)
+    hb = state._host_buf[:n]
+    d2h = state._side_stream(state._copy_streams, dev)
+    h2d = state._side_stream(state._decode_streams, dev)
+    d2h.wait_stream(stream)
+    h2d.wait_stream(stream)
+    step = max(1, -(-n // chunks))
+    for lo in range(0, n, step):
+        hi = min(n, lo + step)
+        with torch.cuda.stream(d2h):
+            hb[lo:hi].copy_(pv[lo:hi], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(d2h)
+        h2d.wait_event(ev)
+        with torch.cuda.stream(h2d):
+            pv[lo:hi].copy_(hb[lo:hi], non_blocking=True)
+    stream.wait_stream(h2d)
+    stream.wait_stream(d2h)
+
+
 def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                     ) -> torch.futures.Future[torch.Tensor]:
     state.maybe_accumulate_momentum_on_bucket(bucket)
@@ -491,14 +519,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         return fut
     plan.pack(input_tensor, err, ef, sid)
     mark("pack")
-    if state.host_staged:  # D2H to a pinned "NIC buffer" and back, stream-ordered
-        pv = plan.packed_view
-        if state._host_buf is None or state._host_buf.numel() < pv.numel():
-            state._host_buf = torch.empty(pv.numel(), dtype=pv.dtype, pin_memory=True)
-        hb = state._host_buf[:pv.numel()]
-        hb.copy_(pv, non_blocking=True)
-        mark("d2h")
-        pv.copy_(hb, non_blocking=True)
+    if state.host_staged:  # D2H to a pinned "NIC buffer" and back (NIC model)
+        _stage_through_host(state, plan.packed_view, stream, dev)
         mark("h2d")
     if world_size > 1:
         dist.all_reduce(plan.packed_view, group=group, async_op=False)

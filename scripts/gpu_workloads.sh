@@ -24,6 +24,7 @@ done <<LIST
 --workload resnet18_conv --ef ef14
 --workload resnet50_mixed --ef ef14
 --workload llama_layer_mixed --ef ef14
+--workload resnet18_ddp --ef ef14
 --workload headline --ef ef14 --hook topk
 --workload headline --ef ef14 --hook randk
 ${EXTRA_WL}
