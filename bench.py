@@ -1,12 +1,13 @@
 """Benchmark of the ARC-TopK comm-hook codec on MI355X (BASELINE.json metric).
 
-One "step" = one ``group_topk_hook`` call on one 256 MiB fp32 gradient bucket
-(16 x [2048, 2048], the Llama-1B projection shape):
-encode -> RCCL all_reduce(sketch) -> select -> pack -> RCCL all_reduce(packed)
--> decode, steady-state EF14 (configs[1]'s mode), compress_ratio 0.2, r 4,
-inputs resident in HBM.
+One "step" = one backward's worth of buckets hooked in order as DDP does (default:
+4 buckets of 256 MiB fp32, 16 x [2048, 2048] each, the Llama-1B projection shape;
+SURVEY.md section 8d): per bucket encode -> RCCL all_reduce(sketch) -> select -> pack
+-> RCCL all_reduce(packed) -> decode, steady-state EF14 (configs[1]'s mode),
+compress_ratio 0.2, r 4, inputs resident in HBM.  At world size > 1 a bucket's packed
+all-reduce and decode overlap the next bucket's encode.
 
-    python bench.py [--gpus N --steps K --warmup W --ef ef14|ef21|noef]
+    python bench.py [--gpus N --steps K --warmup W --ef ef14|ef21|noef --workload W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Prints ONE JSON line (rank 0).  ``value`` = bucket bytes processed by all ranks
