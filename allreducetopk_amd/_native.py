@@ -10,6 +10,8 @@ import os
 import threading
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
 
+import torch
+
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ARCTOPK_LIB", os.path.join(PKG, "lib", "libarctopk.so"))
 
@@ -17,6 +19,8 @@ EF_NONE, EF14, EF21 = 0, 1, 2
 EF_CODE = {"noef": EF_NONE, "ef14": EF14, "ef21": EF21}
 SEG_RAW, SEG_SKETCH = 0, 1
 F32 = 0
+BF16 = 1
+DTYPE_CODE = {torch.float32: F32, torch.bfloat16: BF16}  # bucket dtype -> ARCTOPK_F32 / _BF16
 
 STATUS = {1001: "invalid argument", 1002: "ND tensor numel not divisible by 2*t^2",
           1003: "unsupported dtype", 1004: "empty tensor"}
@@ -67,6 +71,7 @@ _SIGS = {
                                         POINTER(c_int64), c_int64, c_void_p, c_void_p, c_int32, c_int32,
                                         c_int32, c_void_p, c_void_p]),
     "arctopk_ef_apply": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
+    "arctopk_draw_bf16_normal": (c_int32, [c_uint64, c_int64, c_void_p]),
     "arctopk_version": (c_char_p, []),
 }
 

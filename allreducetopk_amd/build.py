@@ -17,7 +17,7 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libarctopk.so")
-SOURCES = ["plan.hip", "arctopk_kernels.hip", "sparse_kernels.hip", "mselect.hip"]
+SOURCES = ["plan.hip", "arctopk_kernels.hip", "sparse_kernels.hip", "mselect.hip", "projection.cpp"]
 ARCH = "gfx950"
 
 

@@ -59,8 +59,8 @@ class BucketPlan:
     """Native plan + persistent device buffers of one bucket layout."""
 
     def __init__(self, shapes: List[Tuple[int, ...]], r: int, ratio: float, dtype, device):
-        if dtype != torch.float32:
-            raise TypeError(f"ARC-TopK HIP codec supports float32 buckets, got {dtype}")
+        if dtype not in N.DTYPE_CODE:
+            raise TypeError(f"ARC-TopK HIP codec supports float32 and bfloat16 buckets, got {dtype}")
         L = N.lib()
         dims: List[int] = []
         nd: List[int] = []
@@ -73,7 +73,7 @@ class BucketPlan:
         self.device = torch.device(device)
         handle = N.c_void_p()
         st = L.arctopk_plan_create((N.c_int64 * max(1, len(dims)))(*dims), (N.c_int32 * len(nd))(*nd),
-                                   len(nd), r, float(ratio), N.F32, self.device.index or 0,
+                                   len(nd), r, float(ratio), N.DTYPE_CODE[dtype], self.device.index or 0,
                                    N.ctypes.byref(handle))
         N.check(st, f"arctopk_plan_create(shapes={shapes}, r={r}, ratio={ratio})")
         self.handle = handle
@@ -87,15 +87,18 @@ class BucketPlan:
             self.segments.append(seg)
         self.ms = tuple(int(s.m) for s in self.segments if s.kind == N.SEG_SKETCH)
         dev = self.device
-        self.sketch = torch.empty(max(1, info.sketch_len), dtype=torch.float32, device=dev)
+        # sketch, packed values and projections live in the bucket dtype, as in the reference
+        # (group_topk_hook_no_reshape.py:49, :53, :263)
+        self.dtype = dtype
+        self.sketch = torch.empty(max(1, info.sketch_len), dtype=dtype, device=dev)
         # zero-filled: the <= 3 alignment pad floats between segments ride the
         # all-reduce as zeros and are never decoded
-        self.packed = torch.zeros(max(1, info.packed_len), dtype=torch.float32, device=dev)
+        self.packed = torch.zeros(max(1, info.packed_len), dtype=dtype, device=dev)
         self.rowlist = torch.empty(max(1, info.sel_rows), dtype=torch.int32, device=dev)
         self.slotmap = torch.empty(max(1, info.rows_total), dtype=torch.int32, device=dev)
         # projections: a ring of device slots filled by H2D copies on a side stream, so the
         # copy for call i+1 overlaps call i's kernels instead of sitting between them
-        self.V_ring = [torch.empty(max(1, info.v_len), dtype=torch.float32, device=dev)
+        self.V_ring = [torch.empty(max(1, info.v_len), dtype=dtype, device=dev)
                        for _ in range(self.V_RING)]
         self._v_used = [None] * self.V_RING  # event after the encode that last read the slot
         self._v_streams = [None] * self.V_RING

@@ -25,6 +25,27 @@ from typing import Dict, Optional, Sequence, Tuple
 import torch
 
 
+# ---- bf16 projections -----------------------------------------------------------------
+# torch's CPU normal_ on a bf16 tensor (the reference's torch.randn(m, r, dtype=bfloat16))
+# runs a scalar BFloat16 loop, ~8x slower than the fp32 path and slower than the device
+# codec.  For every tensor with m*r a multiple of 16 the values are a table function of
+# 8-bit mt19937 uniforms; libarctopk's host routine arctopk_draw_bf16_normal computes them
+# bit-identically (projection.cpp; tests/test_host_logic.py pins it against torch) and,
+# called through ctypes, without holding the GIL.
+
+
+def bf16_fast_ok(ms: Sequence[int], r: int) -> bool:
+    """Every tensor's draw is whole 16-blocks (no tail recompute, no scalar path)."""
+    return all(int(m) * r >= 16 and (int(m) * r) % 16 == 0 for m in ms)
+
+
+def draw_bf16_into(seed: int, out: torch.Tensor) -> None:
+    """Fill the contiguous bf16 CPU tensor `out` (numel % 16 == 0) with the stream."""
+    from allreducetopk_amd import _native as N
+    N.check(N.lib().arctopk_draw_bf16_normal(int(seed), out.numel(), out.data_ptr()),
+            "arctopk_draw_bf16_normal")
+
+
 def _fill_plan(host: torch.Tensor, ms: Sequence[int], r: int, dtype: torch.dtype):
     """Views of `host` that one generator pass fills in the reference's stream order.
 
@@ -59,6 +80,9 @@ def draw_host(seed: int, ms: Sequence[int], r: int, dtype: torch.dtype, pin: boo
     """Concatenated [m_i][r] projections for one call, on the host (pinned if asked)."""
     total = sum(int(m) * r for m in ms)
     host = torch.empty(max(total, 1), dtype=dtype, pin_memory=pin)
+    if dtype == torch.bfloat16 and total and bf16_fast_ok(ms, r):
+        draw_bf16_into(seed, host[:total])
+        return host
     g = torch.Generator().manual_seed(int(seed))
     for v in _fill_plan(host, ms, r, dtype):
         v.normal_(generator=g)
@@ -68,19 +92,24 @@ def draw_host(seed: int, ms: Sequence[int], r: int, dtype: torch.dtype, pin: boo
 class Slot:
     """A reusable pinned host buffer for one column list, with its fill views."""
 
-    __slots__ = ("key", "host", "views", "event")
+    __slots__ = ("key", "host", "views", "event", "fast")
 
     def __init__(self, key, ms, r, dtype, pin):
         self.key = key
         total = sum(int(m) * r for m in ms)
         self.host = torch.empty(max(total, 1), dtype=dtype, pin_memory=pin)
         self.views = _fill_plan(self.host, ms, r, dtype)
+        # bf16: the native table-driven draw (bit-identical to torch's normal_)
+        self.fast = self.host[:total] if dtype == torch.bfloat16 and total and bf16_fast_ok(ms, r) else None
         self.event = None  # set when an async copy out of `host` was enqueued
 
     def fill(self, seed: int):
         if self.event is not None:  # the previous H2D copy from this buffer must be done
             self.event.synchronize()
             self.event = None
+        if self.fast is not None:
+            draw_bf16_into(seed, self.fast)
+            return self
         g = torch.Generator().manual_seed(int(seed))
         for v in self.views:
             v.normal_(generator=g)

@@ -51,14 +51,28 @@ __device__ __forceinline__ float4 ef_apply4(const float4* __restrict__ g4, float
     return x;
 }
 
-template <int EF, bool ERR_IN>
-__device__ __forceinline__ float ef_apply1(const float* __restrict__ g, const float* __restrict__ e,
+// X = G (+|-) E of one element, rounded to T as the reference's in-place add_ on a T bucket
+template <typename T, int EF, bool ERR_IN>
+__device__ __forceinline__ float ef_apply1(const T* __restrict__ g, const T* __restrict__ e,
                                            int64_t i) {
-    float x = __builtin_nontemporal_load(g + i);
+    float x = ld1<T, true>(g + i);
     if constexpr (EF == ARCTOPK_EF14) {
-        if constexpr (ERR_IN) x += __builtin_nontemporal_load(e + i);
+        if constexpr (ERR_IN) x = rnd<T>(x + ld1<T, true>(e + i));
     } else if constexpr (EF == ARCTOPK_EF21) {
-        x -= __builtin_nontemporal_load(e + i);
+        x = rnd<T>(x - ld1<T, true>(e + i));
+    }
+    return x;
+}
+
+// the same on a quad (x = g (+|-) e, rounded to T)
+template <typename T, int EF, bool ERR_IN>
+__device__ __forceinline__ float4 ef_combine4(float4 x, float4 e) {
+    if constexpr (EF == ARCTOPK_EF14 && ERR_IN) {
+        x.x += e.x; x.y += e.y; x.z += e.z; x.w += e.w;
+        return rnd4<T>(x);
+    } else if constexpr (EF == ARCTOPK_EF21) {
+        x.x -= e.x; x.y -= e.y; x.z -= e.z; x.w -= e.w;
+        return rnd4<T>(x);
     }
     return x;
 }
@@ -73,12 +87,12 @@ __device__ __forceinline__ float ef_apply1(const float* __restrict__ g, const fl
 //  ENC_TILE       : m < 64 (ND convs, m = 2*t^2): the tile's rows are loaded coalesced
 //                   into LDS, then one thread per row forms its R dot products.
 //  ENC_RAW        : 1-D tensors: the sketch is the (EF-applied) values themselves.
-template <int R, int EF, bool ERR_IN, bool VLDS>
+template <typename T, int R, int EF, bool ERR_IN>
 __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                                                 const EncTile* __restrict__ tiles,
-                                                const float* __restrict__ G, float* __restrict__ E,
-                                                const float* __restrict__ V,
-                                                float* __restrict__ sketch,
+                                                const T* __restrict__ G, T* __restrict__ E,
+                                                const T* __restrict__ V,
+                                                T* __restrict__ sketch,
                                                 float* __restrict__ part_buf) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const EncTile t = tiles[blockIdx.x];
@@ -90,23 +104,23 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 
     if (t.mode == ENC_RAW) {
         const int64_t base = s.offset + t.row0;
-        float* out = sketch + s.sketch_off + t.row0;
+        T* out = sketch + s.sketch_off + t.row0;
         for (int64_t i = tid; i < t.nrows; i += 256) {
-            const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, i);
-            if constexpr (WRITE_E) __builtin_nontemporal_store(x, E + base + i);
-            out[i] = x;
+            const float x = ef_apply1<T, EF, ERR_IN>(G + base, E + base, i);
+            if constexpr (WRITE_E) st1<T, true>(E + base + i, x);
+            st1<T>(out + i, x);
         }
         return;
     }
 
     const int m = (int)s.m;
-    const float* __restrict__ Vs = V + s.v_off;  // [m][R]
+    const T* __restrict__ Vs = V + s.v_off;  // [m][R]
 
     if (t.mode == ENC_TILE) {
         // LDS: tile [nrows*m] then V [m][R]
         float* tile = lds;
         float* vl = lds + kTileRows * m;
-        for (int i = tid; i < m * R; i += 256) vl[i] = Vs[i];
+        for (int i = tid; i < m * R; i += 256) vl[i] = to_f(Vs[i]);
         const int64_t base = s.offset + t.row0 * m;
         const int cnt = (int)t.nrows * m;
         int done = 0;
@@ -116,28 +130,23 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
             constexpr int Q = 4;
             constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
             const int cnt4 = cnt >> 2;
-            const float4* g4 = reinterpret_cast<const float4*>(G + base);
-            float4* e4 = reinterpret_cast<float4*>(E + base);
+            const T* gp = G + base;
+            T* ep = E + base;
             float4* t4 = reinterpret_cast<float4*>(tile);
             for (int q0 = tid; q0 < cnt4; q0 += 256 * Q) {
                 float4 gv[Q], ev[Q];
 #pragma unroll
                 for (int u = 0; u < Q; ++u) {
                     const int q = min(q0 + u * 256, cnt4 - 1);
-                    gv[u] = ld_stream(g4 + q);
-                    if constexpr (LOAD_E) ev[u] = ld_stream(e4 + q);
+                    gv[u] = ldq<T, true>(gp, q);
+                    if constexpr (LOAD_E) ev[u] = ldq<T, true>(ep, q);
                 }
 #pragma unroll
                 for (int u = 0; u < Q; ++u) {
                     const int q = q0 + u * 256;
                     if (q < cnt4) {
-                        float4 x = gv[u];
-                        if constexpr (EF == ARCTOPK_EF14 && ERR_IN) {
-                            x.x += ev[u].x; x.y += ev[u].y; x.z += ev[u].z; x.w += ev[u].w;
-                        } else if constexpr (EF == ARCTOPK_EF21) {
-                            x.x -= ev[u].x; x.y -= ev[u].y; x.z -= ev[u].z; x.w -= ev[u].w;
-                        }
-                        if constexpr (WRITE_E) st_stream(e4 + q, x);
+                        const float4 x = ef_combine4<T, EF, ERR_IN>(gv[u], ev[u]);
+                        if constexpr (WRITE_E) stq<T, true>(ep, q, x);
                         t4[q] = x;
                     }
                 }
@@ -145,8 +154,8 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
             done = cnt4 << 2;
         }
         for (int i = done + tid; i < cnt; i += 256) {
-            const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, i);
-            if constexpr (WRITE_E) __builtin_nontemporal_store(x, E + base + i);
+            const float x = ef_apply1<T, EF, ERR_IN>(G + base, E + base, i);
+            if constexpr (WRITE_E) st1<T, true>(E + base + i, x);
             tile[i] = x;
         }
         __syncthreads();
@@ -160,9 +169,9 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = fmaf(x, vl[c * R + j], acc[j]);
             }
-            float* out = sketch + s.sketch_off + (t.row0 + tid) * R;
+            T* out = sketch + s.sketch_off + (t.row0 + tid) * R;
 #pragma unroll
-            for (int j = 0; j < R; ++j) out[j] = acc[j];
+            for (int j = 0; j < R; ++j) st1<T>(out + j, acc[j]);
         }
         return;
     }
@@ -172,11 +181,10 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     // of one j).  Column-split tensors write per-part partial sketches, summed in fixed
     // part order by k_sketch_combine.
     const int c0 = t.c0, cl = t.clen;
-    if constexpr (VLDS) {
+    {
         if constexpr (R == 4) {
-            const float4* v4 = reinterpret_cast<const float4*>(Vs) + c0;
             for (int c = tid; c < cl; c += 256) {
-                const float4 v = v4[c];
+                const float4 v = ldq<T, false>(Vs, c0 + c);  // V[c0 + c][0..3]
                 lds[c] = v.x;
                 lds[cl + c] = v.y;
                 lds[2 * cl + c] = v.z;
@@ -185,81 +193,72 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         } else {
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                for (int c = tid; c < cl; c += 256) lds[j * cl + c] = Vs[(int64_t)(c0 + c) * R + j];
+                for (int c = tid; c < cl; c += 256) lds[j * cl + c] = to_f(Vs[(int64_t)(c0 + c) * R + j]);
         }
         __syncthreads();
     }
-    float* const out_base = t.part < 0 ? sketch + s.sketch_off
-                                       : part_buf + s.part_off + (int64_t)t.part * s.n * R;
+    // the row's R sums: rounded to T into the sketch, or fp32 partials of a column part
+    T* const sk_out = sketch + s.sketch_off;
+    float* const pt_out = t.part < 0 ? nullptr : part_buf + s.part_off + (int64_t)t.part * s.n * R;
+    auto put = [&](int64_t i, float v) {
+        if (pt_out) pt_out[i] = v;
+        else st1<T>(sk_out + i, v);
+    };
     const int64_t rs = t.rstride;
     if (t.mode == ENC_ROW_VEC) {
-        // Software-pipelined stream: a wave walks its rows in steps of 64*U float4
-        // (U per lane) with two register buffers: the loads of the next step are in
-        // flight while the current step forms its dot products, stores E and (at a
-        // row end) reduces.  V is read from LDS (VLDS) or L2, chosen at compile time so
-        // the compiler never orders an LDS read behind the prefetched global loads.
-        constexpr int U = 4;
+        // Software-pipelined stream: a wave walks its rows in steps of 64*U 16-B units
+        // (U per lane; a unit is 4 fp32 or 8 bf16 elements) with two register buffers: the
+        // loads of the next step are in flight while the current step forms its dot
+        // products, stores E and (at a row end) reduces.  V^T comes from LDS.
+        constexpr int PQ = kQuadsPer16<T>;  // quads per 16-B unit
+        constexpr int U = 4 / PQ;
         constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
-        const int m4 = cl >> 2;  // float4 columns of this tile
-        const int steps = (m4 + 64 * U - 1) / (64 * U);
+        const int m4 = cl >> 2;   // quads of this tile row
+        const int mu = m4 / PQ;   // 16-B units (the plan makes m4 a multiple of PQ)
+        const int steps = (mu + 64 * U - 1) / (64 * U);
         const float4* vt4 = reinterpret_cast<const float4*>(lds);
-        float4 ga[U], ea[U], gb[U], eb[U];
+        float4 ga[U][PQ], ea[U][PQ], gb[U][PQ], eb[U][PQ];
         float acc[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) acc[j] = 0.f;
 
-        auto issue = [&](float4 (&gx)[U], float4 (&ex)[U], int64_t r_, int st_) {
-            const float4* g4 = reinterpret_cast<const float4*>(G + s.offset + r_ * m + c0);
-            const float4* e4 = reinterpret_cast<const float4*>(E + s.offset + r_ * m + c0);
+        auto issue = [&](float4 (&gx)[U][PQ], float4 (&ex)[U][PQ], int64_t r_, int st_) {
+            const T* gp = G + s.offset + r_ * m + c0;
+            const T* ep = E + s.offset + r_ * m + c0;
 #pragma unroll
             for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: no exec-masked blocks
-                const int c = min(st_ * 64 * U + u * 64 + lane, m4 - 1);
-                gx[u] = ld_stream(g4 + c);
-                if constexpr (LOAD_E) ex[u] = ld_stream(e4 + c);
+                const int c = min(st_ * 64 * U + u * 64 + lane, mu - 1);
+                ld16<T, true>(gp, c, gx[u]);
+                if constexpr (LOAD_E) ld16<T, true>(ep, c, ex[u]);
             }
         };
-        auto consume = [&](float4 (&gx)[U], float4 (&ex)[U], int64_t r_, int st_) {
-            float4* e4 = reinterpret_cast<float4*>(E + s.offset + r_ * m + c0);
+        auto consume = [&](float4 (&gx)[U][PQ], float4 (&ex)[U][PQ], int64_t r_, int st_) {
+            T* ep = E + s.offset + r_ * m + c0;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int cu = st_ * 64 * U + u * 64 + lane;
-                const bool ok = cu < m4;  // lanes past the row end loaded a clamped copy
-                const int c = ok ? cu : m4 - 1;
-                float4 x = gx[u];
-                if constexpr (EF == ARCTOPK_EF14 && ERR_IN) {
-                    x.x += ex[u].x; x.y += ex[u].y; x.z += ex[u].z; x.w += ex[u].w;
-                } else if constexpr (EF == ARCTOPK_EF21) {
-                    x.x -= ex[u].x; x.y -= ex[u].y; x.z -= ex[u].z; x.w -= ex[u].w;
-                }
-                if constexpr (WRITE_E) {
-                    if (ok) st_stream(e4 + c, x);
-                }
-                if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
-                float4 vq[4];  // !VLDS, R = 4: the 4 columns' V rows, 16-B loads from L2
-                if constexpr (!VLDS && R == 4) {
-                    const float4* vr = reinterpret_cast<const float4*>(Vs) + c0 + 4 * c;
+                const bool ok = cu < mu;  // lanes past the row end loaded a clamped copy
+                const int c = ok ? cu : mu - 1;
+                float4 x[PQ];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) vq[q] = vr[q];
+                for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(gx[u][h], ex[u][h]);
+                if constexpr (WRITE_E) {
+                    if (ok) st16<T, true>(ep, c, x);
                 }
+#pragma unroll
+                for (int h = 0; h < PQ; ++h)
+                    if (!ok) x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    float4 v;
-                    if constexpr (VLDS) {
-                        v = vt4[j * m4 + c];
-                    } else if constexpr (R == 4) {
-                        v = make_float4(vq[0].x, vq[1].x, vq[2].x, vq[3].x);
-                        if (j == 1) v = make_float4(vq[0].y, vq[1].y, vq[2].y, vq[3].y);
-                        if (j == 2) v = make_float4(vq[0].z, vq[1].z, vq[2].z, vq[3].z);
-                        if (j == 3) v = make_float4(vq[0].w, vq[1].w, vq[2].w, vq[3].w);
-                    } else {
-                        const float* vp = Vs + (int64_t)(c0 + 4 * c) * R + j;
-                        v = make_float4(vp[0], vp[R], vp[2 * R], vp[3 * R]);
-                    }
                     float a = acc[j];
-                    a = fmaf(x.x, v.x, a);
-                    a = fmaf(x.y, v.y, a);
-                    a = fmaf(x.z, v.z, a);
-                    a = fmaf(x.w, v.w, a);
+#pragma unroll
+                    for (int h = 0; h < PQ; ++h) {
+                        const float4 v = vt4[j * m4 + c * PQ + h];
+                        a = fmaf(x[h].x, v.x, a);
+                        a = fmaf(x[h].y, v.y, a);
+                        a = fmaf(x[h].z, v.z, a);
+                        a = fmaf(x[h].w, v.w, a);
+                    }
                     acc[j] = a;
                 }
             }
@@ -271,7 +270,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                     for (int j = 1; j < R; ++j)
                         if (lane == j) v = acc[j];
-                    out_base[r_ * R + lane] = v;
+                    put(r_ * R + lane, v);
                 }
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = 0.f;
@@ -303,15 +302,10 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[j] = 0.f;
             for (int c = lane; c < cl; c += 64) {
-                const float x = ef_apply1<EF, ERR_IN>(G + base, E + base, c);
-                if constexpr (WRITE_E) __builtin_nontemporal_store(x, E + base + c);
+                const float x = ef_apply1<T, EF, ERR_IN>(G + base, E + base, c);
+                if constexpr (WRITE_E) st1<T, true>(E + base + c, x);
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    float v;
-                    if constexpr (VLDS) v = lds[j * cl + c];
-                    else v = Vs[(int64_t)(c0 + c) * R + j];
-                    acc[j] = fmaf(x, v, acc[j]);
-                }
+                for (int j = 0; j < R; ++j) acc[j] = fmaf(x, lds[j * cl + c], acc[j]);
             }
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
@@ -320,7 +314,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int j = 1; j < R; ++j)
                     if (lane == j) v = acc[j];
-                out_base[row * R + lane] = v;
+                put(row * R + lane, v);
             }
         }
     }
@@ -345,21 +339,33 @@ struct Scale {
 
 // Energy of a row exactly as the reference forms it on the all-reduced sketch:
 // p_j = P_j / ws (IEEE division, ref `P /= ws`), q_j = p_j * p_j (`P ** 2`), then
-// ((q_0 + q_1) + q_2) + q_3 (torch.sum over dim 1, sequential for r <= 4).
+// ((q_0 + q_1) + q_2) + q_3 (torch.sum over dim 1: sequential for fp32 r <= 4; for bf16
+// an fp32 accumulation rounded once), each tensor op's result rounded to T.
 // __fmul_rn/__fadd_rn keep the compiler from contracting into FMAs.
-__device__ __forceinline__ float row_energy(const float* __restrict__ p, int R, const Scale& sc,
+template <typename T>
+__device__ __forceinline__ float energy4(float a, float b, float c, float d, const Scale& sc) {
+    a = rnd<T>(sc(a)); b = rnd<T>(sc(b)); c = rnd<T>(sc(c)); d = rnd<T>(sc(d));
+    float e = rnd<T>(__fmul_rn(a, a));
+    e = __fadd_rn(e, rnd<T>(__fmul_rn(b, b)));
+    e = __fadd_rn(e, rnd<T>(__fmul_rn(c, c)));
+    e = __fadd_rn(e, rnd<T>(__fmul_rn(d, d)));
+    return rnd<T>(e);
+}
+
+template <typename T>
+__device__ __forceinline__ float row_energy(const T* __restrict__ p, int R, const Scale& sc,
                                            int kind) {
     if (kind == ARCTOPK_SEG_RAW) {
-        const float v = sc(p[0]);
-        return __fmul_rn(v, v);
+        const float v = rnd<T>(sc(to_f(p[0])));
+        return rnd<T>(__fmul_rn(v, v));
     }
-    float a = sc(p[0]);
-    float s = __fmul_rn(a, a);
+    float a = rnd<T>(sc(to_f(p[0])));
+    float s = rnd<T>(__fmul_rn(a, a));
     for (int j = 1; j < R; ++j) {
-        const float b = sc(p[j]);
-        s = __fadd_rn(s, __fmul_rn(b, b));
+        const float b = rnd<T>(sc(to_f(p[j])));
+        s = __fadd_rn(s, rnd<T>(__fmul_rn(b, b)));
     }
-    return s;
+    return rnd<T>(s);
 }
 
 // Order key: energies are >= +0 or NaN; as uint32 the non-negative floats are
@@ -370,8 +376,9 @@ __device__ __forceinline__ uint32_t energy_key(float e) {
     return u & 0x7FFFFFFFu ? u : 0u;  // -0 cannot occur; keep +0 = 0
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) k_energy(const SegDev* __restrict__ segs, int nseg,
-                                                const float* __restrict__ sketch, int R, Scale sc,
+                                                const T* __restrict__ sketch, int R, Scale sc,
                                                 uint32_t* __restrict__ keys, float* __restrict__ energy) {
     const int si = blockIdx.y;
     const SegDev s = segs[si];
@@ -424,9 +431,10 @@ __device__ __forceinline__ int64_t block_exscan_s(int64_t v, int64_t* wsum) {
     return before;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__ segs,
                                                       const int32_t* __restrict__ seg_ids,
-                                                      const float* __restrict__ sketch, int R,
+                                                      const T* __restrict__ sketch, int R,
                                                       Scale sc, int32_t* __restrict__ rowlist,
                                                       int32_t* __restrict__ slotmap) {
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
@@ -435,26 +443,20 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
     const int n = (int)s.n;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
-    const float* sk = sketch + s.sketch_off;
+    const T* sk = sketch + s.sketch_off;
     SEL_STAMP(0);
     uint32_t kor = 0u, kand = ~0u;
     if (R == 4 && s.kind == ARCTOPK_SEG_SKETCH && (s.sketch_off & 3) == 0) {
-        // one float4 per row; 8 rows' loads in flight per thread before any use
-        const float4* p4 = reinterpret_cast<const float4*>(sk);
+        // one quad per row; 8 rows' loads in flight per thread before any use
         constexpr int B = 8;
         for (int base = 0; base < n; base += kST * B) {
             float4 v[B];
 #pragma unroll
-            for (int u = 0; u < B; ++u) v[u] = p4[min(base + u * kST + tid, n - 1)];
+            for (int u = 0; u < B; ++u) v[u] = ldq<T, false>(sk, min(base + u * kST + tid, n - 1));
 #pragma unroll
             for (int u = 0; u < B; ++u) {
                 const int row = base + u * kST + tid;
-                const float a = sc(v[u].x), b = sc(v[u].y), c = sc(v[u].z), d = sc(v[u].w);
-                float e = __fmul_rn(a, a);
-                e = __fadd_rn(e, __fmul_rn(b, b));
-                e = __fadd_rn(e, __fmul_rn(c, c));
-                e = __fadd_rn(e, __fmul_rn(d, d));
-                const uint32_t key = energy_key(e);
+                const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
                 if (row < n) {
                     keys[row] = key;
                     kor |= key;
@@ -584,13 +586,13 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
             break;
         }
     }
-    uint32_t T;
+    uint32_t thr;
     int64_t need_eq;
     if (ranked) {
-        T = sh.T;
+        thr = sh.T;
         need_eq = sh.need_eq;
     } else {  // every bit fixed: the threshold is the prefix itself
-        T = prefix;
+        thr = prefix;
         need_eq = kk;
     }
     SEL_STAMP(2);
@@ -605,8 +607,8 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (i + u < r1) {
-                gt += kv[u] > T;
-                eq += kv[u] == T;
+                gt += kv[u] > thr;
+                eq += kv[u] == thr;
             }
         }
     }
@@ -625,8 +627,8 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
         for (int u = 0; u < 4; ++u) {
             if (i + u < r1) {
                 const uint32_t key = kv[u];
-                bool sel = key > T;
-                if (key == T) {
+                bool sel = key > thr;
+                if (key == thr) {
                     sel = eq_seen < take_eq;
                     ++eq_seen;
                 }
@@ -645,9 +647,10 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
 
 // Larger segments: energy keys into global memory plus each segment's key OR / AND
 // (its common leading bits seed the multi-block radix select of mselect.hip).
+template <typename T>
 __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ segs,
                                                   const int32_t* __restrict__ ids, int first,
-                                                  const float* __restrict__ sketch, int R, Scale sc,
+                                                  const T* __restrict__ sketch, int R, Scale sc,
                                                   uint32_t* __restrict__ keys, MWorkspace* ws) {
     const int t = blockIdx.y;
     const SegDev s = segs[ids[first + t]];
@@ -655,20 +658,17 @@ __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ seg
     uint32_t kor = 0u, kand = ~0u;
     const int64_t gs = (int64_t)gridDim.x * 256;
     int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const float* sk = sketch + s.sketch_off;
+    const T* sk = sketch + s.sketch_off;
     if (stride == 4) {  // r = 4: four rows' sketch loads in flight per lane
         for (; row + 3 * gs < s.n; row += 4 * gs) {
             float v[4][4];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[u][j] = sk[(row + u * gs) * 4 + j];
+                for (int j = 0; j < 4; ++j) v[u][j] = to_f(sk[(row + u * gs) * 4 + j]);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const float a = sc(v[u][0]), b = sc(v[u][1]), c = sc(v[u][2]), d = sc(v[u][3]);
-                const float e = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(a, a), __fmul_rn(b, b)),
-                                                    __fmul_rn(c, c)), __fmul_rn(d, d));
-                const uint32_t key = energy_key(e);
+                const uint32_t key = energy_key(energy4<T>(v[u][0], v[u][1], v[u][2], v[u][3], sc));
                 keys[s.row_off + row + u * gs] = key;
                 kor |= key;
                 kand &= key;
@@ -728,69 +728,73 @@ __device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m 
 // ---------------------------------------------------------------------------
 // K3 pack
 // ---------------------------------------------------------------------------
-template <int EF>
-__device__ __forceinline__ float4 pack4(const float* __restrict__ G, float* __restrict__ E,
-                                        int64_t src) {
+// EF21 on a quad: D = G - E (rounded to T, the bucket after add_(E, -1)), E_new = E + D
+template <typename T>
+__device__ __forceinline__ float4 ef21_d(float4 g, float4 e) {
+    return rnd4<T>(make_float4(g.x - e.x, g.y - e.y, g.z - e.z, g.w - e.w));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <typename T, int EF>
+__device__ __forceinline__ float4 pack4(const T* __restrict__ G, T* __restrict__ E, int64_t src) {
     float4 v;
     if constexpr (EF == ARCTOPK_EF_NONE) {
-        v = *reinterpret_cast<const float4*>(G + src);
+        v = ldq<T, false>(G + src, 0);
     } else if constexpr (EF == ARCTOPK_EF14) {
-        v = *reinterpret_cast<const float4*>(E + src);
-        *reinterpret_cast<float4*>(E + src) = make_float4(0.f, 0.f, 0.f, 0.f);
+        v = ldq<T, false>(E + src, 0);
+        stq<T, false>(E + src, 0, make_float4(0.f, 0.f, 0.f, 0.f));
     } else {
-        const float4 g = *reinterpret_cast<const float4*>(G + src);
-        float4 ev = *reinterpret_cast<const float4*>(E + src);
-        v = make_float4(g.x - ev.x, g.y - ev.y, g.z - ev.z, g.w - ev.w);
-        ev.x += v.x; ev.y += v.y; ev.z += v.z; ev.w += v.w;
-        *reinterpret_cast<float4*>(E + src) = ev;
+        const float4 ev = ldq<T, false>(E + src, 0);
+        v = ef21_d<T>(ldq<T, false>(G + src, 0), ev);
+        stq<T, false>(E + src, 0, add4(ev, v));
     }
     return v;
 }
 
-template <int EF>
+template <typename T, int EF>
 __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                                               const Chunk* __restrict__ chunks,
-                                              const float* __restrict__ G, float* __restrict__ E,
+                                              const T* __restrict__ G, T* __restrict__ E,
                                               const int32_t* __restrict__ rowlist,
-                                              float* __restrict__ packed) {
+                                              T* __restrict__ packed) {
     const Chunk ch = chunks[blockIdx.x];
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
     const int32_t* rl = rowlist + s.sel_off + ch.row0;
-    float* dst = packed + s.packed_off + ch.row0 * m;
+    T* dst = packed + s.packed_off + ch.row0 * m;
     if (row_path(s)) {  // wave per selected row: all of a row's loads first, then stores
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const int m4 = m >> 2;
         constexpr int U = 8;
         for (int64_t j = wave; j < ch.nrows; j += 4) {
             const int64_t src_row = s.offset + (int64_t)rl[j] * m;
-            const float4* g4 = reinterpret_cast<const float4*>(G + src_row);
-            float4* e4 = reinterpret_cast<float4*>(E + src_row);
-            float4* d4 = reinterpret_cast<float4*>(dst + j * m);
+            const T* gp = G + src_row;
+            T* ep = E + src_row;
+            T* dp = dst + j * m;
             for (int c0 = 0; c0 < m4; c0 += 64 * U) {
                 float4 a[U], b[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int c = min(c0 + u * 64 + lane, m4 - 1);
-                    if constexpr (EF == ARCTOPK_EF_NONE) a[u] = ld4<kNtPack>(g4 + c);
-                    else if constexpr (EF == ARCTOPK_EF14) a[u] = ld4<kNtPack>(e4 + c);
-                    else { a[u] = ld4<kNtPack>(g4 + c); b[u] = ld4<kNtPack>(e4 + c); }
+                    if constexpr (EF == ARCTOPK_EF_NONE) a[u] = ldq<T, kNtPack>(gp, c);
+                    else if constexpr (EF == ARCTOPK_EF14) a[u] = ldq<T, kNtPack>(ep, c);
+                    else { a[u] = ldq<T, kNtPack>(gp, c); b[u] = ldq<T, kNtPack>(ep, c); }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int c = c0 + u * 64 + lane;
                     if (c < m4) {
                         if constexpr (EF == ARCTOPK_EF_NONE) {
-                            d4[c] = a[u];
+                            stq<T, false>(dp, c, a[u]);
                         } else if constexpr (EF == ARCTOPK_EF14) {
-                            d4[c] = a[u];
-                            st4<kNtPack>(e4 + c, make_float4(0.f, 0.f, 0.f, 0.f));
+                            stq<T, false>(dp, c, a[u]);
+                            stq<T, kNtPack>(ep, c, make_float4(0.f, 0.f, 0.f, 0.f));
                         } else {
-                            const float4 dv = make_float4(a[u].x - b[u].x, a[u].y - b[u].y,
-                                                          a[u].z - b[u].z, a[u].w - b[u].w);
-                            d4[c] = dv;
-                            st4<kNtPack>(e4 + c, make_float4(b[u].x + dv.x, b[u].y + dv.y,
-                                                             b[u].z + dv.z, b[u].w + dv.w));
+                            const float4 dv = ef21_d<T>(a[u], b[u]);
+                            stq<T, false>(dp, c, dv);
+                            stq<T, kNtPack>(ep, c, add4(b[u], dv));
                         }
                     }
                 }
@@ -811,18 +815,18 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
             const int64_t src = s.offset + (int64_t)rs[r] * m + (e - r * (uint32_t)m);
             float v;
             if constexpr (EF == ARCTOPK_EF_NONE) {
-                v = G[src];
+                v = ld1<T>(G + src);
             } else if constexpr (EF == ARCTOPK_EF14) {
-                v = E[src];
-                E[src] = 0.f;
+                v = ld1<T>(E + src);
+                st1<T>(E + src, 0.f);
             } else {
-                const float ev = E[src];
-                v = G[src] - ev;
-                E[src] = ev + v;
+                const float ev = ld1<T>(E + src);
+                v = rnd<T>(ld1<T>(G + src) - ev);
+                st1<T>(E + src, ev + v);
             }
             return v;
         };
-        for (uint32_t e = threadIdx.x; e < (uint32_t)min<int64_t>(pre, cnt); e += 256) dst[e] = one(e);
+        for (uint32_t e = threadIdx.x; e < (uint32_t)min<int64_t>(pre, cnt); e += 256) st1<T>(dst + e, one(e));
         const uint32_t body = cnt > pre ? (uint32_t)((cnt - pre) >> 2) : 0u;
         // body: Q float4 of the packed output per thread and round, every gather load of the
         // round issued before any residual store (the compiler may not move a load from E
@@ -844,9 +848,9 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
             for (int u = 0; u < Q; ++u)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    if constexpr (EF == ARCTOPK_EF_NONE) va[u][j] = G[src[u][j]];
-                    else if constexpr (EF == ARCTOPK_EF14) va[u][j] = E[src[u][j]];
-                    else { va[u][j] = G[src[u][j]]; vb[u][j] = E[src[u][j]]; }
+                    if constexpr (EF == ARCTOPK_EF_NONE) va[u][j] = ld1<T>(G + src[u][j]);
+                    else if constexpr (EF == ARCTOPK_EF14) va[u][j] = ld1<T>(E + src[u][j]);
+                    else { va[u][j] = ld1<T>(G + src[u][j]); vb[u][j] = ld1<T>(E + src[u][j]); }
                 }
 #pragma unroll
             for (int u = 0; u < Q; ++u) {
@@ -860,17 +864,17 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                             vp[j] = va[u][j];
                         } else if constexpr (EF == ARCTOPK_EF14) {
                             vp[j] = va[u][j];
-                            E[src[u][j]] = 0.f;
+                            st1<T>(E + src[u][j], 0.f);
                         } else {
-                            vp[j] = va[u][j] - vb[u][j];
-                            E[src[u][j]] = vb[u][j] + vp[j];
+                            vp[j] = rnd<T>(va[u][j] - vb[u][j]);
+                            st1<T>(E + src[u][j], vb[u][j] + vp[j]);
                         }
                     }
-                    *reinterpret_cast<float4*>(dst + e) = make_float4(vp[0], vp[1], vp[2], vp[3]);
+                    stq<T, false>(dst + e, 0, make_float4(vp[0], vp[1], vp[2], vp[3]));
                 }
             }
         }
-        for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256) dst[e] = one(e);
+        for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256) st1<T>(dst + e, one(e));
         return;
     }
     const uint32_t cnt = (uint32_t)(ch.nrows * m);
@@ -881,7 +885,7 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
             const uint32_t srow = fdiv(e, s.mdiv);
             const uint32_t col = e - srow * (uint32_t)m;
             const int64_t src = s.offset + (int64_t)rl[srow] * m + col;
-            *reinterpret_cast<float4*>(dst + e) = pack4<EF>(G, E, src);
+            stq<T, false>(dst + e, 0, pack4<T, EF>(G, E, src));
         }
     } else {
         for (uint32_t e = threadIdx.x; e < cnt; e += 256) {
@@ -890,16 +894,16 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
             const int64_t src = s.offset + (int64_t)rl[srow] * m + col;
             float v;
             if constexpr (EF == ARCTOPK_EF_NONE) {
-                v = G[src];
+                v = ld1<T>(G + src);
             } else if constexpr (EF == ARCTOPK_EF14) {
-                v = E[src];
-                E[src] = 0.f;
+                v = ld1<T>(E + src);
+                st1<T>(E + src, 0.f);
             } else {
-                const float ev = E[src];
-                v = G[src] - ev;
-                E[src] = ev + v;
+                const float ev = ld1<T>(E + src);
+                v = rnd<T>(ld1<T>(G + src) - ev);
+                st1<T>(E + src, ev + v);
             }
-            dst[e] = v;
+            st1<T>(dst + e, v);
         }
     }
 }
@@ -907,49 +911,51 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
 // ---------------------------------------------------------------------------
 // K4 decode
 // ---------------------------------------------------------------------------
-template <int EF>
+template <typename T, int EF>
 __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                                                 const Chunk* __restrict__ chunks,
-                                                const float* __restrict__ packed,
+                                                const T* __restrict__ packed,
                                                 const int32_t* __restrict__ slotmap, Scale sc,
-                                                float* __restrict__ gE, float* __restrict__ out) {
+                                                T* __restrict__ gE, T* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float dlds[];  // small-m chunk tile
+    // mean of the all-reduced values (ref values_memory.div_(ws)), rounded to T
+    auto mean4 = [&](float4 v) { return rnd4<T>(sc(v)); };
+    auto mean1 = [&](float v) { return rnd<T>(sc(v)); };
     const Chunk ch = chunks[blockIdx.x];
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
     const int64_t base = s.offset + ch.row0 * m;
     const int32_t* sm = slotmap + s.row_off + ch.row0;
-    const float* pk = packed + s.packed_off;
+    const T* pk = packed + s.packed_off;
     if (row_path(s)) {  // wave per row: one slot lookup per row, float4 streams
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const int m4 = m >> 2;
         for (int64_t j = wave; j < ch.nrows; j += 4) {
             const int32_t slot = sm[j];
-            float4* o4 = reinterpret_cast<float4*>(out + base + j * m);
-            float4* g4 = reinterpret_cast<float4*>(gE + base + j * m);
+            T* op = out + base + j * m;
+            T* gp = gE + base + j * m;
             if (slot < 0) {
                 if constexpr (EF == ARCTOPK_EF21) {
 #pragma unroll 4
                     for (int c = lane; c < m4; c += 64) {
-                        const float4 g = ld4<kNtDecode>(g4 + c);
-                        st4<kNtDecode>(o4 + c, make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f));
+                        const float4 g = ldq<T, kNtDecode>(gp, c);
+                        stq<T, kNtDecode>(op, c, make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f));
                     }
                 } else {
 #pragma unroll 8
                     for (int c = lane; c < m4; c += 64)
-                        st4<kNtDecode>(o4 + c, make_float4(0.f, 0.f, 0.f, 0.f));
+                        stq<T, kNtDecode>(op, c, make_float4(0.f, 0.f, 0.f, 0.f));
                 }
             } else {
-                const float4* p4 = reinterpret_cast<const float4*>(pk + (int64_t)slot * m);
+                const T* pp = pk + (int64_t)slot * m;
 #pragma unroll 4
                 for (int c = lane; c < m4; c += 64) {
-                    float4 v = sc(p4[c]);
+                    float4 v = mean4(ldq<T, false>(pp, c));
                     if constexpr (EF == ARCTOPK_EF21) {
-                        const float4 g = ld4<kNtDecode>(g4 + c);
-                        v = make_float4(g.x + v.x, g.y + v.y, g.z + v.z, g.w + v.w);
-                        st4<kNtDecode>(g4 + c, v);
+                        v = rnd4<T>(add4(ldq<T, kNtDecode>(gp, c), v));
+                        stq<T, kNtDecode>(gp, c, v);
                     }
-                    st4<kNtDecode>(o4 + c, v);
+                    stq<T, kNtDecode>(op, c, v);
                 }
             }
         }
@@ -992,14 +998,14 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
         const int cnt = nr * m;
         const int a = (int)(base & 3);
         const int ngroups = (a + cnt + 3) >> 2;
-        float* const ob = out - a + base;  // ob[t] = out[base + e]: 16-B aligned at t % 4 == 0
+        T* const ob = out - a + base;  // ob[t] = out[base + e]: quad-aligned at t % 4 == 0
         // 1. fill
         for (int gi = threadIdx.x; gi < ngroups; gi += 256) {
             const int t0 = gi << 2;
             if (t0 >= a && t0 + 4 <= a + cnt) {
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
                 if constexpr (EF == ARCTOPK_EF21) {
-                    const float4 g = ld4<kNtDecode>(reinterpret_cast<const float4*>(gE - a + base + t0));
+                    const float4 g = ldq<T, kNtDecode>(gE - a + base + t0, 0);
                     v = make_float4(g.x + 0.f, g.y + 0.f, g.z + 0.f, g.w + 0.f);
                 }
                 *reinterpret_cast<float4*>(dlds + t0) = v;
@@ -1008,21 +1014,21 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                 for (int j = 0; j < 4; ++j) {
                     const int t = t0 + j;
                     if (t >= a && t < a + cnt)
-                        dlds[t] = EF == ARCTOPK_EF21 ? gE[base + t - a] + 0.f : 0.f;
+                        dlds[t] = EF == ARCTOPK_EF21 ? ld1<T>(gE + base + t - a) + 0.f : 0.f;
                 }
             }
         }
         __syncthreads();
         // 2. the selected rows
-        const float* src = pk + (int64_t)first * m;
+        const T* src = pk + (int64_t)first * m;
         const uint32_t np = (uint32_t)(nsel * m);
         for (uint32_t p = threadIdx.x; p < np; p += 256) {
             const uint32_t j = div32(p, s.magic32);
             const int le = rows_s[j] * m + (int)(p - j * (uint32_t)m);
-            float v = sc(src[p]);
+            float v = mean1(to_f(src[p]));
             if constexpr (EF == ARCTOPK_EF21) {
-                v = gE[base + le] + v;
-                gE[base + le] = v;
+                v = rnd<T>(ld1<T>(gE + base + le) + v);
+                st1<T>(gE + base + le, v);
             }
             dlds[le + a] = v;
         }
@@ -1031,13 +1037,12 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
         for (int gi = threadIdx.x; gi < ngroups; gi += 256) {
             const int t0 = gi << 2;
             if (t0 >= a && t0 + 4 <= a + cnt) {
-                st4<kNtDecode>(reinterpret_cast<float4*>(ob + t0),
-                               *reinterpret_cast<const float4*>(dlds + t0));
+                stq<T, kNtDecode>(ob + t0, 0, *reinterpret_cast<const float4*>(dlds + t0));
             } else {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int t = t0 + j;
-                    if (t >= a && t < a + cnt) ob[t] = dlds[t];
+                    if (t >= a && t < a + cnt) st1<T>(ob + t, dlds[t]);
                 }
             }
         }
@@ -1052,13 +1057,12 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
             const uint32_t col = e - row * (uint32_t)m;
             const int32_t slot = sm[row];
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (slot >= 0) v = sc(*reinterpret_cast<const float4*>(pk + (int64_t)slot * m + col));
+            if (slot >= 0) v = mean4(ldq<T, false>(pk + (int64_t)slot * m + col, 0));
             if constexpr (EF == ARCTOPK_EF21) {
-                const float4 g = *reinterpret_cast<const float4*>(gE + base + e);
-                v = make_float4(g.x + v.x, g.y + v.y, g.z + v.z, g.w + v.w);
-                if (slot >= 0) *reinterpret_cast<float4*>(gE + base + e) = v;
+                v = rnd4<T>(add4(ldq<T, false>(gE + base + e, 0), v));
+                if (slot >= 0) stq<T, false>(gE + base + e, 0, v);
             }
-            *reinterpret_cast<float4*>(out + base + e) = v;
+            stq<T, false>(out + base + e, 0, v);
         }
     } else {
         for (uint32_t e = threadIdx.x; e < cnt; e += 256) {
@@ -1066,12 +1070,12 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
             const uint32_t col = e - row * (uint32_t)m;
             const int32_t slot = sm[row];
             float v = 0.f;
-            if (slot >= 0) v = sc(pk[(int64_t)slot * m + col]);
+            if (slot >= 0) v = mean1(to_f(pk[(int64_t)slot * m + col]));
             if constexpr (EF == ARCTOPK_EF21) {
-                v = gE[base + e] + v;
-                if (slot >= 0) gE[base + e] = v;
+                v = rnd<T>(ld1<T>(gE + base + e) + v);
+                if (slot >= 0) st1<T>(gE + base + e, v);
             }
-            out[base + e] = v;
+            st1<T>(out + base + e, v);
         }
     }
 }
@@ -1089,81 +1093,78 @@ __global__ void __launch_bounds__(256) k_ef_apply(float* __restrict__ x, float* 
         if constexpr (EF != ARCTOPK_EF14 || ERR_IN) x4[i] = v;
     }
     for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-        const float v = ef_apply1<EF, ERR_IN>(x, E, i);
+        const float v = ef_apply1<float, EF, ERR_IN>(x, E, i);
         if constexpr (EF == ARCTOPK_EF14) E[i] = v;
         if constexpr (EF != ARCTOPK_EF14 || ERR_IN) x[i] = v;
     }
 }
 
-// sketch of column-split tensors: the parts' partial sketches summed in part order
+// sketch of column-split tensors: the parts' fp32 partial sketches summed in part order,
+// then rounded to T once (the reference's mm accumulates in fp32 and rounds its output)
+template <typename T>
 __global__ void __launch_bounds__(256) k_sketch_combine(const SegDev* __restrict__ segs,
                                                         const int32_t* __restrict__ ids, int R,
                                                         const float* __restrict__ part_buf,
-                                                        float* __restrict__ sketch) {
+                                                        T* __restrict__ sketch) {
     const SegDev s = segs[ids[blockIdx.y]];
     const int64_t cnt = s.n * R;
     const float* pb = part_buf + s.part_off;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
         float v = pb[i];
         for (int q = 1; q < s.nparts; ++q) v = __fadd_rn(v, pb[(int64_t)q * cnt + i]);
-        sketch[s.sketch_off + i] = v;
+        st1<T>(sketch + s.sketch_off + i, v);
     }
-}
-
-template <int R, bool VLDS>
-int launch_encode_rv(const arctopk_plan* p, int t0, int t1, size_t lds, const float* G, float* E,
-                     int ef, int err_in, const float* V, float* sk, hipStream_t st) {
-    if (t1 <= t0) return 0;
-    dim3 grid(t1 - t0), block(256);
-    const EncTile* tiles = p->d_enc + t0;
-    float* pb = p->d_part;
-    if (ef == ARCTOPK_EF_NONE)
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF_NONE, false, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-    else if (ef == ARCTOPK_EF14 && err_in)
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, true, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-    else if (ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF14, false, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-    else
-        hipLaunchKernelGGL((k_encode<R, ARCTOPK_EF21, true, VLDS>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-    return (int)hipGetLastError();
 }
 
 // one launch (every tile's V slice fits in LDS), then the partial-sketch sums of
 // column-split tensors
-template <int R>
-int launch_encode_r(const arctopk_plan* p, const float* G, float* E, int ef, int err_in,
-                    const float* V, float* sk, hipStream_t st) {
-    int e = launch_encode_rv<R, true>(p, 0, p->n_enc, (size_t)p->enc_lds_bytes, G, E, ef, err_in, V, sk, st);
-    if (e || p->n_split == 0) return e;
+template <typename T, int R>
+int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
+                    hipStream_t st) {
+    if (p->n_enc > 0) {
+        dim3 grid(p->n_enc), block(256);
+        const size_t lds = (size_t)p->enc_lds_bytes;
+        const EncTile* tiles = p->d_enc;
+        float* pb = p->d_part;
+        if (ef == ARCTOPK_EF_NONE)
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        else if (ef == ARCTOPK_EF14 && err_in)
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        else if (ef == ARCTOPK_EF14)
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        else
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        const int e = (int)hipGetLastError();
+        if (e) return e;
+    }
+    if (p->n_split == 0) return 0;
     const int gx = (int)std::min<int64_t>(256, (p->split_rows_max * R + 255) / 256);
-    hipLaunchKernelGGL(k_sketch_combine, dim3(gx, p->n_split), dim3(256), 0, st, p->d_segs, p->d_split, R,
+    hipLaunchKernelGGL(k_sketch_combine<T>, dim3(gx, p->n_split), dim3(256), 0, st, p->d_segs, p->d_split, R,
                        p->d_part, sk);
     return (int)hipGetLastError();
 }
 
-}  // namespace
-
-extern "C" int arctopk_encode(const arctopk_plan* p, const float* grad, float* err, int32_t ef,
-                              int32_t err_in, const float* V, float* sketch, void* stream) {
-    if (!p || !grad || !sketch) return ARCTOPK_EINVAL;
-    if (ef != ARCTOPK_EF_NONE && !err) return ARCTOPK_EINVAL;
-    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
-    if (p->info.v_len > 0 && !V) return ARCTOPK_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
+template <typename T>
+int launch_encode(const arctopk_plan* p, const void* grad, void* err, int ef, int err_in, const void* V,
+                  void* sketch, hipStream_t st) {
+    const T* G = static_cast<const T*>(grad);
+    T* E = static_cast<T*>(err);
+    const T* Vt = static_cast<const T*>(V);
+    T* sk = static_cast<T*>(sketch);
     switch (p->r) {
-        case 1: return launch_encode_r<1>(p, grad, err, ef, err_in, V, sketch, st);
-        case 2: return launch_encode_r<2>(p, grad, err, ef, err_in, V, sketch, st);
-        case 3: return launch_encode_r<3>(p, grad, err, ef, err_in, V, sketch, st);
-        case 4: return launch_encode_r<4>(p, grad, err, ef, err_in, V, sketch, st);
-        case 5: return launch_encode_r<5>(p, grad, err, ef, err_in, V, sketch, st);
-        case 6: return launch_encode_r<6>(p, grad, err, ef, err_in, V, sketch, st);
-        case 7: return launch_encode_r<7>(p, grad, err, ef, err_in, V, sketch, st);
-        case 8: return launch_encode_r<8>(p, grad, err, ef, err_in, V, sketch, st);
+        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, st);
+        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, st);
+        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, st);
+        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, st);
+        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, st);
+        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, st);
+        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, st);
+        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, st);
     }
     return ARCTOPK_EINVAL;
 }
 
-static Scale make_scale(int32_t ws) {
+Scale make_scale(int32_t ws) {
     Scale sc;
     sc.ws = (float)ws;
     sc.pow2 = (ws & (ws - 1)) == 0;
@@ -1171,29 +1172,24 @@ static Scale make_scale(int32_t ws) {
     return sc;
 }
 
-static int launch_energy(const arctopk_plan* p, const float* sketch, int32_t ws, uint32_t* keys,
-                         float* energy, hipStream_t st) {
+template <typename T>
+int launch_energy(const arctopk_plan* p, const void* sketch, int32_t ws, uint32_t* keys, float* energy,
+                  hipStream_t st) {
     int64_t maxn = 0;
     for (int i = 0; i < p->nseg; ++i) maxn = std::max<int64_t>(maxn, p->h_segs[i].n);
     int gx = (int)std::min<int64_t>(1024, (maxn + 255) / 256);
     dim3 grid(gx, p->nseg);
-    hipLaunchKernelGGL(k_energy, grid, dim3(256), 0, st, p->d_segs, p->nseg, sketch, p->r,
-                       make_scale(ws), keys, energy);
+    hipLaunchKernelGGL(k_energy<T>, grid, dim3(256), 0, st, p->d_segs, p->nseg, static_cast<const T*>(sketch),
+                       p->r, make_scale(ws), keys, energy);
     return (int)hipGetLastError();
 }
 
-extern "C" int arctopk_row_energy(const arctopk_plan* p, const float* sketch, int32_t ws,
-                                  float* energy, void* stream) {
-    if (!p || !sketch || !energy || ws < 1) return ARCTOPK_EINVAL;
-    return launch_energy(p, sketch, ws, nullptr, energy, (hipStream_t)stream);
-}
-
-extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_t ws,
-                              int32_t* rowlist, int32_t* slotmap, void* stream) {
-    if (!p || !sketch || !rowlist || !slotmap || ws < 1) return ARCTOPK_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
+template <typename T>
+int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_t* rowlist, int32_t* slotmap,
+                  hipStream_t st) {
+    const T* sketch = static_cast<const T*>(sketch_);
     if (p->n_small) {
-        hipLaunchKernelGGL(k_select_small, dim3(p->n_small), dim3(kST), (size_t)p->small_lds, st,
+        hipLaunchKernelGGL(k_select_small<T>, dim3(p->n_small), dim3(kST), (size_t)p->small_lds, st,
                            p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
     }
     for (int bi = 0; bi < p->n_large_batches; ++bi) {
@@ -1201,7 +1197,7 @@ extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_
         int64_t maxn = 0;
         for (int i = 0; i < b.cnt; ++i) maxn = std::max<int64_t>(maxn, b.it[i].n);
         const int gx = (int)std::min<int64_t>(kMHistBlocks, (maxn + 1023) / 1024);  // >= 4 rows per lane
-        hipLaunchKernelGGL(k_arc_keys, dim3(gx, b.cnt), dim3(256), 0, st, p->d_segs, p->d_large,
+        hipLaunchKernelGGL(k_arc_keys<T>, dim3(gx, b.cnt), dim3(256), 0, st, p->d_segs, p->d_large,
                            bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws);
         int e = ms_select(b, maxn, p->d_keys, nullptr, true, p->d_mws, p->mws_cap, rowlist, nullptr,
                           slotmap, st);
@@ -1210,58 +1206,110 @@ extern "C" int arctopk_select(const arctopk_plan* p, const float* sketch, int32_
     return (int)hipGetLastError();
 }
 
+template <typename T>
+int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* err_, int32_t ef,
+                const int32_t* rowlist, void* packed_, hipStream_t st) {
+    const T* grad = static_cast<const T*>(grad_);
+    T* err = static_cast<T*>(err_);
+    T* packed = static_cast<T*>(packed_);
+    dim3 grid(c1 - c0), block(256);
+    const Chunk* ch = p->d_pack + c0;
+    if (ef == ARCTOPK_EF_NONE)
+        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF_NONE>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
+    else if (ef == ARCTOPK_EF14)
+        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF14>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
+    else if (ef == ARCTOPK_EF21)
+        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF21>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
+    else
+        return ARCTOPK_EINVAL;
+    return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_decode(const arctopk_plan* p, int c0, int c1, const void* packed_, const int32_t* slotmap,
+                  int32_t ws, int32_t ef, void* gerr_, void* out_, hipStream_t st) {
+    const T* packed = static_cast<const T*>(packed_);
+    T* gerr = static_cast<T*>(gerr_);
+    T* out = static_cast<T*>(out_);
+    dim3 grid(c1 - c0), block(256);
+    const Chunk* ch = p->d_dec + c0;
+    const Scale sc = make_scale(ws);
+    const size_t lds = (size_t)p->dec_lds_bytes;
+    if (ef == ARCTOPK_EF21)
+        hipLaunchKernelGGL((k_decode<T, ARCTOPK_EF21>), grid, block, lds, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+    else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
+        hipLaunchKernelGGL((k_decode<T, ARCTOPK_EF_NONE>), grid, block, lds, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+    else
+        return ARCTOPK_EINVAL;
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int arctopk_encode(const arctopk_plan* p, const void* grad, void* err, int32_t ef,
+                              int32_t err_in, const void* V, void* sketch, void* stream) {
+    if (!p || !grad || !sketch) return ARCTOPK_EINVAL;
+    if (ef != ARCTOPK_EF_NONE && !err) return ARCTOPK_EINVAL;
+    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
+    if (p->info.v_len > 0 && !V) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (p->dtype == ARCTOPK_BF16) return launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, st);
+    return launch_encode<float>(p, grad, err, ef, err_in, V, sketch, st);
+}
+
+extern "C" int arctopk_row_energy(const arctopk_plan* p, const void* sketch, int32_t ws,
+                                  float* energy, void* stream) {
+    if (!p || !sketch || !energy || ws < 1) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (p->dtype == ARCTOPK_BF16) return launch_energy<bf16_t>(p, sketch, ws, nullptr, energy, st);
+    return launch_energy<float>(p, sketch, ws, nullptr, energy, st);
+}
+
+extern "C" int arctopk_select(const arctopk_plan* p, const void* sketch, int32_t ws,
+                              int32_t* rowlist, int32_t* slotmap, void* stream) {
+    if (!p || !sketch || !rowlist || !slotmap || ws < 1) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (p->dtype == ARCTOPK_BF16) return launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, st);
+    return launch_select<float>(p, sketch, ws, rowlist, slotmap, st);
+}
+
 extern "C" int arctopk_pack_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,
-                                     const float* grad, float* err, int32_t ef,
-                                     const int32_t* rowlist, float* packed, void* stream) {
+                                     const void* grad, void* err, int32_t ef,
+                                     const int32_t* rowlist, void* packed, void* stream) {
     if (!p || !rowlist || !packed) return ARCTOPK_EINVAL;
     if (seg_begin < 0 || seg_end > p->nseg || seg_begin > seg_end) return ARCTOPK_EINVAL;
+    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF_NONE ? !grad : !err) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF21 && !grad) return ARCTOPK_EINVAL;
     const int c0 = p->h_pack_begin[seg_begin], c1 = p->h_pack_begin[seg_end];
     if (c1 == c0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid(c1 - c0), block(256);
-    const Chunk* ch = p->d_pack + c0;
-    if (ef == ARCTOPK_EF_NONE)
-        hipLaunchKernelGGL(k_pack<ARCTOPK_EF_NONE>, grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
-    else if (ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL(k_pack<ARCTOPK_EF14>, grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
-    else if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL(k_pack<ARCTOPK_EF21>, grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
-    else
-        return ARCTOPK_EINVAL;
-    return (int)hipGetLastError();
+    if (p->dtype == ARCTOPK_BF16) return launch_pack<bf16_t>(p, c0, c1, grad, err, ef, rowlist, packed, st);
+    return launch_pack<float>(p, c0, c1, grad, err, ef, rowlist, packed, st);
 }
 
-extern "C" int arctopk_pack(const arctopk_plan* p, const float* grad, float* err, int32_t ef,
-                            const int32_t* rowlist, float* packed, void* stream) {
+extern "C" int arctopk_pack(const arctopk_plan* p, const void* grad, void* err, int32_t ef,
+                            const int32_t* rowlist, void* packed, void* stream) {
     if (!p) return ARCTOPK_EINVAL;
     return arctopk_pack_segments(p, 0, p->nseg, grad, err, ef, rowlist, packed, stream);
 }
 
 extern "C" int arctopk_decode_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,
-                                       const float* packed, const int32_t* slotmap, int32_t ws,
-                                       int32_t ef, float* gerr, float* out, void* stream) {
+                                       const void* packed, const int32_t* slotmap, int32_t ws,
+                                       int32_t ef, void* gerr, void* out, void* stream) {
     if (!p || !packed || !slotmap || !out || ws < 1) return ARCTOPK_EINVAL;
     if (seg_begin < 0 || seg_end > p->nseg || seg_begin > seg_end) return ARCTOPK_EINVAL;
+    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF21 && !gerr) return ARCTOPK_EINVAL;
     const int c0 = p->h_dec_begin[seg_begin], c1 = p->h_dec_begin[seg_end];
     if (c1 == c0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid(c1 - c0), block(256);
-    const Chunk* ch = p->d_dec + c0;
-    const Scale sc = make_scale(ws);
-    if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL(k_decode<ARCTOPK_EF21>, grid, block, (size_t)p->dec_lds_bytes, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
-    else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL(k_decode<ARCTOPK_EF_NONE>, grid, block, (size_t)p->dec_lds_bytes, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
-    else
-        return ARCTOPK_EINVAL;
-    return (int)hipGetLastError();
+    if (p->dtype == ARCTOPK_BF16) return launch_decode<bf16_t>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st);
+    return launch_decode<float>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st);
 }
 
-extern "C" int arctopk_decode(const arctopk_plan* p, const float* packed, const int32_t* slotmap,
-                              int32_t ws, int32_t ef, float* gerr, float* out, void* stream) {
+extern "C" int arctopk_decode(const arctopk_plan* p, const void* packed, const int32_t* slotmap,
+                              int32_t ws, int32_t ef, void* gerr, void* out, void* stream) {
     if (!p) return ARCTOPK_EINVAL;
     return arctopk_decode_segments(p, 0, p->nseg, packed, slotmap, ws, ef, gerr, out, stream);
 }

@@ -70,6 +70,111 @@ __device__ __forceinline__ void st4(float4* p, float4 v) {
     if constexpr (NT) st_stream(p, v);
     else *p = v;
 }
+// ---- bucket element types: fp32 and bf16 ---------------------------------------------
+// bf16 is stored as its 16 bits; arithmetic happens in fp32 and every value the
+// reference rounds to bf16 (each aten op on a bf16 tensor: float compute, then
+// round-to-nearest-even, NaN -> 0x7FC0, as c10::BFloat16) is rounded here the same way.
+struct bf16_t {
+    uint16_t u;
+};
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16_t x) { return __uint_as_float((uint32_t)x.u << 16); }
+template <typename T> __device__ __forceinline__ T from_f(float f);
+template <> __device__ __forceinline__ float from_f<float>(float f) { return f; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return bf16_t{(uint16_t)0x7FC0u};
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return bf16_t{(uint16_t)(u >> 16)};
+}
+// value after the reference's rounding to T (identity for fp32)
+template <typename T> __device__ __forceinline__ float rnd(float f) { return to_f(from_f<T>(f)); }
+template <typename T> __device__ __forceinline__ float4 rnd4(float4 v) {
+    return make_float4(rnd<T>(v.x), rnd<T>(v.y), rnd<T>(v.z), rnd<T>(v.w));
+}
+
+// quad I/O: elements 4q .. 4q+3 of p (p 4-element aligned); fp32: 16 B, bf16: 8 B
+typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
+template <typename T, bool NT> __device__ __forceinline__ float4 ldq(const T* p, int64_t q);
+template <> __device__ __forceinline__ float4 ldq<float, false>(const float* p, int64_t q) {
+    return reinterpret_cast<const float4*>(p)[q];
+}
+template <> __device__ __forceinline__ float4 ldq<float, true>(const float* p, int64_t q) {
+    return ld_stream(reinterpret_cast<const float4*>(p) + q);
+}
+__device__ __forceinline__ float4 unpack_bf16x4(u2_t w) {
+    return make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xFFFF0000u),
+                       __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xFFFF0000u));
+}
+__device__ __forceinline__ u2_t pack_bf16x4(float4 v) {
+    const uint32_t a = from_f<bf16_t>(v.x).u, b = from_f<bf16_t>(v.y).u;
+    const uint32_t c = from_f<bf16_t>(v.z).u, d = from_f<bf16_t>(v.w).u;
+    return u2_t{a | (b << 16), c | (d << 16)};
+}
+template <> __device__ __forceinline__ float4 ldq<bf16_t, false>(const bf16_t* p, int64_t q) {
+    return unpack_bf16x4(reinterpret_cast<const u2_t*>(p)[q]);
+}
+template <> __device__ __forceinline__ float4 ldq<bf16_t, true>(const bf16_t* p, int64_t q) {
+    return unpack_bf16x4(__builtin_nontemporal_load(reinterpret_cast<const u2_t*>(p) + q));
+}
+template <typename T, bool NT> __device__ __forceinline__ void stq(T* p, int64_t q, float4 v);
+template <> __device__ __forceinline__ void stq<float, false>(float* p, int64_t q, float4 v) {
+    reinterpret_cast<float4*>(p)[q] = v;
+}
+template <> __device__ __forceinline__ void stq<float, true>(float* p, int64_t q, float4 v) {
+    st_stream(reinterpret_cast<float4*>(p) + q, v);
+}
+template <> __device__ __forceinline__ void stq<bf16_t, false>(bf16_t* p, int64_t q, float4 v) {
+    reinterpret_cast<u2_t*>(p)[q] = pack_bf16x4(v);
+}
+template <> __device__ __forceinline__ void stq<bf16_t, true>(bf16_t* p, int64_t q, float4 v) {
+    __builtin_nontemporal_store(pack_bf16x4(v), reinterpret_cast<u2_t*>(p) + q);
+}
+// 16-B unit I/O: the quads of 16 bytes at unit c of p (p 16-B aligned): fp32 one quad,
+// bf16 two quads (8 elements)
+template <typename T> constexpr int kQuadsPer16 = 16 / (4 * (int)sizeof(T));
+typedef unsigned int u4_t __attribute__((ext_vector_type(4)));
+template <typename T, bool NT>
+__device__ __forceinline__ void ld16(const T* p, int64_t c, float4 (&q)[kQuadsPer16<T>]) {
+    if constexpr (sizeof(T) == 4) {
+        q[0] = ldq<T, NT>(p, c);
+    } else {
+        const u4_t* w4 = reinterpret_cast<const u4_t*>(p) + c;
+        const u4_t w = NT ? __builtin_nontemporal_load(w4) : *w4;
+        q[0] = unpack_bf16x4(u2_t{w.x, w.y});
+        q[1] = unpack_bf16x4(u2_t{w.z, w.w});
+    }
+}
+template <typename T, bool NT>
+__device__ __forceinline__ void st16(T* p, int64_t c, const float4 (&q)[kQuadsPer16<T>]) {
+    if constexpr (sizeof(T) == 4) {
+        stq<T, NT>(p, c, q[0]);
+    } else {
+        const u2_t a = pack_bf16x4(q[0]), b = pack_bf16x4(q[1]);
+        const u4_t w = u4_t{a.x, a.y, b.x, b.y};
+        u4_t* w4 = reinterpret_cast<u4_t*>(p) + c;
+        if constexpr (NT) __builtin_nontemporal_store(w, w4);
+        else *w4 = w;
+    }
+}
+// scalar I/O
+template <typename T, bool NT = false> __device__ __forceinline__ float ld1(const T* p) {
+    if constexpr (NT) {
+        if constexpr (sizeof(T) == 4) return __builtin_nontemporal_load(reinterpret_cast<const float*>(p));
+        else return to_f(bf16_t{__builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(p))});
+    } else {
+        return to_f(*p);
+    }
+}
+template <typename T, bool NT = false> __device__ __forceinline__ void st1(T* p, float v) {
+    if constexpr (NT) {
+        if constexpr (sizeof(T) == 4) __builtin_nontemporal_store(v, reinterpret_cast<float*>(p));
+        else __builtin_nontemporal_store(from_f<bf16_t>(v).u, reinterpret_cast<uint16_t*>(p));
+    } else {
+        *p = from_f<T>(v);
+    }
+}
+
 // streaming hints of the pack / decode kernels (build-time A/B switches)
 #ifndef ARCTOPK_NT_PACK
 #define ARCTOPK_NT_PACK 1
@@ -109,6 +214,7 @@ namespace arctopk { struct MBatch; struct MWorkspace; }
 
 struct arctopk_plan {
     int device;
+    int dtype;                    // ARCTOPK_F32 / ARCTOPK_BF16 (bucket element type)
     int r;
     double ratio;
     int nseg;

@@ -85,7 +85,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     if (!dims || !ndims || !out || ntensors < 1) return ARCTOPK_EINVAL;
     if (r < 1 || r > kMaxR) return ARCTOPK_EINVAL;
     if (!(compress_ratio > 0.0) || compress_ratio > 1.0) return ARCTOPK_EINVAL;
-    if (dtype != ARCTOPK_F32) return ARCTOPK_EDTYPE;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EDTYPE;
     *out = nullptr;
 
     std::vector<arctopk_segment> segs;
@@ -118,13 +118,16 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     bool interleave = true;  // tuning switch (A/B): interleaved row tiles vs contiguous ranges
     if (const char* env = std::getenv("ARCTOPK_ENC_INTERLEAVE")) interleave = std::atoi(env) != 0;
     int64_t part_len = 0, split_rows_max = 0;
+    // vector paths: 16-B encode units (4 fp32 / 8 bf16 elements) need m and the offset to be
+    // multiples of va; pack / decode quads need 4
+    const int64_t va = dtype == ARCTOPK_BF16 ? 8 : 4;
     for (size_t i = 0; i < segs.size(); ++i) {
         const arctopk_segment& s = segs[i];
         SegDev& g = dsegs[i];
         g.offset = s.offset; g.n = s.n; g.m = s.m; g.k_rows = s.k_rows;
         g.sketch_off = s.sketch_off; g.v_off = s.v_off; g.packed_off = s.packed_off;
         g.row_off = s.row_off; g.sel_off = s.sel_off; g.kind = s.kind;
-        g.vec = (s.m % 4 == 0 && s.offset % 4 == 0) ? 1 : 0;  // packed_off is 4-aligned
+        g.vec = (s.m % va == 0 && s.offset % va == 0) ? 1 : 0;  // packed_off is 4-aligned
         g.mdiv = make_fastdiv((uint32_t)s.m);
         g.magic32 = s.m > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)s.m - 1) / (uint64_t)s.m) : 0u;
         g.nparts = 1;
@@ -148,10 +151,10 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         } else {
             const int mode = g.vec ? ENC_ROW_VEC : ENC_ROW_SCALAR;
             // columns per part: V^T slice [r][clen] within kVLdsMaxBytes (multiple of 4)
-            const int64_t max_cols = (kVLdsMaxBytes / (4 * r)) & ~int64_t(3);
+            const int64_t max_cols = (kVLdsMaxBytes / (4 * r)) / va * va;
             const int nparts = (int)((s.m + max_cols - 1) / max_cols);
             int64_t clen = (s.m + nparts - 1) / nparts;
-            clen = (clen + 3) & ~int64_t(3);
+            clen = (clen + va - 1) / va * va;
             if (nparts > 1) {
                 g.nparts = nparts;
                 g.part_off = part_len;
@@ -206,6 +209,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     if (!p) return ARCTOPK_EINVAL;
     std::memset(p, 0, sizeof(*p));
     p->device = device;
+    p->dtype = dtype;
     p->r = r;
     p->ratio = compress_ratio;
     p->nseg = (int)segs.size();

@@ -88,8 +88,8 @@ def ddp_buckets(shapes, first_cap=1 << 20, cap=25 << 20, elem_bytes=4):
     return out
 
 
-def algorithmic_bytes(ef: str, shapes, ratio: float, r: int):
-    """Minimum HBM bytes per call, per phase (fp32, fused design).
+def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4):
+    """Minimum HBM bytes per call, per phase (element size eb, fused design).
 
     1-D tensors are their own sketch (written by encode, read by select); 2-D/ND
     tensors add an [n, r] sketch and read an [m, r] projection.
@@ -100,20 +100,20 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int):
     for s_ in shapes:
         kind, n, m = _geometry(s_)
         k_el += max(1, int(n * ratio)) * m
-        sk += 4 * n * (1 if m == 1 and len(s_) == 1 else r)
-        vbytes += 0 if len(s_) == 1 else m * r * 4
+        sk += eb * n * (1 if m == 1 and len(s_) == 1 else r)
+        vbytes += 0 if len(s_) == 1 else m * r * eb
     if ef == "noef":
-        enc = 4 * n_el + sk + vbytes
-        pack = 4 * k_el + 4 * k_el
-        dec = 4 * k_el + 4 * n_el
+        enc = eb * n_el + sk + vbytes
+        pack = 2 * eb * k_el
+        dec = eb * (k_el + n_el)
     elif ef == "ef14":
-        enc = 12 * n_el + sk + vbytes          # read G, E; write E := G + E
-        pack = 4 * k_el + 4 * k_el + 4 * k_el  # read E rows, write packed, zero E rows
-        dec = 4 * k_el + 4 * n_el
+        enc = 3 * eb * n_el + sk + vbytes          # read G, E; write E := G + E
+        pack = 3 * eb * k_el  # read E rows, write packed, zero E rows
+        dec = eb * (k_el + n_el)
     else:  # ef21
-        enc = 8 * n_el + sk + vbytes           # read G, E
-        pack = 8 * k_el + 4 * k_el + 4 * k_el  # read G, E rows; write packed, E rows
-        dec = 4 * k_el + 4 * n_el + 4 * n_el + 4 * k_el  # packed, gE, out, gE rows
+        enc = 2 * eb * n_el + sk + vbytes           # read G, E
+        pack = 4 * eb * k_el  # read G, E rows; write packed, E rows
+        dec = eb * (2 * k_el + 2 * n_el)  # packed, gE, out, gE rows
     sel = 2 * sk
     return dict(encode=enc, select=sel, pack=pack, decode=dec, total=enc + sel + pack + dec)
 
@@ -178,6 +178,8 @@ def main():
     ap.add_argument("--buckets", type=int, default=4,
                     help="buckets per step (a backward's worth, hooked in order as DDP does); "
                          "each is one workload bucket")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                    help="bucket dtype (f32: every BASELINE config; bf16: the Llama driver's default)")
     ap.add_argument("--ratio", type=float, default=0.2)
     ap.add_argument("--r", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -215,12 +217,14 @@ def main():
         label, shapes = WORKLOADS[args.workload]
         layouts = [shapes] * args.buckets
     nb = len(layouts)
-    bytes_per_step = sum(4 * bucket_numel(sh) for sh in layouts)
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    eb = 2 if args.dtype == "bf16" else 4
+    bytes_per_step = sum(eb * bucket_numel(sh) for sh in layouts)
     n = bucket_numel(shapes)
     bucket_bytes = bytes_per_step // nb
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     # one step = one backward's worth of buckets, hooked in bucket order as DDP does
-    buckets = [SyntheticBucket(torch.randn(bucket_numel(sh), device=dev, generator=g), sh, index=i,
+    buckets = [SyntheticBucket(torch.randn(bucket_numel(sh), device=dev, generator=g).to(dt), sh, index=i,
                                is_last=(i == nb - 1)) for i, sh in enumerate(layouts)]
     if args.hook == "arc":
         st = GroupTopKState(None, r=args.r, compress_ratio=args.ratio, start_compress_iter=0,
@@ -271,7 +275,7 @@ def main():
 
     value = world * args.steps * bytes_per_step / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
-    per_bucket = [algorithmic_bytes(args.ef, sh, args.ratio, args.r) for sh in layouts]
+    per_bucket = [algorithmic_bytes(args.ef, sh, args.ratio, args.r, eb) for sh in layouts]
     alg = {k: sum(d[k] for d in per_bucket) / nb for k in per_bucket[0]}  # mean over the step's buckets
     roof = None
     if phase_ms:
@@ -287,13 +291,14 @@ def main():
                         "achieved": round(alg["total"] / hook_s / 1e9, 1),
                         "frac": round(alg["total"] / hook_s / 1e9 / HBM_PEAK_GBS, 4)}
     if roof is not None:
-        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.workload, args.ef, "k_encode")
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.workload + ("_bf16" if args.dtype == "bf16" else ""), args.ef, "k_encode")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (N(0,1) fp32 gradients, per-rank seed)",
         "config": {"workload": f"{'arctopk' if args.hook == 'arc' else args.hook}_{args.ef}_{nb}x_{label}"
+                               + ("_as_bf16" if args.dtype == "bf16" else "")
                                + ("_host_staged" if args.host_staged else ""),
                    "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
                    "bucket_bytes": bucket_bytes, "buckets_per_step": nb,

@@ -22,7 +22,9 @@
  *    `stream`: no host synchronisation, no allocation (graph-capturable).
  *  - A plan owns its device tables and a select workspace; calls that share a
  *    plan must be ordered on one stream.
- *  - Element type: ARCTOPK_F32 (the bucket dtype of every BASELINE config).
+ *  - Element types: ARCTOPK_F32 (every BASELINE config's bucket) and ARCTOPK_BF16
+ *    (the Llama driver's default dtype).  Bucket-typed buffers are passed as void*.
+ *    The TopK / RandK entry points are fp32 only.
  */
 #ifndef ARCTOPK_H
 #define ARCTOPK_H
@@ -45,8 +47,11 @@ extern "C" {
 #define ARCTOPK_EF14 1
 #define ARCTOPK_EF21 2
 
-/* element types */
+/* element types of a bucket (and of its sketch, projections and packed values, which
+ * the reference keeps in the bucket's dtype: group_topk_hook_no_reshape.py:49, :263) */
 #define ARCTOPK_F32 0
+#define ARCTOPK_BF16 1   /* bfloat16 storage; arithmetic in fp32, each value the reference
+                            rounds to bf16 rounded the same way (round-to-nearest-even) */
 
 /* segment kinds */
 #define ARCTOPK_SEG_RAW 0     /* 1-D tensor: the "sketch" is the tensor itself (ref :19-41) */
@@ -108,8 +113,8 @@ int arctopk_plan_segment(const arctopk_plan* plan, int32_t i, arctopk_segment* s
  * Replaces: input_tensor.add_(error, alpha=+-1) (:227, :234), tensor @ V (:53, :83),
  *           P = P_local.clone() (:31, :56, :86).
  */
-int arctopk_encode(const arctopk_plan* plan, const float* grad, float* err, int32_t ef,
-                   int32_t err_in, const float* V, float* sketch, void* stream);
+int arctopk_encode(const arctopk_plan* plan, const void* grad, void* err, int32_t ef,
+                   int32_t err_in, const void* V, void* sketch, void* stream);
 
 /*
  * K2 select.  From the all-reduced sketch: P /= world_size, row energy
@@ -120,14 +125,14 @@ int arctopk_encode(const arctopk_plan* plan, const float* grad, float* err, int3
  * Replaces: P /= ws; norms = sum(P**2, 1); torch.topk(norms, k, sorted=False);
  *           row*m + arange(m) index materialisation (:34-38, :59-66, :89-96).
  */
-int arctopk_select(const arctopk_plan* plan, const float* sketch, int32_t world_size,
+int arctopk_select(const arctopk_plan* plan, const void* sketch, int32_t world_size,
                    int32_t* rowlist, int32_t* slotmap, void* stream);
 
 /*
  * K2 variant for tests/bit-exact checks: the per-row energy keys only
  * (float bits of the energy the reference feeds torch.topk), keys[row_off + row].
  */
-int arctopk_row_energy(const arctopk_plan* plan, const float* sketch, int32_t world_size,
+int arctopk_row_energy(const arctopk_plan* plan, const void* sketch, int32_t world_size,
                        float* energy, void* stream);
 
 /*
@@ -140,8 +145,8 @@ int arctopk_row_energy(const arctopk_plan* plan, const float* sketch, int32_t wo
  * indices_memory packing (:116-117), EF14 tensor.view(-1)[indices] = 0 (:124),
  * EF21 zero_/index_put (:126-128) and the residual persistence (:270-275).
  */
-int arctopk_pack(const arctopk_plan* plan, const float* grad, float* err, int32_t ef,
-                 const int32_t* rowlist, float* packed, void* stream);
+int arctopk_pack(const arctopk_plan* plan, const void* grad, void* err, int32_t ef,
+                 const int32_t* rowlist, void* packed, void* stream);
 
 /*
  * K4 decode.  From the all-reduced packed values:
@@ -151,8 +156,8 @@ int arctopk_pack(const arctopk_plan* plan, const float* grad, float* err, int32_
  * Replaces: values_memory.div_(ws) (:281), input_tensor.zero_() (:284), the
  * per-tensor index_put scatter (:131-141) and gE.add_/input.copy_ (:288-290).
  */
-int arctopk_decode(const arctopk_plan* plan, const float* packed, const int32_t* slotmap,
-                   int32_t world_size, int32_t ef, float* gerr, float* out, void* stream);
+int arctopk_decode(const arctopk_plan* plan, const void* packed, const int32_t* slotmap,
+                   int32_t world_size, int32_t ef, void* gerr, void* out, void* stream);
 
 /*
  * Segment-range forms of K3/K4 (segments [seg_begin, seg_end) only), so a caller can
@@ -161,11 +166,11 @@ int arctopk_decode(const arctopk_plan* plan, const float* packed, const int32_t*
  * segments in [b, e) occupy packed[seg(b).packed_off, seg(e-1).packed_off + k(e-1)).
  */
 int arctopk_pack_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t seg_end,
-                          const float* grad, float* err, int32_t ef, const int32_t* rowlist,
-                          float* packed, void* stream);
+                          const void* grad, void* err, int32_t ef, const int32_t* rowlist,
+                          void* packed, void* stream);
 int arctopk_decode_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t seg_end,
-                            const float* packed, const int32_t* slotmap, int32_t world_size,
-                            int32_t ef, float* gerr, float* out, void* stream);
+                            const void* packed, const int32_t* slotmap, int32_t world_size,
+                            int32_t ef, void* gerr, void* out, void* stream);
 
 /* ---- TopK / RandK baselines (comm_hooks/sparse_hook.py, sparse_hook_c4.py) ---------- */
 /*
@@ -239,6 +244,15 @@ int arctopk_sparse_decode(float* out, int64_t numel, int32_t ntensors, const int
  * full-bucket E.copy_(input_tensor) of EF14 (:258).
  */
 int arctopk_ef_apply(float* x, float* E, int64_t numel, int32_t ef, int32_t err_in, void* stream);
+
+/*
+ * Host-only (no GPU): `total` (a multiple of 16) consecutive values of the reference's
+ * bf16 projection stream -- torch.randn(..., dtype=bfloat16) on CPU after
+ * torch.manual_seed(seed) (group_topk_hook_no_reshape.py:49, :79, :255) -- as bf16 bit
+ * patterns.  Valid when every tensor's m*r is a multiple of 16 (no tail recompute).
+ * Replaces torch's scalar BFloat16 normal_fill (~8x slower) in the projection prefetch.
+ */
+int arctopk_draw_bf16_normal(uint64_t seed, int64_t total, uint16_t* out);
 
 /* library build identification (for smoke tests) */
 const char* arctopk_version(void);

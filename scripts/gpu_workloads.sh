@@ -27,6 +27,7 @@ done <<LIST
 --workload resnet18_ddp --ef ef14
 --workload headline --ef ef14 --hook topk
 --workload headline --ef ef14 --hook randk
+--workload headline --ef ef14 --dtype bf16
 ${EXTRA_WL}
 LIST
 python scripts/wl_table.py gpurun_out/wl/all.jsonl

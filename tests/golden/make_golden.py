@@ -66,6 +66,11 @@ CASES += [
     dict(name="arc_ties_noef_ws1", hook="arc", shapes=TIES, ratio=0.25, r=4, ef="noef",
          ws=1, iters=1, start=0, seed=11, ties=True),
 ]
+# bf16 buckets (the Llama driver's default dtype, c4/run_llama_pretraining.py:55): V, the
+# sketch, norms and values all in bf16 as the reference keeps them in the bucket dtype
+for ef, ws, iters in (("ef14", 1, 3), ("ef21", 1, 3), ("noef", 2, 2)):
+    CASES.append(dict(name=f"arc_mix_{ef}_bf16_ws{ws}", hook="arc", shapes=MIX, ratio=0.2, r=4,
+                      ef=ef, ws=ws, iters=iters, start=0, seed=1234, dtype="bf16"))
 for ef in ("noef", "ef14", "ef21"):
     CASES.append(dict(name=f"topk_mix_{ef}_ws1", hook="sparse", random=False, shapes=SPARSE_MIX,
                       ratio=0.2, ef=ef, ws=1, iters=2, start=0, seed=5))
@@ -99,7 +104,15 @@ def make_grad(case, it, rank):
         rows[~keep] = 0.0
         tail = x[n0:]
         tail[torch.rand(tail.numel(), generator=g) < 0.6] = 0.0
+    if case.get("dtype") == "bf16":
+        x = x.to(torch.bfloat16)
     return x
+
+
+def _np(t):
+    """numpy has no bf16: bf16 tensors are stored as their int16 bit patterns (meta dtype)."""
+    t = t.detach().cpu()
+    return t.view(torch.int16).numpy() if t.dtype == torch.bfloat16 else t.numpy()
 
 
 # --------------------------------------------------------------------------
@@ -185,22 +198,22 @@ def run_rank(rank, ws, case, port, outdir):
             fut = hook(state, bucket)
             out = fut.wait()
         p = f"it{it}_"
-        arrays[p + "G"] = G.numpy()
-        arrays[p + "out"] = out.detach().clone().numpy()
+        arrays[p + "G"] = _np(G)
+        arrays[p + "out"] = _np(out.clone())
         if 0 in getattr(state, "error_dict", {}):
-            arrays[p + "E"] = state.error_dict[0].clone().numpy()
+            arrays[p + "E"] = _np(state.error_dict[0].clone())
         if 0 in getattr(state, "global_error_dict", {}):
-            arrays[p + "gE"] = state.global_error_dict[0].clone().numpy()
+            arrays[p + "gE"] = _np(state.global_error_dict[0].clone())
         arrays[p + "bits"] = np.array(int(state.comm_bits_this_round), dtype=np.int64)
         arrays[p + "iter_after"] = np.array(int(state.iter), dtype=np.int64)
         if "seed" in rec:
             arrays[p + "seed"] = np.array(rec["seed"], dtype=np.int64)
         for j, v in enumerate(rec.get("V", [])):
-            arrays[p + f"V{j}"] = v.numpy()
+            arrays[p + f"V{j}"] = _np(v)
         for j, a in enumerate(rec.get("AR", [])):
-            arrays[p + f"AR{j}"] = a.numpy()
+            arrays[p + f"AR{j}"] = _np(a)
         for j, (inp, k, idx) in enumerate(rec.get("topk", [])):
-            arrays[p + f"topk{j}_in"] = inp.numpy()
+            arrays[p + f"topk{j}_in"] = _np(inp)
             arrays[p + f"topk{j}_k"] = np.array(k, dtype=np.int64)
             arrays[p + f"topk{j}_idx"] = idx.numpy()
         for j, perm in enumerate(rec.get("perm", [])):

@@ -29,7 +29,10 @@ class Golden:
         return self.z[f"r{rank}_it{it}_{key}"]
 
     def t(self, rank, it, key):
-        return torch.from_numpy(np.array(self.z[f"r{rank}_it{it}_{key}"]))
+        a = torch.from_numpy(np.array(self.z[f"r{rank}_it{it}_{key}"]))
+        if self.meta.get("dtype") == "bf16" and a.dtype == torch.int16:  # stored bit patterns
+            a = a.view(torch.bfloat16)
+        return a
 
     def count(self, rank, it, prefix):
         n = 0

@@ -173,7 +173,7 @@ def test_hook_end_to_end_vs_oracle(ef, which):
     assert numel == bucket.buffer().numel()
 
 
-@pytest.mark.parametrize("name", [n for n in case_names("arc_") if n.endswith("ws1")])
+@pytest.mark.parametrize("name", [n for n in case_names("arc_") if n.endswith("ws1") and "bf16" not in n])
 def test_golden_vectors_on_gpu(name):
     """Replay reference-generated golden vectors through the HIP hook."""
     g = Golden(name)
@@ -315,3 +315,91 @@ def test_select_degenerate_energies(fill):
     for r_, nrm, s in zip(_gpu_rows(plan), norms, plan.segments):
         assert check_rows_tie_aware(r_, nrm, int(s.k_rows), band=0.0) == 0
         assert torch.all(r_[1:] > r_[:-1])
+
+
+@pytest.mark.parametrize("name", [n for n in case_names("arc_") if "bf16" in n and n.endswith("ws1")])
+def test_bf16_golden_on_gpu(name):
+    """bf16 buckets against reference-generated golden vectors.
+
+    bf16 norms tie often at the k-th value and the reference's topk tie order is
+    implementation-defined, so: energies from the reference's own sketch are compared
+    bit for bit, the device's selected rows must satisfy the reference's norms under the
+    tie rule (within one bf16 rounding of the sketch), and every output / residual is
+    bit-exact against the oracle (pinned to the same golden vectors) given those rows.
+    """
+    g = Golden(name)
+    m = g.meta
+    shapes = [tuple(s) for s in m["shapes"]]
+    ef = m["ef"]
+    segs = A.segments(shapes, m["ratio"])
+    st = GroupTopKState(None, r=m["r"], compress_ratio=m["ratio"],
+                        start_compress_iter=m["start"], use_error_feedback=ef, seed=m["seed"])
+    ost = A.OracleState(seed=m["seed"])
+    E_prev = gE_prev = None
+    stream = torch.cuda.current_stream().cuda_stream
+    for it in range(m["iters"]):
+        G = g.t(0, it, "G")
+        assert G.dtype == torch.bfloat16
+        out = group_topk_hook(st, SyntheticBucket(G.to(DEV), shapes, index=0, is_last=True)).wait()
+        torch.cuda.synchronize()
+        if ef == "ef21" and E_prev is None:  # dense init call: bit-exact vs the reference
+            assert_bitwise(out, g.t(0, it, "out"), f"{name} it{it} init out")
+            E_prev, gE_prev = G.clone(), g.t(0, it, "gE")
+            assert_bitwise(st.global_error_dict[0], gE_prev, f"{name} it{it} init gE")
+            continue
+        plan = st._plans[0][1]
+        rows = _gpu_rows(plan)
+        # select math on the reference's own (all-reduced) sketch: bit-exact energies
+        ref_sk = torch.cat([g.t(0, it, f"AR{j}").flatten() for j in range(len(segs))])
+        plan.sketch[:ref_sk.numel()].copy_(ref_sk.to(DEV))
+        energy = torch.empty(plan.info.rows_total, device=DEV)
+        plan.row_energy(1, energy, stream)
+        torch.cuda.synchronize()
+        en = energy.cpu()
+        for j, s in enumerate(plan.segments):
+            ref_norm = g.t(0, it, f"topk{j}_in").float()
+            assert_bitwise(en[s.row_off:s.row_off + s.n], ref_norm, f"{name} it{it} energy seg{j}")
+            # rows chosen from the device's own sketch: the reference's norms, tie rule, one
+            # bf16 rounding (2^-8 relative) of band for sketch values summed in another order
+            check_rows_tie_aware(rows[j], ref_norm, int(s.k_rows), band=2.0 ** -7)
+        seed = ost.next_seed()
+        assert int(g.np(0, it, "seed")[0]) == seed
+        res = A.simulate_step([G], [E_prev], gE_prev, shapes, m["ratio"], m["r"], ef, seed,
+                              rows_override=rows)
+        assert_bitwise(out, res["out"], f"{name} it{it} out given the rows")
+        if ef != "noef":
+            assert_bitwise(st.error_dict[0], res["E_new"][0], f"{name} it{it} E given the rows")
+            E_prev = res["E_new"][0]
+        if ef == "ef21":
+            assert_bitwise(st.global_error_dict[0], res["gE_new"], f"{name} it{it} gE")
+            gE_prev = res["gE_new"]
+        assert st.comm_bits_this_round == int(g.np(0, it, "bits"))
+
+
+def test_bf16_headline_bucket_properties():
+    """16 x [2048, 2048] bf16 (128 MiB), EF14: exact k, kept rows outrank dropped rows, and
+    out + E_new == G + E_old bit for bit (all in bf16)."""
+    shapes = [[2048, 2048]] * 16
+    numel = bucket_numel(shapes)
+    torch.manual_seed(0)
+    st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                        use_error_feedback="ef14", seed=1234)
+    group_topk_hook(st, SyntheticBucket(torch.randn(numel, device=DEV).bfloat16(), shapes)).wait()
+    G1 = torch.randn(numel, device=DEV).bfloat16()
+    E_before = st.error_dict[0].clone()
+    assert E_before.dtype == torch.bfloat16
+    out = group_topk_hook(st, SyntheticBucket(G1.clone(), shapes)).wait()
+    torch.cuda.synchronize()
+    plan = st._plans[0][1]
+    rows = _gpu_rows(plan)
+    energy = torch.empty(plan.info.rows_total, device=DEV)
+    plan.row_energy(1, energy, torch.cuda.current_stream().cuda_stream)
+    en = energy.cpu()
+    for s, r_ in zip(plan.segments, rows):
+        assert r_.numel() == s.k_rows == 409
+        e = en[s.row_off:s.row_off + s.n]
+        mask = torch.zeros(s.n, dtype=torch.bool)
+        mask[r_] = True
+        assert e[mask].min() >= e[~mask].max(), "a dropped row outranks a selected one"
+    X = G1 + E_before  # bf16 add, as the reference's input_tensor.add_(error)
+    assert torch.equal(out + st.error_dict[0], X)

@@ -212,3 +212,37 @@ def test_state_dict_roundtrip_weights_only(tmp_path, which):
     a = torch.randint(0, 1_000_000_000, (4,), generator=st.rng)
     b = torch.randint(0, 1_000_000_000, (4,), generator=st2.rng)
     assert torch.equal(a, b)
+
+
+def test_bf16_projection_tables_match_torch():
+    """libarctopk's table-driven bf16 draw equals torch's CPU bf16 normal_ bit for bit: 8M
+    draws at four seeds exercise every one of the 65,536 (u[j], u[j+8]) table cells."""
+    import numpy as np
+    from allreducetopk_amd.comm_hooks.projections import draw_bf16_into
+    seen = np.zeros((256, 256), dtype=bool)
+    for seed in (0, 1, 123456789, 999_999_999):
+        n = 1 << 21
+        ref = torch.randn(n, dtype=torch.bfloat16, generator=torch.Generator().manual_seed(seed))
+        got = torch.empty(n, dtype=torch.bfloat16)
+        draw_bf16_into(seed, got)
+        assert torch.equal(got, ref), f"seed {seed}: {(got != ref).sum().item()} values differ"
+        st = np.random.RandomState(seed).get_state()  # torch's CPU generator = mt19937(seed)
+        bg = np.random.MT19937()
+        bg.state = {"bit_generator": "MT19937", "state": {"key": st[1], "pos": st[2]}}
+        d = (bg.random_raw(n) & 0xFF).reshape(-1, 2, 8)
+        seen[d[:, 0].ravel(), d[:, 1].ravel()] = True
+    assert seen.all(), "not every table cell was exercised"
+
+
+@pytest.mark.parametrize("seed", [0, 440527571])
+def test_bf16_projection_draw_matches_reference_stream(seed):
+    """A bucket's bf16 projections (fast path and torch fallback) equal the reference's
+    per-tensor torch.randn(m, r, dtype=bf16) after the global reseed."""
+    for shapes in ([(2048, 2048)] * 3 + [(40, 16), (4, 3, 3, 3)],   # fast path: m*r % 16 == 0
+                   [(40, 16), (16, 8, 1, 1), (96, 40), (5461, 33)]):  # m*r = 8, 132: fallback
+        segs = A.segments(shapes, 0.2)
+        ref = torch.cat([v.flatten() for v in A.draw_projections(seed, segs, 4, torch.bfloat16)
+                         if v is not None])
+        ms = [s.m for s in segs if s.kind == A.SKETCH]
+        got = draw_host(seed, ms, 4, torch.bfloat16, pin=False)
+        assert torch.equal(got[:ref.numel()], ref)

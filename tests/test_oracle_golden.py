@@ -28,6 +28,7 @@ def test_arc_oracle_matches_reference(name):
     g = Golden(name)
     m = g.meta
     ws, shapes, ef = m["ws"], [tuple(s) for s in m["shapes"]], m["ef"]
+    eb = 16 if m.get("dtype") == "bf16" else 32  # element bits of the bucket dtype
     st = A.OracleState(r=m["r"], compress_ratio=m["ratio"], start_compress_iter=m["start"],
                        use_error_feedback=ef, seed=m["seed"])
     Es = [None] * ws
@@ -42,7 +43,7 @@ def test_arc_oracle_matches_reference(name):
                 acc = acc + Gs[q] / ws
             for q in range(ws):
                 _eq(acc, g.t(q, it, "out"), f"{name} it{it} warm-up out")
-            bits += 2 * (ws - 1) * Gs[0].numel() * 32
+            bits += 2 * (ws - 1) * Gs[0].numel() * eb
         elif ef == "ef21" and Es[0] is None:  # EF21 init (ref :236-250)
             Es = [G.clone() for G in Gs]
             acc = Gs[0].clone()
@@ -54,7 +55,7 @@ def test_arc_oracle_matches_reference(name):
                 _eq(acc, g.t(q, it, "out"), f"{name} it{it} ef21-init out")
                 _eq(gE, g.t(q, it, "gE"), f"{name} it{it} ef21-init gE")
                 _eq(Es[q], g.t(q, it, "E"), f"{name} it{it} ef21-init E")
-            bits += Gs[0].numel() * 32
+            bits += Gs[0].numel() * eb
         else:
             if ef == "ef14" and Es[0] is None:
                 Es = [None] * ws
@@ -84,7 +85,7 @@ def test_arc_oracle_matches_reference(name):
                 Es = res["E_new"]
             if ef == "ef21":
                 gE = res["gE_new"]
-            bits += 2 * (ws - 1) * A.bits_per_call(segs, m["r"], 32)
+            bits += 2 * (ws - 1) * A.bits_per_call(segs, m["r"], eb)
             del first
         it_count += 1
         for q in range(ws):
