@@ -20,8 +20,14 @@ same projections V (torch CPU generator), the same k per tensor, the same
 output bucket and residuals.  Selected rows are identical to the reference's
 except where two rows' sketch energies are equal within fp32 rounding of the
 sketch (the GPU sums G.V in a different order than CPU sgemm); exact ties at
-the k-th energy are resolved lowest-row-first.  The hook returns an already
-completed Future holding the bucket, as the reference does (:294-297).
+the k-th energy are resolved lowest-row-first.  Buckets may be float32 or
+bfloat16 (every value the reference rounds to bf16 is rounded the same way).
+
+At world size 1 the hook returns an already completed Future holding the bucket,
+as the reference does (:294-297).  At world size > 1 (``async_exchange``) the
+packed all-reduce and the decode run off the caller's stream and the Future is
+device-aware: ``wait()`` makes the waiting stream wait for the decode, as DDP's
+finalize does, so the next bucket's encode overlaps this bucket's exchange.
 """
 
 import logging
