@@ -106,7 +106,12 @@ class BucketPlan:
         # copy for call i+1 overlaps call i's kernels instead of sitting between them
         self.V_ring = [torch.empty(max(1, info.v_len), dtype=dtype, device=dev)
                        for _ in range(self.V_RING)]
-        self._v_used = [None] * self.V_RING  # event after the encode that last read the slot
+        # events are created once and re-recorded (a wait captures the latest record):
+        # _v_used[i] follows the encode that last read slot i, _v_ready[i] its H2D copy
+        self._v_used = [None] * self.V_RING
+        self._v_ready = [None] * self.V_RING
+        self._v_live = [False] * self.V_RING
+        self.decode_done = None  # recorded after this bucket's side-stream decode
         self._v_streams = [None] * self.V_RING
         self._v_next = 0
         self.groups = self._make_groups()
@@ -128,20 +133,21 @@ class BucketPlan:
         if self._v_streams[i] is not copy_stream:  # allocator: the slot is also used there
             buf.record_stream(copy_stream)
             self._v_streams[i] = copy_stream
-        if self._v_used[i] is not None:  # the encode that read this slot must be done
+        if self._v_live[i]:  # the encode that read this slot must be done
             copy_stream.wait_event(self._v_used[i])
         n = int(self.info.v_len)
         with torch.cuda.stream(copy_stream):
             buf[:n].copy_(host[:n], non_blocking=True)
-        ready = torch.cuda.Event()
-        ready.record(copy_stream)
-        stream.wait_event(ready)
+        if self._v_ready[i] is None:
+            self._v_ready[i] = torch.cuda.Event()
+            self._v_used[i] = torch.cuda.Event()
+        self._v_ready[i].record(copy_stream)
+        stream.wait_event(self._v_ready[i])
         return i, buf
 
     def projection_consumed(self, i: int, stream) -> None:
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        self._v_used[i] = ev
+        self._v_used[i].record(stream)
+        self._v_live[i] = True
 
     def _make_groups(self):
         """Contiguous segment ranges with roughly equal packed bytes: (b, e, lo, hi)."""
@@ -501,9 +507,10 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                 w.wait()  # the side stream (current here) waits for the collective
                 plan.decode_range(b_, e_, world_size, ef, gerr, input_tensor, ds.cuda_stream)
             mark("decode", ds)
-            done = torch.cuda.Event()
-            done.record(ds)
-            state._pending[b] = done
+            if plan.decode_done is None:
+                plan.decode_done = torch.cuda.Event()
+            plan.decode_done.record(ds)
+            state._pending[b] = plan.decode_done
             state.maybe_increase_iter(bucket)
             # a device-aware Future: wait()/value() make the waiter's stream wait for decode
             fut = torch.futures.Future(devices=[dev])

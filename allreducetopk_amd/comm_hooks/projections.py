@@ -92,7 +92,7 @@ def draw_host(seed: int, ms: Sequence[int], r: int, dtype: torch.dtype, pin: boo
 class Slot:
     """A reusable pinned host buffer for one column list, with its fill views."""
 
-    __slots__ = ("key", "host", "views", "event", "fast")
+    __slots__ = ("key", "host", "views", "event", "pending", "fast")
 
     def __init__(self, key, ms, r, dtype, pin):
         self.key = key
@@ -101,12 +101,13 @@ class Slot:
         self.views = _fill_plan(self.host, ms, r, dtype)
         # bf16: the native table-driven draw (bit-identical to torch's normal_)
         self.fast = self.host[:total] if dtype == torch.bfloat16 and total and bf16_fast_ok(ms, r) else None
-        self.event = None  # set when an async copy out of `host` was enqueued
+        self.event = None      # reused event: recorded after an async copy out of `host`
+        self.pending = False   # ... and that copy may still be running
 
     def fill(self, seed: int):
-        if self.event is not None:  # the previous H2D copy from this buffer must be done
+        if self.pending:  # the previous H2D copy from this buffer must be done
             self.event.synchronize()
-            self.event = None
+            self.pending = False
         if self.fast is not None:
             draw_bf16_into(seed, self.fast)
             return self
@@ -173,9 +174,10 @@ class ProjectionSource:
     def release(self, slot: Slot, stream=None):
         """Return a slot; with `stream`, after the work enqueued on it so far (the copy)."""
         if stream is not None:
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            slot.event = ev
+            if slot.event is None:
+                slot.event = torch.cuda.Event()
+            slot.event.record(stream)
+            slot.pending = True
         with self._lock:
             self._free[slot.key].append(slot)
 

@@ -16,13 +16,21 @@ os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29511")
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import WORKLOADS  # noqa: E402
-shapes = WORKLOADS[os.environ.get("WORKLOAD", "headline")][1]
-buf = torch.randn(bucket_numel(shapes), device="cuda:0")
-b = SyntheticBucket(buf, shapes)
+from bench import WORKLOADS, ddp_buckets, resnet18_cifar_shapes  # noqa: E402
+wl = os.environ.get("WORKLOAD", "headline")
+layouts = ddp_buckets(resnet18_cifar_shapes()) if wl == "resnet18_ddp" else [WORKLOADS[wl][1]]
+bks = [SyntheticBucket(torch.randn(bucket_numel(sh), device="cuda:0"), sh, index=i,
+                       is_last=(i == len(layouts) - 1)) for i, sh in enumerate(layouts)]
 st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback="ef14", seed=1)
+
+
+def call_all():
+    for b in bks:
+        group_topk_hook(st, b)
+
+
 for _ in range(5):
-    group_topk_hook(st, b)
+    call_all()
 torch.cuda.synchronize()
 
 
@@ -30,7 +38,7 @@ def loop(n):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(n):
-        group_topk_hook(st, b)
+        call_all()
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
