@@ -72,6 +72,7 @@ _SIGS = {
                                         c_int32, c_void_p, c_void_p]),
     "arctopk_ef_apply": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
     "arctopk_draw_bf16_normal": (c_int32, [c_uint64, c_int64, c_void_p]),
+    "arctopk_draw_normal": (c_int32, [c_uint64, c_int32, c_int32, POINTER(c_int64), c_void_p]),
     "arctopk_version": (c_char_p, []),
 }
 

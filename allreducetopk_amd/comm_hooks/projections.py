@@ -3,40 +3,78 @@
 Reference semantics (comm_hooks/group_topk_hook_no_reshape.py:254-255, :49, :79):
 per bucket call a seed is drawn from ``state.rng`` (a CPU generator), the global
 RNG is reseeded with it, and ``torch.randn(m, r)`` is drawn once per 2-D/ND
-tensor in bucket order.  V is drawn here with torch's CPU generator (mt19937 +
-torch's normal transform): a private ``torch.Generator`` seeded with the same
-seed yields exactly that stream, so the projections -- and therefore the
-selected rows -- are those of the reference on CPU bit for bit.
+tensor in bucket order.  V is drawn here from torch's CPU generator stream (mt19937 +
+torch's normal transform), so the projections -- and therefore the selected rows --
+are those of the reference on CPU bit for bit.
 
-Drawing V for a 16 x [2048, 2048] bucket costs ~0.5 ms of host time, more than
-the whole GPU codec.  V depends only on (seed, column counts), and the seed
-sequence is deterministic, so a small thread pool draws the projections of the
-*next* calls while the current one runs (``depth`` calls ahead).  A miss (first
-call, changed bucket order) draws synchronously; hits and misses return the
-same values.
+One native call (libarctopk's ``arctopk_draw_normal``, projection.cpp) draws a whole
+bucket's V without the GIL; it restates torch's CPU ``normal_`` (vectorised 16-blocks
+with the tail recompute, the scalar Box-Muller path with its cached sample for tensors
+of < 16 values).  It is checked against torch itself once per process and dtype
+(:func:`native_ok`); should they ever differ (a torch build whose kernel uses other math
+routines) the projections fall back to per-tensor torch draws -- the same values, slower.
+
+Drawing V for a 16 x [2048, 2048] bucket still costs ~1 ms of host time, more than the
+whole GPU codec.  V depends only on (seed, column counts), and the seed sequence is
+deterministic, so a small thread pool draws the projections of the *next* calls while
+the current one runs (``depth`` calls ahead); buckets with few projection values are
+drawn synchronously (cheaper than a hand-off to a thread).  A miss (first call, changed
+bucket order) draws synchronously; hits and misses return the same values.
 """
 from __future__ import annotations
 
 import collections
+import ctypes
+import logging
 import threading
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 
+logger = logging.getLogger(__name__)
 
-# ---- bf16 projections -----------------------------------------------------------------
-# torch's CPU normal_ on a bf16 tensor (the reference's torch.randn(m, r, dtype=bfloat16))
-# runs a scalar BFloat16 loop, ~8x slower than the fp32 path and slower than the device
-# codec.  For every tensor with m*r a multiple of 16 the values are a table function of
-# 8-bit mt19937 uniforms; libarctopk's host routine arctopk_draw_bf16_normal computes them
-# bit-identically (projection.cpp; tests/test_host_logic.py pins it against torch) and,
-# called through ctypes, without holding the GIL.
+SYNC_MAX_VALUES = 4096  # projection values drawn on the caller's thread instead of prefetched
 
 
-def bf16_fast_ok(ms: Sequence[int], r: int) -> bool:
-    """Every tensor's draw is whole 16-blocks (no tail recompute, no scalar path)."""
-    return all(int(m) * r >= 16 and (int(m) * r) % 16 == 0 for m in ms)
+def _sizes(ms: Sequence[int], r: int):
+    return (ctypes.c_int64 * max(1, len(ms)))(*[int(m) * r for m in ms])
+
+
+def _draw_native(seed: int, sizes, ntensors: int, dtype: torch.dtype, out: torch.Tensor) -> None:
+    from allreducetopk_amd import _native as N
+    N.check(N.lib().arctopk_draw_normal(int(seed), N.DTYPE_CODE[dtype], ntensors, sizes,
+                                        out.data_ptr()), "arctopk_draw_normal")
+
+
+_NATIVE_OK: Dict[torch.dtype, bool] = {}
+_NATIVE_LOCK = threading.Lock()
+# sizes covering both torch paths: < 16 values (scalar, with the cached second sample
+# carried across tensors, odd counts), 16-multiples, and tails that are recomputed
+_CHECK_SIZES = (8, 3, 72, 16, 5, 4101, 12, 8192, 7, 36, 1, 600)
+
+
+def native_ok(dtype: torch.dtype) -> bool:
+    """Whether the native draw equals torch's CPU randn stream here (checked once)."""
+    ok = _NATIVE_OK.get(dtype)
+    if ok is not None:
+        return ok
+    with _NATIVE_LOCK:
+        ok = _NATIVE_OK.get(dtype)
+        if ok is None:
+            seed = 440527571
+            g = torch.Generator().manual_seed(seed)
+            ref = torch.cat([torch.randn(n, dtype=dtype, generator=g) for n in _CHECK_SIZES])
+            got = torch.empty_like(ref)
+            _draw_native(seed, (ctypes.c_int64 * len(_CHECK_SIZES))(*_CHECK_SIZES),
+                         len(_CHECK_SIZES), dtype, got)
+            iv = torch.int16 if dtype == torch.bfloat16 else torch.int32
+            ok = bool(torch.equal(got.view(iv), ref.view(iv)))
+            if not ok:
+                logger.warning("native %s projection draw differs from this torch build's CPU "
+                               "randn; using per-tensor torch draws", dtype)
+            _NATIVE_OK[dtype] = ok
+    return ok
 
 
 def draw_bf16_into(seed: int, out: torch.Tensor) -> None:
@@ -47,7 +85,8 @@ def draw_bf16_into(seed: int, out: torch.Tensor) -> None:
 
 
 def _fill_plan(host: torch.Tensor, ms: Sequence[int], r: int, dtype: torch.dtype):
-    """Views of `host` that one generator pass fills in the reference's stream order.
+    """Views of `host` that one torch generator pass fills in the reference's stream order
+    (the fallback when the native draw is not usable).
 
     Consecutive tensors whose m*r is a multiple of 16 share ONE view: torch's CPU normal
     fill draws all uniforms in stream order and transforms them in independent 16-value
@@ -76,31 +115,36 @@ def _fill_plan(host: torch.Tensor, ms: Sequence[int], r: int, dtype: torch.dtype
     return views
 
 
+def _torch_fill(seed: int, views) -> None:
+    g = torch.Generator().manual_seed(int(seed))
+    for v in views:
+        v.normal_(generator=g)
+
+
 def draw_host(seed: int, ms: Sequence[int], r: int, dtype: torch.dtype, pin: bool) -> torch.Tensor:
     """Concatenated [m_i][r] projections for one call, on the host (pinned if asked)."""
     total = sum(int(m) * r for m in ms)
     host = torch.empty(max(total, 1), dtype=dtype, pin_memory=pin)
-    if dtype == torch.bfloat16 and total and bf16_fast_ok(ms, r):
-        draw_bf16_into(seed, host[:total])
-        return host
-    g = torch.Generator().manual_seed(int(seed))
-    for v in _fill_plan(host, ms, r, dtype):
-        v.normal_(generator=g)
+    if total and native_ok(dtype):
+        _draw_native(seed, _sizes(ms, r), len(ms), dtype, host)
+    else:
+        _torch_fill(seed, _fill_plan(host, ms, r, dtype))
     return host
 
 
 class Slot:
-    """A reusable pinned host buffer for one column list, with its fill views."""
+    """A reusable pinned host buffer for one column list."""
 
-    __slots__ = ("key", "host", "views", "event", "pending", "fast")
+    __slots__ = ("key", "host", "total", "sizes", "n", "dtype", "views", "event", "pending")
 
     def __init__(self, key, ms, r, dtype, pin):
         self.key = key
-        total = sum(int(m) * r for m in ms)
-        self.host = torch.empty(max(total, 1), dtype=dtype, pin_memory=pin)
-        self.views = _fill_plan(self.host, ms, r, dtype)
-        # bf16: the native table-driven draw (bit-identical to torch's normal_)
-        self.fast = self.host[:total] if dtype == torch.bfloat16 and total and bf16_fast_ok(ms, r) else None
+        self.total = sum(int(m) * r for m in ms)
+        self.host = torch.empty(max(self.total, 1), dtype=dtype, pin_memory=pin)
+        self.sizes = _sizes(ms, r)
+        self.n = len(ms)
+        self.dtype = dtype
+        self.views = None if native_ok(dtype) else _fill_plan(self.host, ms, r, dtype)
         self.event = None      # reused event: recorded after an async copy out of `host`
         self.pending = False   # ... and that copy may still be running
 
@@ -108,12 +152,12 @@ class Slot:
         if self.pending:  # the previous H2D copy from this buffer must be done
             self.event.synchronize()
             self.pending = False
-        if self.fast is not None:
-            draw_bf16_into(seed, self.fast)
+        if not self.total:
             return self
-        g = torch.Generator().manual_seed(int(seed))
-        for v in self.views:
-            v.normal_(generator=g)
+        if self.views is None:
+            _draw_native(seed, self.sizes, self.n, self.dtype, self.host)
+        else:
+            _torch_fill(seed, self.views)
         return self
 
 
@@ -196,16 +240,18 @@ class ProjectionSource:
         """Schedule the projections of the next ``len(upcoming_ms)`` calls."""
         if self.depth <= 0 or not upcoming_ms:
             return
-        if self._pool is None:
-            self._pool = ThreadPoolExecutor(max_workers=self._workers,
-                                            thread_name_prefix="arctopk-proj")
         seeds = self._peek_seeds(min(self.depth, len(upcoming_ms)))
         stale = []
         with self._lock:
             live = set()
             for seed, ms in zip(seeds, upcoming_ms):
+                if sum(ms) * self.r < SYNC_MAX_VALUES:  # drawn by get() on the caller's thread
+                    continue
                 key = (seed, ms, dtype)
                 live.add(key)
+                if self._pool is None:
+                    self._pool = ThreadPoolExecutor(max_workers=self._workers,
+                                                    thread_name_prefix="arctopk-proj")
                 if key not in self._pending:
                     self._pending[key] = self._pool.submit(
                         lambda sd=seed, m_=ms: self._slot(m_, dtype).fill(sd))

@@ -254,6 +254,17 @@ int arctopk_ef_apply(float* x, float* E, int64_t numel, int32_t ef, int32_t err_
  */
 int arctopk_draw_bf16_normal(uint64_t seed, int64_t total, uint16_t* out);
 
+/*
+ * Host-only (no GPU): one bucket call's projections -- for each of `ntensors` tensors in
+ * bucket order, sizes[t] = m_t * r values of torch.randn(m_t, r, dtype) on CPU, all drawn
+ * from ONE generator stream after torch.manual_seed(seed) (group_topk_hook_no_reshape.py:49,
+ * :79, :255) -- concatenated into `out` (dtype ARCTOPK_F32: float, ARCTOPK_BF16: bf16 bit
+ * patterns).  Replaces the reference's per-tensor torch.randn calls (one torch dispatch and
+ * Python round trip each) with one call that runs without the GIL.
+ */
+int arctopk_draw_normal(uint64_t seed, int32_t dtype, int32_t ntensors, const int64_t* sizes,
+                        void* out);
+
 /* library build identification (for smoke tests) */
 const char* arctopk_version(void);
 

@@ -46,6 +46,29 @@ def loop(n):
 
 
 print("no events: host enqueue %.1f us/step, wall %.1f us/step" % loop(50))
+for depth, workers in ((8, 1), (0, 1), (8, 8)):
+    st._proj.close()
+    st._proj.depth, st._proj._workers = depth, workers
+    st._proj.reset()
+    loop(5)
+    print("proj depth %d workers %d: host enqueue %.1f us/step, wall %.1f us/step" % ((depth, workers) + loop(50)))
+# bare launch cost: the encode entry point alone, back to back
+plan = st._plan_for(bks[0])
+sid = torch.cuda.current_stream().cuda_stream
+err = st.error_dict[0]
+torch.cuda.synchronize()
+t = time.perf_counter()
+for _ in range(200):
+    plan.encode(bks[0].buffer(), err, 1, True, plan.V_ring[0], sid)
+t1 = time.perf_counter()
+torch.cuda.synchronize()
+print("bare encode launch %.1f us host, %.1f us wall" % ((t1 - t) / 200 * 1e6, (time.perf_counter() - t) / 200 * 1e6))
+t = time.perf_counter()
+for _ in range(200):
+    plan.select(1, sid)
+t1 = time.perf_counter()
+torch.cuda.synchronize()
+print("bare select launch %.1f us host, %.1f us wall" % ((t1 - t) / 200 * 1e6, (time.perf_counter() - t) / 200 * 1e6))
 st.phase_events = []
 print("events   : host enqueue %.1f us/step, wall %.1f us/step" % loop(50))
 st.phase_events = None

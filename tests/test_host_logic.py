@@ -234,6 +234,44 @@ def test_bf16_projection_tables_match_torch():
     assert seen.all(), "not every table cell was exercised"
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_native_projection_draw_matches_torch(dtype):
+    """libarctopk's one-call projection draw (arctopk_draw_normal) equals per-tensor torch
+    CPU randn from one generator bit for bit (-0 vs +0 included): tensors of < 16 values
+    (scalar Box-Muller with the generator's cached sample carried across tensors), whole
+    16-blocks, recomputed tails, and 4 M values of one tensor."""
+    import ctypes
+    import random
+    from allreducetopk_amd.comm_hooks import projections as PJ
+    assert PJ.native_ok(dtype)
+    iv = torch.int16 if dtype == torch.bfloat16 else torch.int32
+    rng = random.Random(5)
+    cases = [[1 << 22], [2, 16, 8, 3], [4101, 7, 17, 16, 1]]
+    cases += [[rng.choice([1, 2, 3, 5, 8, 12, 15, 16, 17, 33, 72, 100, 4096, 4101])
+               for _ in range(rng.randint(1, 8))] for _ in range(60)]
+    for sizes in cases:
+        seed = rng.randrange(1_000_000_000)
+        g = torch.Generator().manual_seed(seed)
+        ref = torch.cat([torch.randn(n, dtype=dtype, generator=g) for n in sizes])
+        got = torch.empty_like(ref)
+        PJ._draw_native(seed, (ctypes.c_int64 * len(sizes))(*sizes), len(sizes), dtype, got)
+        diff = (got.view(iv) != ref.view(iv)).sum().item()
+        assert diff == 0, f"sizes {sizes[:6]} seed {seed}: {diff} values differ"
+
+
+@pytest.mark.parametrize("seed", [0, 440527571])
+def test_f32_projection_draw_matches_reference_stream(seed):
+    """A bucket's fp32 projections equal the reference's per-tensor torch.randn(m, r)."""
+    for shapes in ([(2048, 2048)] * 3 + [(40, 16), (4, 3, 3, 3)],
+                   [(40, 16), (16, 8, 1, 1), (96, 40), (5461, 33), (10, 2), (7, 3)]):
+        segs = A.segments(shapes, 0.2)
+        ref = torch.cat([v.flatten() for v in A.draw_projections(seed, segs, 4, torch.float32)
+                         if v is not None])
+        ms = [s.m for s in segs if s.kind == A.SKETCH]
+        got = draw_host(seed, ms, 4, torch.float32, pin=False)
+        assert torch.equal(got[:ref.numel()].view(torch.int32), ref.view(torch.int32))
+
+
 @pytest.mark.parametrize("seed", [0, 440527571])
 def test_bf16_projection_draw_matches_reference_stream(seed):
     """A bucket's bf16 projections (fast path and torch fallback) equal the reference's
