@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "mselect.h"
@@ -402,15 +403,14 @@ __global__ void __launch_bounds__(256) k_energy(const SegDev* __restrict__ segs,
 //     number of T-equal keys to take;
 //  4. index-ordered compaction (ties at T: lowest rows first).
 constexpr int kST = 256;
-constexpr int kSTW = kST / 64;
 constexpr int kCandMax = 256;
 
 struct SmallSel {
     uint32_t hist[256];
     __attribute__((aligned(16))) uint32_t cand[kCandMax + 4];
     uint32_t ncand;
-    uint32_t wor[kSTW], wand[kSTW];
-    int64_t wsum[kSTW];
+    uint32_t wor[16], wand[16];  // per wave, up to 1024 threads
+    int64_t wsum[16];
     uint32_t digit, dcount, T;
     int64_t kk, need_eq;
 };
@@ -431,8 +431,8 @@ __device__ __forceinline__ int64_t block_exscan_s(int64_t v, int64_t* wsum) {
     return before;
 }
 
-template <typename T>
-__global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__ segs,
+template <typename T, int NT>
+__global__ void __launch_bounds__(NT) k_select_small(const SegDev* __restrict__ segs,
                                                       const int32_t* __restrict__ seg_ids,
                                                       const T* __restrict__ sketch, int R,
                                                       Scale sc, int32_t* __restrict__ rowlist,
@@ -449,13 +449,13 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
     if (R == 4 && s.kind == ARCTOPK_SEG_SKETCH && (s.sketch_off & 3) == 0) {
         // one quad per row; 8 rows' loads in flight per thread before any use
         constexpr int B = 8;
-        for (int base = 0; base < n; base += kST * B) {
+        for (int base = 0; base < n; base += NT * B) {
             float4 v[B];
 #pragma unroll
-            for (int u = 0; u < B; ++u) v[u] = ldq<T, false>(sk, min(base + u * kST + tid, n - 1));
+            for (int u = 0; u < B; ++u) v[u] = ldq<T, false>(sk, min(base + u * NT + tid, n - 1));
 #pragma unroll
             for (int u = 0; u < B; ++u) {
-                const int row = base + u * kST + tid;
+                const int row = base + u * NT + tid;
                 const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
                 if (row < n) {
                     keys[row] = key;
@@ -465,7 +465,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
             }
         }
     } else {
-        for (int row = tid; row < n; row += kST) {
+        for (int row = tid; row < n; row += NT) {
             const uint32_t key = energy_key(row_energy(sk + (int64_t)row * stride, R, sc, s.kind));
             keys[row] = key;
             kor |= key;
@@ -485,7 +485,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
     kor = 0u;
     kand = ~0u;
 #pragma unroll
-    for (int w = 0; w < kSTW; ++w) {
+    for (int w = 0; w < (NT / 64); ++w) {
         kor |= sh.wor[w];
         kand &= sh.wand[w];
     }
@@ -501,9 +501,9 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
         const int w = bit < 8 ? bit : 8;
         const int shift = bit - w;
         const uint32_t dmask = (1u << w) - 1u;
-        for (int i = tid; i < 256; i += kST) sh.hist[i] = 0;
+        for (int i = tid; i < 256; i += NT) sh.hist[i] = 0;
         __syncthreads();
-        for (int i = tid; i < n; i += kST) {
+        for (int i = tid; i < n; i += NT) {
             const uint32_t key = keys[i];
             if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & dmask], 1u);
         }
@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
             __syncthreads();
             // wave-aggregated append: one LDS atomic per wave and round, not per key
             const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-            for (int b0 = 0; b0 < n; b0 += kST) {
+            for (int b0 = 0; b0 < n; b0 += NT) {
                 const int i = b0 + tid;
                 const uint32_t key = i < n ? keys[i] : 0u;
                 const bool in = i < n && (key & mask) == prefix;
@@ -561,10 +561,10 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
             __syncthreads();
             SEL_STAMP(6);
             const int nc = (int)sh.ncand;
-            for (int i = nc + tid; i < ((nc + 3) & ~3); i += kST) sh.cand[i] = 0u;  // pad to x4
+            for (int i = nc + tid; i < ((nc + 3) & ~3); i += NT) sh.cand[i] = 0u;  // pad to x4
             __syncthreads();
             const uint4* c4 = reinterpret_cast<const uint4*>(sh.cand);
-            for (int t = tid; t < nc; t += kST) {
+            for (int t = tid; t < nc; t += NT) {
                 const uint32_t v = sh.cand[t];
                 int gt = 0, ge = 0;
                 const int nq = (nc + 3) >> 2;
@@ -598,7 +598,7 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
     SEL_STAMP(2);
     // index-ordered compaction over contiguous per-thread row ranges (multiples of 4
     // rows, read as 16-B LDS vectors; the key array is padded to a multiple of 4)
-    const int per = (((n + kST - 1) / kST) + 3) & ~3;
+    const int per = (((n + NT - 1) / NT) + 3) & ~3;
     const int r0 = min(n, tid * per), r1 = min(n, r0 + per);
     int64_t gt = 0, eq = 0;
     for (int i = r0; i < r1; i += 4) {
@@ -645,82 +645,48 @@ __global__ void __launch_bounds__(kST) k_select_small(const SegDev* __restrict__
     SEL_STAMP(4);
 }
 
-// Larger segments: energy keys into global memory plus each segment's key OR / AND
-// (its common leading bits seed the multi-block radix select of mselect.hip).
+// Larger segments: energy keys into global memory, fused with the first radix pass of
+// the multi-block select (mselect.h): each block histograms its keys' top 12 bits in LDS
+// and merges the non-empty bins into the segment's global histogram; the last block to
+// finish picks the bin holding the k-th largest key (ms_arc_first_digit).
 template <typename T>
 __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ segs,
                                                   const int32_t* __restrict__ ids, int first,
                                                   const T* __restrict__ sketch, int R, Scale sc,
                                                   uint32_t* __restrict__ keys, MWorkspace* ws) {
+    __shared__ uint32_t h[kMBins];
     const int t = blockIdx.y;
     const SegDev s = segs[ids[first + t]];
+    for (int i = threadIdx.x; i < kMBins; i += 256) h[i] = 0u;
+    __syncthreads();
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
-    uint32_t kor = 0u, kand = ~0u;
     const int64_t gs = (int64_t)gridDim.x * 256;
     int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const T* sk = sketch + s.sketch_off;
-    if (stride == 4) {  // r = 4: four rows' sketch loads in flight per lane
+    uint32_t* kout = keys + s.row_off;
+    if (stride == 4 && (s.sketch_off & 3) == 0) {  // r = 4: one quad load per row, 4 rows in flight
         for (; row + 3 * gs < s.n; row += 4 * gs) {
-            float v[4][4];
+            float4 v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[u][j] = to_f(sk[(row + u * gs) * 4 + j]);
+            for (int u = 0; u < 4; ++u) v[u] = ldq<T, false>(sk, row + u * gs);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const uint32_t key = energy_key(energy4<T>(v[u][0], v[u][1], v[u][2], v[u][3], sc));
-                keys[s.row_off + row + u * gs] = key;
-                kor |= key;
-                kand &= key;
+                const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
+                kout[row + u * gs] = key;
+                atomicAdd(&h[key >> kArcShift], 1u);
             }
         }
     }
     for (; row < s.n; row += gs) {
         const uint32_t key = energy_key(row_energy(sk + row * stride, R, sc, s.kind));
-        keys[s.row_off + row] = key;
-        kor |= key;
-        kand &= key;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        kor |= __shfl_xor(kor, o, 64);
-        kand &= __shfl_xor(kand, o, 64);
-    }
-    // per-block partials (one memory-side store each: same-line atomics from every block
-    // would serialise); the last block of the segment reduces them and initialises the
-    // segment's select state
-    __shared__ uint32_t s_or[4], s_and[4];
-    if ((threadIdx.x & 63) == 0) {
-        s_or[threadIdx.x >> 6] = kor;
-        s_and[threadIdx.x >> 6] = kand;
+        kout[row] = key;
+        atomicAdd(&h[key >> kArcShift], 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_exchange(&ws->part_or[t][blockIdx.x], s_or[0] | s_or[1] | s_or[2] | s_or[3],
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_exchange(&ws->part_and[t][blockIdx.x], s_and[0] & s_and[1] & s_and[2] & s_and[3],
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int i = threadIdx.x; i < kMBins; i += 256)
+        if (h[i]) atomicAdd(&ws->hist[t][hist_slot(i)], h[i]);
     if (!ms_arrive_last(&ws->done[t].v, gridDim.x)) return;
-    kor = 0u;
-    kand = ~0u;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
-        kor |= ms_take(&ws->part_or[t][i]);
-        kand &= ms_take(&ws->part_and[t][i]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        kor |= __shfl_xor(kor, o, 64);
-        kand &= __shfl_xor(kand, o, 64);
-    }
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) {
-        s_or[threadIdx.x >> 6] = kor;
-        s_and[threadIdx.x >> 6] = kand;
-    }
-    __syncthreads();
-    ms_init_item(ws, t, s.k_rows, s_or[0] | s_or[1] | s_or[2] | s_or[3],
-                 s_and[0] & s_and[1] & s_and[2] & s_and[3]);
+    ms_arc_first_digit(ws, t, s.k_rows);
 }
 
 __device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m >= 256; }
@@ -1189,18 +1155,27 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
                   hipStream_t st) {
     const T* sketch = static_cast<const T*>(sketch_);
     if (p->n_small) {
-        hipLaunchKernelGGL(k_select_small<T>, dim3(p->n_small), dim3(kST), (size_t)p->small_lds, st,
-                           p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
+        // one block per segment: 1024 threads once a segment has more than 4096 rows (the
+        // radix rounds and the compaction are per-block latency chains)
+        if (p->small_lds > 4096 * 4 + 16)
+            hipLaunchKernelGGL((k_select_small<T, 1024>), dim3(p->n_small), dim3(1024), (size_t)p->small_lds,
+                               st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
+        else
+            hipLaunchKernelGGL((k_select_small<T, kST>), dim3(p->n_small), dim3(kST), (size_t)p->small_lds,
+                               st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
     }
     for (int bi = 0; bi < p->n_large_batches; ++bi) {
         const MBatch& b = p->h_large_batches[bi];
         int64_t maxn = 0;
         for (int i = 0; i < b.cnt; ++i) maxn = std::max<int64_t>(maxn, b.it[i].n);
-        const int gx = (int)std::min<int64_t>(kMHistBlocks, (maxn + 1023) / 1024);  // >= 4 rows per lane
+        // >= 32 rows per lane: few blocks per segment keep the global histogram merge
+        // (one memory-side atomic per non-empty bin and block) short
+        int64_t rpb = 8192;  // tuning switch (A/B): rows per block
+        if (const char* env = std::getenv("ARCTOPK_KEYS_ROWS_PER_BLOCK")) rpb = std::max(256, std::atoi(env));
+        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + rpb - 1) / rpb));
         hipLaunchKernelGGL(k_arc_keys<T>, dim3(gx, b.cnt), dim3(256), 0, st, p->d_segs, p->d_large,
                            bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws);
-        int e = ms_select(b, maxn, p->d_keys, nullptr, true, p->d_mws, p->mws_cap, rowlist, nullptr,
-                          slotmap, st);
+        int e = ms_select_arc(b, p->d_keys, p->d_mws, p->mws_cap, rowlist, slotmap, st);
         if (e) return e;
     }
     return (int)hipGetLastError();

@@ -124,6 +124,59 @@ __device__ inline void ms_init_item(MWorkspace* ws, int t, int64_t k, uint32_t k
     }
 }
 
+// ARC first pass, run by the LAST block of the fused key kernel (256 threads) once every
+// block merged its LDS histogram of the keys' top 12 bits (bits 31..20) into
+// ws->hist[t]: read-and-clear the bins (leaving them zero for the next call), find the
+// bin holding the k-th largest key, and start the item in candidate mode on that bin
+// (cand_cap = n for ARC items: every key of the bin fits).
+constexpr int kArcShift = 32 - 12;
+__device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k) {
+    __shared__ uint32_t s_w[4], s_d, s_acc;
+    constexpr int PER = kMBins / 256;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int bin = kMBins - 1 - (tid * PER + q);  // descending
+        c[q] = ms_take(&ws->hist[t][hist_slot(bin)]);
+        sum += c[q];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += s_w[w];
+    const uint64_t excl = (uint64_t)before + incl - sum;
+    if (excl < (uint64_t)k && excl + sum >= (uint64_t)k) {
+        uint64_t acc = excl;
+        int q = 0;
+        for (; q < PER - 1; ++q) {
+            if (acc + c[q] >= (uint64_t)k) break;
+            acc += c[q];
+        }
+        s_d = (uint32_t)(kMBins - 1 - (tid * PER + q));
+        s_acc = (uint32_t)acc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        MState& g = ws->st[t];
+        g.prefix = s_d << kArcShift;
+        g.mask = ~((1u << kArcShift) - 1u);
+        g.bit = kArcShift;
+        g.kk = k - (int64_t)s_acc;
+        g.cand = 1;
+        g.p1 = g.prefix;
+        g.m1 = g.mask;
+        g.ncand = 0;
+        ws->ncand[t].v = 0;
+    }
+}
+
 // host-side geometry of one item: fills range / nranges / cand_cap (cand_off by caller)
 void ms_item_geometry(MItem& it);
 // workspace bytes for batches whose candidate capacities sum to <= cap_total
@@ -138,5 +191,12 @@ int64_t ms_workspace_bytes(int64_t cap_total);
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* x, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, float* out_val,
               int32_t* out_slot, hipStream_t st);
+
+// ARC selection after the fused key kernel (keys + first-pass histogram + digit, every
+// item in candidate mode): compact the bin's keys -> one block per item fixes the
+// remaining bits from the candidates in LDS and computes the per-range offsets -> write
+// the ascending row list and slot map.  Three launches per batch.
+int ms_select_arc(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+                  int32_t* out_idx, int32_t* out_slot, hipStream_t st);
 
 }  // namespace arctopk

@@ -394,6 +394,104 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
     }
 }
 
+// ARC, after compact: one 1024-thread block per item.  The candidates (every key of the
+// first-pass bin, with its index) are few and hot in L2: the block fixes the remaining
+// 20 bits in two 10-bit LDS histogram rounds, then counts the candidates above / equal to
+// the threshold per range and turns the counts into per-range T-equal allowances (lowest
+// ranges first) and output offsets, as k_ms_count's last block does.
+constexpr int kRefineThreads = 1024;
+constexpr int kRefineU = 8;  // candidates per thread in flight
+static_assert(kRefineThreads == kMMaxRanges, "one range per thread in the offset scan");
+
+__global__ void __launch_bounds__(kRefineThreads) k_ms_refine(MBatch b, MWorkspace* ws,
+                                                              const uint32_t* __restrict__ ckey,
+                                                              const uint32_t* __restrict__ cidx) {
+    constexpr int NW = kRefineThreads / 64;
+    __shared__ uint32_t h[1 << kW2];
+    __shared__ uint32_t cgt[kMMaxRanges], ceq[kMMaxRanges];
+    __shared__ uint32_t lds[NW], s_digit, s_acc;
+    const int t = blockIdx.x;
+    const int tid = threadIdx.x;
+    const MItem it = b.it[t];
+    MState s = ws->st[t];
+    const int64_t nc = (int64_t)ws->ncand[t].v;
+    const uint32_t* ck = ckey + it.cand_off;
+    const uint32_t* ci = cidx + it.cand_off;
+    while (s.bit > 0) {
+        const int w = s.bit < kW2 ? s.bit : kW2;
+        const int shift = s.bit - w;
+        const uint32_t dmask = (1u << w) - 1u;
+        h[tid] = 0u;  // 1 << kW2 == kRefineThreads bins
+        __syncthreads();
+        for (int64_t base = 0; base < nc; base += (int64_t)kRefineThreads * kRefineU) {
+            uint32_t kv[kRefineU];  // all loads of a batch in flight before the LDS atomics
+#pragma unroll
+            for (int u = 0; u < kRefineU; ++u) {
+                const int64_t i = base + u * kRefineThreads + tid;
+                kv[u] = i < nc ? ck[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kRefineU; ++u) {
+                const int64_t i = base + u * kRefineThreads + tid;
+                if (i < nc && (kv[u] & s.mask) == s.prefix) atomicAdd(&h[(kv[u] >> shift) & dmask], 1u);
+            }
+        }
+        __syncthreads();
+        const int nb = 1 << w;
+        const uint32_t c = tid < nb ? h[nb - 1 - tid] : 0u;  // descending bins
+        uint32_t total;
+        const uint32_t excl = block_exscan_u32<NW>(c, lds, &total);
+        if ((uint64_t)excl < (uint64_t)s.kk && (uint64_t)excl + c >= (uint64_t)s.kk) {
+            s_digit = (uint32_t)(nb - 1 - tid);
+            s_acc = excl;
+        }
+        __syncthreads();
+        s.prefix |= s_digit << shift;
+        s.mask |= dmask << shift;
+        s.kk -= (int64_t)s_acc;
+        s.bit = shift;
+        __syncthreads();  // s_digit / s_acc / h are rewritten by the next round
+    }
+    const uint32_t T = s.prefix;
+    const int nr = it.nranges;
+    for (int r = tid; r < kMMaxRanges; r += kRefineThreads) {
+        cgt[r] = 0u;
+        ceq[r] = 0u;
+    }
+    __syncthreads();
+    for (int64_t base = 0; base < nc; base += (int64_t)kRefineThreads * kRefineU) {
+        uint32_t kv[kRefineU], iv[kRefineU];
+#pragma unroll
+        for (int u = 0; u < kRefineU; ++u) {
+            const int64_t i = base + u * kRefineThreads + tid;
+            kv[u] = i < nc ? ck[i] : 0u;
+            iv[u] = i < nc ? ci[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kRefineU; ++u) {
+            const int64_t i = base + u * kRefineThreads + tid;
+            if (i < nc && kv[u] >= T) {
+                const int r = (int)(iv[u] / (uint32_t)it.range);
+                atomicAdd(kv[u] > T ? &cgt[r] : &ceq[r], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    const int r = tid;
+    const uint32_t eq = r < nr ? ceq[r] : 0u;
+    const uint32_t gt = r < nr ? ws->cnt_gt[t][r] + cgt[r] : 0u;  // + keys above the bin
+    uint32_t tot;
+    const uint32_t eq_before = block_exscan_u32<NW>(eq, lds, &tot);
+    int64_t take = s.kk - (int64_t)eq_before;
+    take = take < 0 ? 0 : (take > (int64_t)eq ? (int64_t)eq : take);
+    const uint32_t sel_before = block_exscan_u32<NW>(gt + (uint32_t)take, lds, &tot);
+    if (r < nr) {
+        ws->take_eq[t][r] = (uint32_t)take;
+        ws->sel_before[t][r] = sel_before;
+    }
+    if (tid == 0) ws->st[t] = s;  // the write pass reads the threshold (prefix)
+}
+
 }  // namespace
 
 void ms_item_geometry(MItem& it) {
@@ -443,6 +541,28 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
     else
         MS_LAUNCH(true, false);
 #undef MS_LAUNCH
+    return (int)hipGetLastError();
+}
+
+int ms_select_arc(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+                  int32_t* out_idx, int32_t* out_slot, hipStream_t st) {
+    const int cnt = b.cnt;
+    if (cnt < 1) return 0;
+    int gr = 1;
+    for (int i = 0; i < cnt; ++i) {
+        const MItem& it = b.it[i];
+        if (it.nranges < 1 || it.nranges > kMMaxRanges || it.cand_off < 0 || it.cand_cap < it.n ||
+            it.cand_off + it.cand_cap > cap_total || (int64_t)it.range * it.nranges < it.n)
+            return 1001;  // ARCTOPK_EINVAL: ARC items need cand_cap >= n
+        gr = std::max(gr, it.nranges);
+    }
+    uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
+    uint32_t* cidx = ckey + cap_total;
+    const dim3 gt(gr, cnt);
+    hipLaunchKernelGGL(k_ms_compact<false>, gt, dim3(256), 0, st, b, keys, nullptr, ws, ckey, cidx);
+    hipLaunchKernelGGL(k_ms_refine, dim3(cnt), dim3(kRefineThreads), 0, st, b, ws, ckey, cidx);
+    hipLaunchKernelGGL((k_ms_write<false, true>), gt, dim3(256), 0, st, b, keys, nullptr, ws, out_idx,
+                       nullptr, out_slot);
     return (int)hipGetLastError();
 }
 

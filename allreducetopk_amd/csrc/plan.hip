@@ -266,6 +266,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 it.out_off = sg.sel_off;
                 it.slot_off = sg.row_off;
                 ms_item_geometry(it);
+                it.cand_cap = it.n;  // ARC: every key of the first-pass bin is a candidate
                 it.cand_off = cap;
                 cap += it.cand_cap;
             }
