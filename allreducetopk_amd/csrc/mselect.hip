@@ -401,6 +401,7 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
 // ranges first) and output offsets, as k_ms_count's last block does.
 constexpr int kRefineThreads = 1024;
 constexpr int kRefineU = 8;  // candidates per thread in flight
+constexpr int kRefineLdsCap = 12288;  // candidate keys staged in LDS (48 KiB, + ~12 KiB static)
 static_assert(kRefineThreads == kMMaxRanges, "one range per thread in the offset scan");
 
 __global__ void __launch_bounds__(kRefineThreads) k_ms_refine(MBatch b, MWorkspace* ws,
@@ -417,6 +418,24 @@ __global__ void __launch_bounds__(kRefineThreads) k_ms_refine(MBatch b, MWorkspa
     const int64_t nc = (int64_t)ws->ncand[t].v;
     const uint32_t* ck = ckey + it.cand_off;
     const uint32_t* ci = cidx + it.cand_off;
+    if (nc <= kRefineLdsCap) {  // usual case: stage the candidate keys in LDS, one round trip
+        extern __shared__ uint32_t stage[];
+        for (int64_t base = 0; base < nc; base += (int64_t)kRefineThreads * kRefineU) {
+            uint32_t kv[kRefineU];
+#pragma unroll
+            for (int u = 0; u < kRefineU; ++u) {
+                const int64_t i = base + u * kRefineThreads + tid;
+                kv[u] = i < nc ? ck[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kRefineU; ++u) {
+                const int64_t i = base + u * kRefineThreads + tid;
+                if (i < nc) stage[i] = kv[u];
+            }
+        }
+        __syncthreads();
+        ck = stage;  // a flat pointer into LDS from here on
+    }
     while (s.bit > 0) {
         const int w = s.bit < kW2 ? s.bit : kW2;
         const int shift = s.bit - w;
@@ -465,14 +484,33 @@ __global__ void __launch_bounds__(kRefineThreads) k_ms_refine(MBatch b, MWorkspa
         for (int u = 0; u < kRefineU; ++u) {
             const int64_t i = base + u * kRefineThreads + tid;
             kv[u] = i < nc ? ck[i] : 0u;
-            iv[u] = i < nc ? ci[i] : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < kRefineU; ++u) {
+        for (int u = 0; u < kRefineU; ++u) {  // indices only of the keys that count
             const int64_t i = base + u * kRefineThreads + tid;
-            if (i < nc && kv[u] >= T) {
-                const int r = (int)(iv[u] / (uint32_t)it.range);
-                atomicAdd(kv[u] > T ? &cgt[r] : &ceq[r], 1u);
+            iv[u] = (i < nc && kv[u] >= T) ? ci[i] : 0u;
+        }
+        const int lane = tid & 63;
+#pragma unroll
+        for (int u = 0; u < kRefineU; ++u) {
+            // segmented wave reduction: a wave's 64 consecutive candidates come from one or
+            // two block tiles of the compact pass, so one LDS atomic pair per distinct range
+            const int64_t i = base + u * kRefineThreads + tid;
+            const bool valid = i < nc && kv[u] >= T;
+            const int r = valid ? (int)(iv[u] / (uint32_t)it.range) : -1;
+            const bool gt = valid && kv[u] > T;
+            uint64_t pending = __ballot(valid);
+            while (pending) {
+                const int leader = __ffsll((long long)pending) - 1;
+                const int rl = __shfl(r, leader, 64);
+                const bool mine = valid && r == rl;
+                const uint32_t ng = popc64(__ballot(mine && gt));
+                const uint32_t ne = popc64(__ballot(mine && !gt));
+                if (lane == leader) {
+                    if (ng) atomicAdd(&cgt[rl], ng);
+                    if (ne) atomicAdd(&ceq[rl], ne);
+                }
+                pending &= ~__ballot(mine);
             }
         }
     }
@@ -560,7 +598,8 @@ int ms_select_arc(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t
     uint32_t* cidx = ckey + cap_total;
     const dim3 gt(gr, cnt);
     hipLaunchKernelGGL(k_ms_compact<false>, gt, dim3(256), 0, st, b, keys, nullptr, ws, ckey, cidx);
-    hipLaunchKernelGGL(k_ms_refine, dim3(cnt), dim3(kRefineThreads), 0, st, b, ws, ckey, cidx);
+    hipLaunchKernelGGL(k_ms_refine, dim3(cnt), dim3(kRefineThreads), (size_t)kRefineLdsCap * 4, st, b, ws,
+                       ckey, cidx);
     hipLaunchKernelGGL((k_ms_write<false, true>), gt, dim3(256), 0, st, b, keys, nullptr, ws, out_idx,
                        nullptr, out_slot);
     return (int)hipGetLastError();
