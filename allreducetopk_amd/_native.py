@@ -73,6 +73,17 @@ _SIGS = {
     "arctopk_ef_apply": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
     "arctopk_draw_bf16_normal": (c_int32, [c_uint64, c_int64, c_void_p]),
     "arctopk_draw_normal": (c_int32, [c_uint64, c_int32, c_int32, POINTER(c_int64), c_void_p]),
+    "arctopk_draw_pool_create": (c_int32, [c_int32, POINTER(c_void_p)]),
+    "arctopk_draw_pool_destroy": (c_int32, [c_void_p]),
+    "arctopk_draw_submit": (c_int64, [c_void_p, c_uint64, c_int32, c_int32, POINTER(c_int64), c_void_p]),
+    "arctopk_draw_wait": (c_int32, [c_void_p, c_int64]),
+    "arctopk_draw_poll": (c_int32, [c_void_p, c_int64]),
+    "arctopk_memcpy_h2d_async": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "arctopk_event_create": (c_int32, [POINTER(c_void_p)]),
+    "arctopk_event_destroy": (c_int32, [c_void_p]),
+    "arctopk_event_record": (c_int32, [c_void_p, c_void_p]),
+    "arctopk_event_wait": (c_int32, [c_void_p, c_void_p]),
+    "arctopk_event_query": (c_int32, [c_void_p]),
     "arctopk_version": (c_char_p, []),
 }
 
@@ -120,3 +131,37 @@ def i64_array(values):
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+class DeviceEvent:
+    """A device-scope HIP event (libarctopk's arctopk_event_*): ordering between this
+    process's streams on one GPU without torch's system-scope release."""
+
+    __slots__ = ("handle",)
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        check(lib().arctopk_event_create(ctypes.byref(h)), "arctopk_event_create")
+        self.handle = h.value
+
+    def record(self, stream: int) -> None:
+        check(lib().arctopk_event_record(self.handle, stream), "arctopk_event_record")
+
+    def wait(self, stream: int) -> None:
+        """Make `stream` wait for the last record."""
+        check(lib().arctopk_event_wait(stream, self.handle), "arctopk_event_wait")
+
+    def query(self) -> bool:
+        st = lib().arctopk_event_query(self.handle)
+        if st not in (0, 1):
+            check(st, "arctopk_event_query")
+        return st == 0
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _lib is not None:
+            try:
+                _lib.arctopk_event_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self.handle = None

@@ -30,7 +30,10 @@ device-aware: ``wait()`` makes the waiting stream wait for the decode, as DDP's
 finalize does, so the next bucket's encode overlaps this bucket's exchange.
 """
 
+import collections
 import logging
+import os
+import time
 from typing import Dict, List, Tuple
 
 import torch
@@ -102,18 +105,19 @@ class BucketPlan:
         self.packed = torch.zeros(max(1, info.packed_len), dtype=dtype, device=dev)
         self.rowlist = torch.empty(max(1, info.sel_rows), dtype=torch.int32, device=dev)
         self.slotmap = torch.empty(max(1, info.rows_total), dtype=torch.int32, device=dev)
-        # projections: a ring of device slots filled by H2D copies on a side stream, so the
-        # copy for call i+1 overlaps call i's kernels instead of sitting between them
+        # projections: device slots filled by H2D copies on a side stream, so the copy for a
+        # call overlaps the kernels before it.  A slot is reused (least recently used first)
+        # only once the host sees its last reader complete; otherwise another slot is
+        # added: the copy stream never waits for the caller's stream (such a wait makes
+        # hipMemcpyAsync block the host until that stream drains, starving the GPU).
         self.V_ring = [torch.empty(max(1, info.v_len), dtype=dtype, device=dev)
                        for _ in range(self.V_RING)]
-        # events are created once and re-recorded (a wait captures the latest record):
-        # _v_used[i] follows the encode that last read slot i, _v_ready[i] its H2D copy
-        self._v_used = [None] * self.V_RING
-        self._v_ready = [None] * self.V_RING
-        self._v_live = [False] * self.V_RING
-        self.decode_done = None  # recorded after this bucket's side-stream decode
+        self._v_used = [None] * self.V_RING    # event after the encode that last read slot i
+        self._v_ready = [None] * self.V_RING   # event after slot i's H2D copy
+        self._v_live = [False] * self.V_RING   # _v_used[i] is pending or done
         self._v_streams = [None] * self.V_RING
-        self._v_next = 0
+        self._v_order = collections.deque(range(self.V_RING))  # least recently used first
+        self.decode_done = None  # recorded after this bucket's side-stream decode
         self.groups = self._make_groups()
         bits = dtype_bits(dtype)
         # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
@@ -122,22 +126,45 @@ class BucketPlan:
 
     PIPELINE_GROUPS = 4             # packed all-reduce split into up to this many pieces
     PIPELINE_MIN_BYTES = 4 << 20    # ... each at least this large (RCCL efficiency)
-    V_RING = 3                      # projection slots in flight per bucket
+    V_RING = 4        # projection slots allocated up front per bucket
+    V_RING_MAX = 32   # ... and at most (then the copy stream waits for the oldest reader)
+
+    def _take_v_slot(self, copy_stream) -> int:
+        order = self._v_order
+        i = order[0]
+        if self._v_live[i] and not self._v_used[i].query():  # LRU slot still being read
+            if len(self.V_ring) < self.V_RING_MAX:
+                i = len(self.V_ring)
+                self.V_ring.append(torch.empty_like(self.V_ring[0]))
+                self._v_used.append(None)
+                self._v_ready.append(None)
+                self._v_live.append(False)
+                self._v_streams.append(None)
+                order.append(i)
+                return i
+            copy_stream.wait_event(self._v_used[i])
+        order.rotate(-1)
+        self._v_live[i] = False
+        return i
 
     def stage_projection(self, host: torch.Tensor, copy_stream, stream):
         """Copy this call's projections `host` (pinned) into the next ring slot on
         `copy_stream`; `stream` waits for the copy.  Returns (slot index, device buffer)."""
-        i = self._v_next
-        self._v_next = (i + 1) % len(self.V_ring)
+        i = self._take_v_slot(copy_stream) if copy_stream is not stream else 0
         buf = self.V_ring[i]
+        n = int(self.info.v_len)
+        nbytes = n * buf.element_size()
+        _ht("stage_pre")
+        if copy_stream is stream:  # in order on the caller's stream: no cross-stream events
+            N.check(N.lib().arctopk_memcpy_h2d_async(buf.data_ptr(), host.data_ptr(), nbytes,
+                                                     stream.cuda_stream), "arctopk_memcpy_h2d_async")
+            self._v_live[i] = False
+            return i, buf
         if self._v_streams[i] is not copy_stream:  # allocator: the slot is also used there
             buf.record_stream(copy_stream)
             self._v_streams[i] = copy_stream
-        if self._v_live[i]:  # the encode that read this slot must be done
-            copy_stream.wait_event(self._v_used[i])
-        n = int(self.info.v_len)
-        with torch.cuda.stream(copy_stream):
-            buf[:n].copy_(host[:n], non_blocking=True)
+        N.check(N.lib().arctopk_memcpy_h2d_async(buf.data_ptr(), host.data_ptr(), nbytes,
+                                                 copy_stream.cuda_stream), "arctopk_memcpy_h2d_async")
         if self._v_ready[i] is None:
             self._v_ready[i] = torch.cuda.Event()
             self._v_used[i] = torch.cuda.Event()
@@ -146,6 +173,8 @@ class BucketPlan:
         return i, buf
 
     def projection_consumed(self, i: int, stream) -> None:
+        if self._v_used[i] is None:  # the slot was filled on the caller's stream
+            return
         self._v_used[i].record(stream)
         self._v_live[i] = True
 
@@ -260,6 +289,8 @@ class GroupTopKState(HookState):
         # bucket's encode runs while this one is on the wire; sketches use a second
         # communicator so they never queue behind a packed all-reduce
         self.async_exchange = True
+        # projection H2D on a copy stream (event-ordered) or in order on the caller's stream
+        self.v_copy_side_stream = os.environ.get("ARCTOPK_V_COPY", "side") != "main"
         self._copy_streams: Dict[int, torch.cuda.Stream] = {}
         self._decode_streams: Dict[int, torch.cuda.Stream] = {}
         self._pending: Dict[int, torch.cuda.Event] = {}  # bucket -> its decode-done event
@@ -291,15 +322,21 @@ class GroupTopKState(HookState):
 
     def _plan_for(self, bucket) -> BucketPlan:
         buf = bucket.buffer()
+        # fast path: the bucket's flat buffer is the one this plan was built for (DDP keeps a
+        # bucket's buffer across iterations; a bucket rebuild allocates new buffers)
+        ident = (buf.data_ptr(), buf.numel(), buf.dtype, self.r, float(self.compress_ratio))
+        hit = self._plans.get(bucket.index())
+        if hit is not None and hit[2] == ident:
+            return hit[1]
         grads = bucket.gradients()
         shapes = [tuple(g.shape) for g in grads]
         key = (tuple(shapes), buf.dtype, buf.device, self.r, float(self.compress_ratio))
-        hit = self._plans.get(bucket.index())
         if hit is not None and hit[0] == key:
+            self._plans[bucket.index()] = (key, hit[1], ident)
             return hit[1]
         _check_bucket_layout(buf, grads)
         plan = BucketPlan(shapes, self.r, self.compress_ratio, buf.dtype, buf.device)
-        self._plans[bucket.index()] = (key, plan)
+        self._plans[bucket.index()] = (key, plan, ident)
         return plan
 
     def _upcoming_ms(self, bucket) -> List[Tuple[int, ...]]:
@@ -320,6 +357,19 @@ class GroupTopKState(HookState):
 
 
 _RESEED_FAST = None
+
+# optional host-time breakdown of the hook (diagnostics; ARCTOPK_HOST_TIMING=1)
+HOST_TIMES = {} if os.environ.get("ARCTOPK_HOST_TIMING") == "1" else None
+_ht_last = [0.0]
+
+
+def _ht(name=None):
+    if HOST_TIMES is None:
+        return
+    t = time.perf_counter()
+    if name is not None:
+        HOST_TIMES[name] = HOST_TIMES.get(name, 0.0) + (t - _ht_last[0])
+    _ht_last[0] = t
 
 
 def _reseed_global(seed: int) -> None:
@@ -442,8 +492,10 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                            "residual was created")
 
     # per-call projection seed, and the reference's global reseed side effect (:254-255)
+    _ht()
     seed = state._proj.consume_seed(state.rng)
     _reseed_global(seed)
+    _ht("seed")
 
     plan = state._plan_for(bucket)
     dev = input_tensor.device
@@ -453,15 +505,20 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     if pend is not None:  # this bucket's previous decode (side stream) must be done
         stream.wait_event(pend)
     dtype = input_tensor.dtype
+    _ht("plan+pending")
     slot = state._proj.get(seed, plan.ms, dtype)
+    _ht("proj_get")
     vslot, V = -1, plan.V_ring[0]
     if plan.info.v_len:  # 512 KiB pinned H2D at headline, on a side stream, ahead of encode
-        cs = state._side_stream(state._copy_streams, dev)
+        cs = state._side_stream(state._copy_streams, dev) if state.v_copy_side_stream else stream
         vslot, V = plan.stage_projection(slot.host, cs, stream)
+        _ht("stage_copy")
         state._proj.release(slot, cs)  # refilled only after this copy completed
     else:
         state._proj.release(slot)
+    _ht("stage_v")
     state._proj.prefetch(state._upcoming_ms(bucket), dtype)
+    _ht("prefetch")
 
     evs = None
     if state.phase_events is not None:
@@ -477,9 +534,12 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             evs[name] = e
 
     mark("start")
+    _ht("events")
     plan.encode(input_tensor, err, ef, err_in, V, sid)
+    _ht("encode")
     if vslot >= 0:
         plan.projection_consumed(vslot, stream)
+    _ht("consumed")
     mark("encode")
 
     overlap = world_size > 1 and state.async_exchange and not state.host_staged
@@ -489,6 +549,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     mark("sketch_allreduce")
     plan.select(world_size, sid)
     mark("select")
+    _ht("select")
     state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum
     if overlap:
         # pack group g, start its all-reduce (RCCL stream), pack g+1 ...; decode runs on a
@@ -535,6 +596,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         return fut
     plan.pack(input_tensor, err, ef, sid)
     mark("pack")
+    _ht("pack")
     if state.host_staged:  # D2H to a pinned "NIC buffer" and back (NIC model)
         _stage_through_host(state, plan.packed_view, stream, dev)
         mark("h2d")
@@ -543,8 +605,10 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     mark("packed_allreduce")
     plan.decode(world_size, ef, gerr, input_tensor, sid)
     mark("decode")
+    _ht("decode")
 
     state.maybe_increase_iter(bucket)
     fut = torch.futures.Future()
     fut.set_result(input_tensor)
+    _ht("tail")
     return fut

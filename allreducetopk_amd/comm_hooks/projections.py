@@ -26,8 +26,8 @@ from __future__ import annotations
 import collections
 import ctypes
 import logging
+import os
 import threading
-from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, Optional, Sequence, Tuple
 
 import torch
@@ -148,7 +148,14 @@ class Slot:
         self.event = None      # reused event: recorded after an async copy out of `host`
         self.pending = False   # ... and that copy may still be running
 
+    def copy_done(self) -> bool:
+        """Whether the last H2D copy out of this buffer has completed (non-blocking)."""
+        if self.pending and self.event.query():
+            self.pending = False
+        return not self.pending
+
     def fill(self, seed: int):
+        """Draw on the calling thread."""
         if self.pending:  # the previous H2D copy from this buffer must be done
             self.event.synchronize()
             self.pending = False
@@ -166,17 +173,20 @@ class ProjectionSource:
 
     ``get`` returns a filled :class:`Slot`; the caller copies ``slot.host`` to the device
     and hands the slot back with :meth:`release` (recording the copy's stream, so the
-    buffer is refilled only after that copy completed).
+    buffer is refilled only after that copy completed).  Prefetched draws run on
+    libarctopk's native thread pool (``arctopk_draw_submit`` / ``_wait``): no Python
+    thread competes with the hook's thread for the GIL.
     """
 
-    def __init__(self, r: int, depth: int = 8, workers: int = 8):
+    def __init__(self, r: int, depth: int = 8,
+                 workers: int = int(os.environ.get("ARCTOPK_DRAW_THREADS", "4"))):
         self.r = r
         self.depth = depth
-        self._pool: Optional[ThreadPoolExecutor] = None
+        self._pool = None  # native draw pool handle, created on first prefetch
         self._workers = workers
-        self._pending: Dict[Tuple, object] = {}
+        self._pending: Dict[Tuple, Tuple[int, Slot]] = {}  # (seed, ms, dtype) -> (ticket, slot)
+        self._stale: list = []  # (ticket, slot) of predictions that did not come true
         self._free: Dict[Tuple, list] = collections.defaultdict(list)
-        self._lock = threading.Lock()
         self._lookahead: Optional[torch.Generator] = None
         self._future_seeds: collections.deque = collections.deque()
         self.hits = 0
@@ -208,11 +218,12 @@ class ProjectionSource:
 
     # -- slots --------------------------------------------------------------
     def _slot(self, ms: Tuple[int, ...], dtype: torch.dtype) -> Slot:
+        """A free slot whose last H2D copy has completed, or a new one."""
         key = (tuple(ms), dtype)
-        with self._lock:
-            free = self._free[key]
-            if free:
-                return free.pop()
+        free = self._free[key]
+        for i in range(len(free) - 1, -1, -1):
+            if free[i].copy_done():
+                return free.pop(i)
         return Slot(key, ms, self.r, dtype, pin=torch.cuda.is_available())
 
     def release(self, slot: Slot, stream=None):
@@ -222,53 +233,83 @@ class ProjectionSource:
                 slot.event = torch.cuda.Event()
             slot.event.record(stream)
             slot.pending = True
-        with self._lock:
-            self._free[slot.key].append(slot)
+        self._free[slot.key].append(slot)
 
     # -- drawing ------------------------------------------------------------
+    def _native_pool(self):
+        if self._pool is None:
+            from allreducetopk_amd import _native as N
+            h = ctypes.c_void_p()
+            N.check(N.lib().arctopk_draw_pool_create(self._workers, ctypes.byref(h)),
+                    "arctopk_draw_pool_create")
+            self._pool = h.value
+        return self._pool
+
     def get(self, seed: int, ms: Tuple[int, ...], dtype: torch.dtype) -> Slot:
-        key = (seed, ms, dtype)
-        with self._lock:
-            fut = self._pending.pop(key, None)
-        if fut is not None:
+        ent = self._pending.pop((seed, ms, dtype), None)
+        if ent is not None:
+            from allreducetopk_amd import _native as N
+            ticket, slot = ent
+            N.check(N.lib().arctopk_draw_wait(self._pool, ticket), "arctopk_draw_wait")
             self.hits += 1
-            return fut.result()
+            return slot
         self.misses += 1
         return self._slot(ms, dtype).fill(seed)
 
+    def _reap_stale(self):
+        from allreducetopk_amd import _native as N
+        keep = []
+        for ticket, slot in self._stale:
+            if N.lib().arctopk_draw_poll(self._pool, ticket) == 1:
+                self.release(slot)
+            else:
+                keep.append((ticket, slot))
+        self._stale = keep
+
     def prefetch(self, upcoming_ms: Sequence[Tuple[int, ...]], dtype: torch.dtype):
         """Schedule the projections of the next ``len(upcoming_ms)`` calls."""
-        if self.depth <= 0 or not upcoming_ms:
-            return
+        if self.depth <= 0 or not upcoming_ms or not native_ok(dtype):
+            return  # (torch fallback draws: synchronously in get())
+        from allreducetopk_amd import _native as N
+        if self._stale:
+            self._reap_stale()
         seeds = self._peek_seeds(min(self.depth, len(upcoming_ms)))
-        stale = []
-        with self._lock:
-            live = set()
-            for seed, ms in zip(seeds, upcoming_ms):
-                if sum(ms) * self.r < SYNC_MAX_VALUES:  # drawn by get() on the caller's thread
-                    continue
-                key = (seed, ms, dtype)
-                live.add(key)
-                if self._pool is None:
-                    self._pool = ThreadPoolExecutor(max_workers=self._workers,
-                                                    thread_name_prefix="arctopk-proj")
-                if key not in self._pending:
-                    self._pending[key] = self._pool.submit(
-                        lambda sd=seed, m_=ms: self._slot(m_, dtype).fill(sd))
-            for key in [k for k in self._pending if k not in live]:  # stale predictions
-                stale.append(self._pending.pop(key))
-        for fut in stale:  # recycle their slots once drawn
-            fut.add_done_callback(lambda f: self.release(f.result()) if not f.cancelled()
-                                  and f.exception() is None else None)
+        live = set()
+        for seed, ms in zip(seeds, upcoming_ms):
+            if sum(ms) * self.r < SYNC_MAX_VALUES:  # drawn by get() on the caller's thread
+                continue
+            key = (seed, ms, dtype)
+            live.add(key)
+            if key not in self._pending:
+                slot = self._slot(ms, dtype)
+                ticket = N.lib().arctopk_draw_submit(self._native_pool(), int(seed),
+                                                     N.DTYPE_CODE[dtype], slot.n, slot.sizes,
+                                                     slot.host.data_ptr())
+                if ticket < 0:
+                    N.check(-ticket, "arctopk_draw_submit")
+                self._pending[key] = (ticket, slot)
+        for key in [k for k in self._pending if k not in live]:  # stale predictions
+            self._stale.append(self._pending.pop(key))
 
     def reset(self):
         """Forget the seed look-ahead and pending draws (the rng was repositioned)."""
-        with self._lock:
-            self._pending.clear()
+        self._stale.extend(self._pending.values())
+        self._pending.clear()
         self._lookahead = None
         self._future_seeds.clear()
 
     def close(self):
-        if self._pool is not None:
-            self._pool.shutdown(wait=False, cancel_futures=True)
-            self._pool = None
+        """Stop the native pool (queued draws are dropped, running ones finish)."""
+        pool, self._pool = self._pool, None
+        if pool is not None:
+            from allreducetopk_amd import _native as N
+            if N._lib is not None:
+                N._lib.arctopk_draw_pool_destroy(pool)
+        self._pending.clear()
+        self._stale.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass

@@ -332,6 +332,36 @@ extern "C" int arctopk_plan_segment(const arctopk_plan* p, int32_t i, arctopk_se
     return 0;
 }
 
+extern "C" int arctopk_event_create(void** event) {
+    if (!event) return ARCTOPK_EINVAL;
+    hipEvent_t e = nullptr;
+    const hipError_t st = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice);
+    *event = st == hipSuccess ? (void*)e : nullptr;
+    return (int)st;
+}
+
+extern "C" int arctopk_event_destroy(void* event) {
+    return event ? (int)hipEventDestroy((hipEvent_t)event) : 0;
+}
+
+extern "C" int arctopk_event_record(void* event, void* stream) {
+    if (!event) return ARCTOPK_EINVAL;
+    return (int)hipEventRecord((hipEvent_t)event, (hipStream_t)stream);
+}
+
+extern "C" int arctopk_event_wait(void* stream, void* event) {
+    if (!event) return ARCTOPK_EINVAL;
+    return (int)hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0);
+}
+
+extern "C" int arctopk_event_query(void* event) {
+    if (!event) return ARCTOPK_EINVAL;
+    const hipError_t st = hipEventQuery((hipEvent_t)event);
+    if (st == hipSuccess) return 0;
+    if (st == hipErrorNotReady) return 1;
+    return (int)st;
+}
+
 extern "C" const char* arctopk_version(void) {
     return "libarctopk 0.1 gfx950 (ARC-TopK encode/select/pack/decode, TopK/RandK)";
 }

@@ -24,9 +24,16 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
 
 #include <immintrin.h>
+
+#include <hip/hip_runtime.h>
 
 #include "arctopk.h"
 
@@ -367,4 +374,115 @@ extern "C" int arctopk_draw_bf16_normal(uint64_t seed, int64_t total, uint16_t* 
     Gen g(seed);
     if (total) draw_bf16(g, total, out);
     return 0;
+}
+
+// ---- background draws -------------------------------------------------------------------
+// The projections of the next calls are drawn ahead on native threads: no Python thread
+// holds or waits for the GIL while the hook's thread enqueues kernels.
+namespace {
+
+struct DrawTask {
+    int64_t ticket;
+    uint64_t seed;
+    int32_t dtype;
+    std::vector<int64_t> sizes;
+    void* out;
+};
+
+struct DrawPool {
+    std::mutex mu;
+    std::condition_variable cv_task, cv_done;
+    std::deque<DrawTask> queue;
+    std::unordered_map<int64_t, int> done;  // ticket -> status, until waited / polled
+    std::vector<std::thread> threads;
+    int64_t next_ticket = 1;
+    bool stop = false;
+
+    void run() {
+        for (;;) {
+            DrawTask t;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_task.wait(lk, [&] { return stop || !queue.empty(); });
+                if (stop) return;  // queued draws are dropped: their buffers are the caller's
+                t = std::move(queue.front());
+                queue.pop_front();
+            }
+            const int rc = arctopk_draw_normal(t.seed, t.dtype, (int32_t)t.sizes.size(), t.sizes.data(), t.out);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                done[t.ticket] = rc;
+            }
+            cv_done.notify_all();
+        }
+    }
+};
+
+}  // namespace
+
+extern "C" int arctopk_draw_pool_create(int32_t nthreads, void** pool) {
+    if (!pool || nthreads < 1 || nthreads > 64) return ARCTOPK_EINVAL;
+    DrawPool* p = new DrawPool;
+    for (int i = 0; i < nthreads; ++i) p->threads.emplace_back([p] { p->run(); });
+    *pool = p;
+    return 0;
+}
+
+extern "C" int arctopk_draw_pool_destroy(void* pool) {
+    if (!pool) return 0;
+    DrawPool* p = static_cast<DrawPool*>(pool);
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        p->stop = true;
+        p->queue.clear();
+    }
+    p->cv_task.notify_all();
+    for (std::thread& t : p->threads) t.join();  // running draws finish first
+    delete p;
+    return 0;
+}
+
+extern "C" int64_t arctopk_draw_submit(void* pool, uint64_t seed, int32_t dtype, int32_t ntensors,
+                                       const int64_t* sizes, void* out) {
+    if (!pool || ntensors < 0 || (ntensors > 0 && (!sizes || !out))) return -ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return -ARCTOPK_EINVAL;
+    DrawPool* p = static_cast<DrawPool*>(pool);
+    DrawTask t{0, seed, dtype, std::vector<int64_t>(sizes, sizes + ntensors), out};
+    int64_t ticket;
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        ticket = t.ticket = p->next_ticket++;
+        p->queue.push_back(std::move(t));
+    }
+    p->cv_task.notify_one();
+    return ticket;
+}
+
+// Block until the draw of `ticket` is complete; returns its status and forgets the ticket.
+extern "C" int arctopk_draw_wait(void* pool, int64_t ticket) {
+    if (!pool || ticket < 1) return ARCTOPK_EINVAL;
+    DrawPool* p = static_cast<DrawPool*>(pool);
+    std::unique_lock<std::mutex> lk(p->mu);
+    p->cv_done.wait(lk, [&] { return p->done.count(ticket) != 0; });
+    const int rc = p->done[ticket];
+    p->done.erase(ticket);
+    return rc;
+}
+
+// Non-blocking: 1 (and the ticket is forgotten) if the draw is complete, 0 if not yet.
+extern "C" int arctopk_draw_poll(void* pool, int64_t ticket) {
+    if (!pool || ticket < 1) return -ARCTOPK_EINVAL;
+    DrawPool* p = static_cast<DrawPool*>(pool);
+    std::lock_guard<std::mutex> lk(p->mu);
+    auto it = p->done.find(ticket);
+    if (it == p->done.end()) return 0;
+    p->done.erase(it);
+    return 1;
+}
+
+// Stream-ordered host -> device copy (hipMemcpyAsync) without a torch dispatch.
+extern "C" int arctopk_memcpy_h2d_async(void* dst, const void* src, int64_t bytes, void* stream) {
+    if (!dst || !src || bytes < 0) return ARCTOPK_EINVAL;
+    if (bytes == 0) return 0;
+    return (int)hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
 }

@@ -316,6 +316,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, rank, shapes, label,
                                            args.hook)
+    from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as _G
+    if _G.HOST_TIMES is not None and rank == 0:  # ARCTOPK_HOST_TIMING=1: host us per hook call
+        calls = max(1, (args.steps + args.warmup) * nb)
+        print("host_us_per_call " + json.dumps({k: round(v / calls * 1e6, 1)
+                                                for k, v in _G.HOST_TIMES.items()}), flush=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.barrier()

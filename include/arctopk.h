@@ -265,6 +265,37 @@ int arctopk_draw_bf16_normal(uint64_t seed, int64_t total, uint16_t* out);
 int arctopk_draw_normal(uint64_t seed, int32_t dtype, int32_t ntensors, const int64_t* sizes,
                         void* out);
 
+/*
+ * Host-only: a pool of native threads drawing projections ahead (arctopk_draw_normal into
+ * caller-owned buffers that must stay alive until the draw is waited or polled complete).
+ * submit returns a ticket (> 0) or -status; wait blocks until that draw is done and returns
+ * its status; poll returns 1 when done (ticket then forgotten), 0 if still pending.
+ * destroy drops queued draws and joins the threads (running draws finish).
+ */
+int arctopk_draw_pool_create(int32_t nthreads, void** pool);
+int arctopk_draw_pool_destroy(void* pool);
+int64_t arctopk_draw_submit(void* pool, uint64_t seed, int32_t dtype, int32_t ntensors,
+                            const int64_t* sizes, void* out);
+int arctopk_draw_wait(void* pool, int64_t ticket);
+int arctopk_draw_poll(void* pool, int64_t ticket);
+
+/* Stream-ordered host -> device copy (hipMemcpyAsync), for the projection ring. */
+int arctopk_memcpy_h2d_async(void* dst, const void* src, int64_t bytes, void* stream);
+
+/*
+ * Device-scope stream events for the hook's own intra-device ordering (projection copy ->
+ * encode, encode -> reuse of a projection slot).  torch's events release to system scope:
+ * recording one between two kernels writes back the L2 and leaves the GPU idle for several
+ * microseconds; these use hipEventReleaseToDevice | hipEventDisableTiming.  No reference
+ * counterpart (the reference is synchronous).
+ *   query: 0 = complete, 1 = not yet, < 0 / other = HIP error.
+ */
+int arctopk_event_create(void** event);
+int arctopk_event_destroy(void* event);
+int arctopk_event_record(void* event, void* stream);
+int arctopk_event_wait(void* stream, void* event);
+int arctopk_event_query(void* event);
+
 /* library build identification (for smoke tests) */
 const char* arctopk_version(void);
 
