@@ -13,3 +13,11 @@ print(f"calls {len(enc)}  spacing median {statistics.median(sp):.1f} us  p90 {so
       f"  idle-before-encode median {statistics.median(idle):.1f} p90 {sorted(idle)[int(.9 * len(idle))]:.1f} max {max(idle):.1f}")
 big = sorted(range(len(idle)), key=lambda i: -idle[i])[:8]
 print("largest idle gaps (us):", [round(idle[i], 1) for i in big])
+# idle time before each kernel kind (GPU timeline, any stream)
+kinds = {}
+for i in range(1, len(ks)):
+    nm = ks[i][2].replace("void ", "").replace("(anonymous namespace)::", "").split("<")[0].split("(")[0]
+    kinds.setdefault(nm, []).append((ks[i][0] - ks[i - 1][1]) / 1e3)
+for nm, v in sorted(kinds.items(), key=lambda kv: -sum(kv[1]))[:8]:
+    v = sorted(v)
+    print(f"  idle before {nm[:40]:40s} n={len(v):4d} median {v[len(v) // 2]:7.1f} p90 {v[int(.9 * len(v))]:7.1f} sum {sum(v):9.1f}")
