@@ -84,6 +84,7 @@ _SIGS = {
     "arctopk_event_record": (c_int32, [c_void_p, c_void_p]),
     "arctopk_event_wait": (c_int32, [c_void_p, c_void_p]),
     "arctopk_event_query": (c_int32, [c_void_p]),
+    "arctopk_round_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "arctopk_version": (c_char_p, []),
 }
 

@@ -1308,3 +1308,19 @@ extern "C" int arctopk_ef_apply(float* x, float* E, int64_t n, int32_t ef, int32
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
 }
+
+// Test entry point: the device's fp32 -> bf16 rounding (the one every kernel uses) on n
+// values, for checking it against c10::BFloat16's round-to-nearest-even on the host.
+__global__ void __launch_bounds__(256) k_round_bf16(const float* __restrict__ in, uint16_t* __restrict__ out,
+                                                    int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = from_f<bf16_t>(in[i]).u;
+}
+
+extern "C" int arctopk_round_bf16(const float* in, uint16_t* out, int64_t n, void* stream) {
+    if (!in || !out || n < 0) return ARCTOPK_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_round_bf16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       in, out, n);
+    return (int)hipGetLastError();
+}

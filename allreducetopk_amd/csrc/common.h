@@ -81,16 +81,29 @@ __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16_t x) { return __uint_as_float((uint32_t)x.u << 16); }
 template <typename T> __device__ __forceinline__ T from_f(float f);
 template <> __device__ __forceinline__ float from_f<float>(float f) { return f; }
+// gfx950 converts two floats to packed bf16 with round-to-nearest-even in one instruction
+// (v_cvt_pk_bf16_f32); only NaN needs fixing up to c10's canonical 0x7FC0
+typedef float f2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+    uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2_t{a, b}, bf2_t));
+    if (a != a) u = (u & 0xFFFF0000u) | 0x7FC0u;
+    if (b != b) u = (u & 0x0000FFFFu) | 0x7FC00000u;
+    return u;
+}
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return bf16_t{(uint16_t)0x7FC0u};
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return bf16_t{(uint16_t)(u >> 16)};
+    return bf16_t{(uint16_t)(cvt_pk_bf16(f, 0.0f) & 0xFFFFu)};
 }
 // value after the reference's rounding to T (identity for fp32)
 template <typename T> __device__ __forceinline__ float rnd(float f) { return to_f(from_f<T>(f)); }
 template <typename T> __device__ __forceinline__ float4 rnd4(float4 v) {
-    return make_float4(rnd<T>(v.x), rnd<T>(v.y), rnd<T>(v.z), rnd<T>(v.w));
+    if constexpr (sizeof(T) == 2) {
+        const uint32_t a = cvt_pk_bf16(v.x, v.y), b = cvt_pk_bf16(v.z, v.w);
+        return make_float4(__uint_as_float(a << 16), __uint_as_float(a & 0xFFFF0000u),
+                           __uint_as_float(b << 16), __uint_as_float(b & 0xFFFF0000u));
+    } else {
+        return v;
+    }
 }
 
 // quad I/O: elements 4q .. 4q+3 of p (p 4-element aligned); fp32: 16 B, bf16: 8 B
@@ -107,9 +120,7 @@ __device__ __forceinline__ float4 unpack_bf16x4(u2_t w) {
                        __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xFFFF0000u));
 }
 __device__ __forceinline__ u2_t pack_bf16x4(float4 v) {
-    const uint32_t a = from_f<bf16_t>(v.x).u, b = from_f<bf16_t>(v.y).u;
-    const uint32_t c = from_f<bf16_t>(v.z).u, d = from_f<bf16_t>(v.w).u;
-    return u2_t{a | (b << 16), c | (d << 16)};
+    return u2_t{cvt_pk_bf16(v.x, v.y), cvt_pk_bf16(v.z, v.w)};
 }
 template <> __device__ __forceinline__ float4 ldq<bf16_t, false>(const bf16_t* p, int64_t q) {
     return unpack_bf16x4(reinterpret_cast<const u2_t*>(p)[q]);

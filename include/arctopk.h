@@ -296,6 +296,10 @@ int arctopk_event_record(void* event, void* stream);
 int arctopk_event_wait(void* stream, void* event);
 int arctopk_event_query(void* event);
 
+/* Test entry point: the kernels' fp32 -> bf16 rounding (RNE, NaN -> 0x7FC0) of n device
+ * values, to check it against c10::BFloat16 on the host. */
+int arctopk_round_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
+
 /* library build identification (for smoke tests) */
 const char* arctopk_version(void);
 

@@ -403,3 +403,30 @@ def test_bf16_headline_bucket_properties():
         assert e[mask].min() >= e[~mask].max(), "a dropped row outranks a selected one"
     X = G1 + E_before  # bf16 add, as the reference's input_tensor.add_(error)
     assert torch.equal(out + st.error_dict[0], X)
+
+
+def test_device_bf16_rounding_matches_torch():
+    """The kernels' fp32 -> bf16 rounding (gfx950 v_cvt_pk_bf16_f32 + NaN fix-up) equals
+    torch's CPU .to(bfloat16) bit for bit: random values over the whole exponent range,
+    exact ties, subnormals, signed zeros, infinities, NaN."""
+    g = torch.Generator().manual_seed(7)
+    bits = torch.randint(0, 2 ** 32, (1 << 20,), generator=g, dtype=torch.int64)
+    special = torch.tensor([0x00000001, 0x00008000, 0x00018000, 0x007FFFFF, 0x00800000, 0x3F808000,
+                            0x3F818000, 0x3F80FFFF, 0x7F7FFFFF, 0x7F800000, 0xFF800000, 0x80000000,
+                            0x00000000, 0x7FC00001, 0xFFFFFFFF, 0x7F808000, 0x80008000],
+                           dtype=torch.int64)
+    x = torch.cat([bits, special]).to(torch.int32).view(torch.float32)
+    # c10::BFloat16's round_to_nearest_even, restated on the bits (torch's vectorised CPU
+    # casts may use the host's bf16 instructions, which flush subnormals)
+    u = torch.cat([bits, special]) & 0xFFFFFFFF
+    ref = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) & 0xFFFF
+    ref[torch.isnan(x)] = 0x7FC0
+    ref = ref.to(torch.int32).to(torch.int16)
+    xd = x.to(DEV)
+    out = torch.empty(x.numel(), dtype=torch.int16, device=DEV)
+    N.check(N.lib().arctopk_round_bf16(xd.data_ptr(), out.data_ptr(), x.numel(),
+                                       torch.cuda.current_stream().cuda_stream), "arctopk_round_bf16")
+    got = out.cpu()
+    bad = (got != ref).nonzero().flatten()
+    assert bad.numel() == 0, [(hex(int(x[i].view(torch.int32)) & 0xFFFFFFFF), hex(int(got[i]) & 0xFFFF),
+                               hex(int(ref[i]) & 0xFFFF)) for i in bad[:5]]
