@@ -84,6 +84,8 @@ _SIGS = {
     "arctopk_event_record": (c_int32, [c_void_p, c_void_p]),
     "arctopk_event_wait": (c_int32, [c_void_p, c_void_p]),
     "arctopk_event_query": (c_int32, [c_void_p]),
+    "arctopk_event_create_timed": (c_int32, [POINTER(c_void_p)]),
+    "arctopk_event_elapsed_ms": (c_int32, [POINTER(ctypes.c_float), c_void_p, c_void_p]),
     "arctopk_round_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "arctopk_version": (c_char_p, []),
 }
@@ -140,10 +142,20 @@ class DeviceEvent:
 
     __slots__ = ("handle",)
 
-    def __init__(self):
+    def __init__(self, timing: bool = False):
         h = ctypes.c_void_p()
-        check(lib().arctopk_event_create(ctypes.byref(h)), "arctopk_event_create")
+        if timing:
+            check(lib().arctopk_event_create_timed(ctypes.byref(h)), "arctopk_event_create_timed")
+        else:
+            check(lib().arctopk_event_create(ctypes.byref(h)), "arctopk_event_create")
         self.handle = h.value
+
+    def elapsed_time(self, end: "DeviceEvent") -> float:
+        """Milliseconds from this record to `end`'s (both timed events, both complete)."""
+        ms = ctypes.c_float()
+        check(lib().arctopk_event_elapsed_ms(ctypes.byref(ms), self.handle, end.handle),
+              "arctopk_event_elapsed_ms")
+        return float(ms.value)
 
     def record(self, stream: int) -> None:
         check(lib().arctopk_event_record(self.handle, stream), "arctopk_event_record")

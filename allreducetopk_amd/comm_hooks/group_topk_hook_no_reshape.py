@@ -118,6 +118,7 @@ class BucketPlan:
         self._v_streams = [None] * self.V_RING
         self._v_order = collections.deque(range(self.V_RING))  # least recently used first
         self.decode_done = None  # recorded after this bucket's side-stream decode
+        self.prestaged = None    # (seed, ring slot) of the next call's V, copied a call early
         self.groups = self._make_groups()
         bits = dtype_bits(dtype)
         # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
@@ -142,7 +143,7 @@ class BucketPlan:
                 self._v_streams.append(None)
                 order.append(i)
                 return i
-            copy_stream.wait_event(self._v_used[i])
+            self._v_used[i].wait(copy_stream.cuda_stream)
         order.rotate(-1)
         self._v_live[i] = False
         return i
@@ -150,32 +151,46 @@ class BucketPlan:
     def stage_projection(self, host: torch.Tensor, copy_stream, stream):
         """Copy this call's projections `host` (pinned) into the next ring slot on
         `copy_stream`; `stream` waits for the copy.  Returns (slot index, device buffer)."""
-        i = self._take_v_slot(copy_stream) if copy_stream is not stream else 0
-        buf = self.V_ring[i]
-        n = int(self.info.v_len)
-        nbytes = n * buf.element_size()
-        _ht("stage_pre")
         if copy_stream is stream:  # in order on the caller's stream: no cross-stream events
-            N.check(N.lib().arctopk_memcpy_h2d_async(buf.data_ptr(), host.data_ptr(), nbytes,
+            buf = self.V_ring[0]
+            N.check(N.lib().arctopk_memcpy_h2d_async(buf.data_ptr(), host.data_ptr(),
+                                                     int(self.info.v_len) * buf.element_size(),
                                                      stream.cuda_stream), "arctopk_memcpy_h2d_async")
-            self._v_live[i] = False
-            return i, buf
+            self._v_live[0] = False
+            return 0, buf
+        i = self.copy_projection(host, copy_stream)
+        return i, self.await_projection(i, stream)
+
+    def copy_projection(self, host: torch.Tensor, copy_stream) -> int:
+        """Issue the H2D copy of `host` into a free ring slot on `copy_stream`; returns the
+        slot.  The copy may be issued a call early (see `group_topk_hook`'s pre-staging)."""
+        i = self._take_v_slot(copy_stream)
+        buf = self.V_ring[i]
+        _ht("stage_pre")
         if self._v_streams[i] is not copy_stream:  # allocator: the slot is also used there
             buf.record_stream(copy_stream)
             self._v_streams[i] = copy_stream
-        N.check(N.lib().arctopk_memcpy_h2d_async(buf.data_ptr(), host.data_ptr(), nbytes,
+        N.check(N.lib().arctopk_memcpy_h2d_async(buf.data_ptr(), host.data_ptr(),
+                                                 int(self.info.v_len) * buf.element_size(),
                                                  copy_stream.cuda_stream), "arctopk_memcpy_h2d_async")
         if self._v_ready[i] is None:
             self._v_ready[i] = torch.cuda.Event()
-            self._v_used[i] = torch.cuda.Event()
+            # device scope: only the host's query and a copy-stream wait depend on it
+            self._v_used[i] = N.DeviceEvent()
         self._v_ready[i].record(copy_stream)
-        stream.wait_event(self._v_ready[i])
-        return i, buf
+        return i
+
+    def await_projection(self, i: int, stream) -> torch.Tensor:
+        """Order `stream` after slot i's copy.  A copy the host already sees complete needs
+        no stream wait: that wait (a barrier packet) idles the GPU ~18 us before encode."""
+        if not self._v_ready[i].query():
+            stream.wait_event(self._v_ready[i])
+        return self.V_ring[i]
 
     def projection_consumed(self, i: int, stream) -> None:
         if self._v_used[i] is None:  # the slot was filled on the caller's stream
             return
-        self._v_used[i].record(stream)
+        self._v_used[i].record(stream.cuda_stream)
         self._v_live[i] = True
 
     def _make_groups(self):
@@ -278,6 +293,8 @@ class GroupTopKState(HookState):
         # `phase_event_every`-th call (HIP events on the hook's stream)
         self.phase_events = None
         self.phase_event_every = 1
+        self.phase_event_device_scope = True  # False: torch (system-scope) timing events
+        self.prestage_hits = 0  # calls whose projections were copied during the previous call
         self._ev_calls = 0
         # measurement option (not in the reference): model a NIC-staged exchange by moving
         # the packed payload device -> pinned host -> device around the all-reduce
@@ -354,6 +371,34 @@ class GroupTopKState(HookState):
                 break
             out.append(ent[1].ms)
         return out
+
+
+def _prestage_next(state, bucket, dtype, dev) -> None:
+    """Issue the H2D copy of the NEXT call's projections now, if its prefetched draw is
+    already complete.  The next call is predicted as for the prefetch (bucket order
+    repeats) with the seed the rng will yield; a wrong prediction is simply not used (the
+    next call compares seeds).  Copying a call early lets that call skip its stream wait
+    on the copy (`BucketPlan.await_projection`)."""
+    order = state._order
+    b = bucket.index()
+    if b not in order:
+        return
+    ent = state._plans.get(order[(order.index(b) + 1) % len(order)])
+    if ent is None:
+        return
+    nplan = ent[1]
+    if not nplan.info.v_len or nplan.dtype != dtype or nplan.device != dev:
+        return
+    seed = state._proj.peek_next_seed()
+    if seed is None:
+        return
+    slot = state._proj.try_get(seed, nplan.ms, dtype)
+    if slot is None:  # not drawn yet (or drawn synchronously): staged at its call
+        return
+    cs = state._side_stream(state._copy_streams, dev)
+    i = nplan.copy_projection(slot.host, cs)
+    state._proj.release(slot, cs)
+    nplan.prestaged = (seed, i)
 
 
 _RESEED_FAST = None
@@ -506,19 +551,29 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         stream.wait_event(pend)
     dtype = input_tensor.dtype
     _ht("plan+pending")
-    slot = state._proj.get(seed, plan.ms, dtype)
-    _ht("proj_get")
     vslot, V = -1, plan.V_ring[0]
-    if plan.info.v_len:  # 512 KiB pinned H2D at headline, on a side stream, ahead of encode
-        cs = state._side_stream(state._copy_streams, dev) if state.v_copy_side_stream else stream
-        vslot, V = plan.stage_projection(slot.host, cs, stream)
-        _ht("stage_copy")
-        state._proj.release(slot, cs)  # refilled only after this copy completed
+    pre, plan.prestaged = plan.prestaged, None
+    if pre is not None and pre[0] == seed and state.v_copy_side_stream:
+        # copied during the previous call: usually complete by now, so no stream wait
+        vslot, V = pre[1], plan.await_projection(pre[1], stream)
+        state.prestage_hits += 1
+        _ht("prestaged")
     else:
-        state._proj.release(slot)
+        slot = state._proj.get(seed, plan.ms, dtype)
+        _ht("proj_get")
+        if plan.info.v_len:  # 512 KiB pinned H2D at headline, on a side stream, ahead of encode
+            cs = state._side_stream(state._copy_streams, dev) if state.v_copy_side_stream else stream
+            vslot, V = plan.stage_projection(slot.host, cs, stream)
+            _ht("stage_copy")
+            state._proj.release(slot, cs)  # refilled only after this copy completed
+        else:
+            state._proj.release(slot)
     _ht("stage_v")
     state._proj.prefetch(state._upcoming_ms(bucket), dtype)
     _ht("prefetch")
+    if state.v_copy_side_stream:
+        _prestage_next(state, bucket, dtype, dev)
+        _ht("prestage_next")
 
     evs = None
     if state.phase_events is not None:
@@ -529,8 +584,13 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
 
     def mark(name, on=None):
         if evs is not None:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(on if on is not None else stream)
+            s_ = on if on is not None else stream
+            if state.phase_event_device_scope:  # no system-scope L2 writeback per marker
+                e = N.DeviceEvent(timing=True)
+                e.record(s_.cuda_stream)
+            else:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(s_)
             evs[name] = e
 
     mark("start")

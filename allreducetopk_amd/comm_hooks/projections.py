@@ -256,11 +256,35 @@ class ProjectionSource:
         self.misses += 1
         return self._slot(ms, dtype).fill(seed)
 
+    def try_get(self, seed: int, ms: Tuple[int, ...], dtype: torch.dtype) -> Optional[Slot]:
+        """The prefetched draw for (seed, ms, dtype) if it has already completed, else None
+        (non-blocking; used to stage the next call's projections a call early)."""
+        key = (seed, tuple(ms), dtype)
+        ent = self._pending.get(key)
+        if ent is None:
+            return None
+        from allreducetopk_amd import _native as N
+        st = N.lib().arctopk_draw_poll(self._pool, ent[0])
+        if st == 0:
+            return None
+        del self._pending[key]
+        if st < 0:
+            self._free[ent[1].key].append(ent[1])
+            N.check(-st, "arctopk_draw_submit (prefetched draw)")
+        self.hits += 1
+        return ent[1]
+
+    def peek_next_seed(self) -> Optional[int]:
+        """The seed the next call will draw (None before the first call)."""
+        if self._lookahead is None:
+            return None
+        return self._peek_seeds(1)[0]
+
     def _reap_stale(self):
         from allreducetopk_amd import _native as N
         keep = []
         for ticket, slot in self._stale:
-            if N.lib().arctopk_draw_poll(self._pool, ticket) == 1:
+            if N.lib().arctopk_draw_poll(self._pool, ticket) != 0:  # done (or failed)
                 self.release(slot)
             else:
                 keep.append((ticket, slot))

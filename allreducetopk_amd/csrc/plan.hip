@@ -340,6 +340,19 @@ extern "C" int arctopk_event_create(void** event) {
     return (int)st;
 }
 
+extern "C" int arctopk_event_create_timed(void** event) {
+    if (!event) return ARCTOPK_EINVAL;
+    hipEvent_t e = nullptr;
+    const hipError_t st = hipEventCreateWithFlags(&e, hipEventReleaseToDevice);
+    *event = st == hipSuccess ? (void*)e : nullptr;
+    return (int)st;
+}
+
+extern "C" int arctopk_event_elapsed_ms(float* ms, void* start, void* end) {
+    if (!ms || !start || !end) return ARCTOPK_EINVAL;
+    return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end);
+}
+
 extern "C" int arctopk_event_destroy(void* event) {
     return event ? (int)hipEventDestroy((hipEvent_t)event) : 0;
 }

@@ -469,15 +469,17 @@ extern "C" int arctopk_draw_wait(void* pool, int64_t ticket) {
     return rc;
 }
 
-// Non-blocking: 1 (and the ticket is forgotten) if the draw is complete, 0 if not yet.
+// Non-blocking: 1 if the draw is complete, -status if it failed (the ticket is forgotten
+// either way), 0 if not yet.
 extern "C" int arctopk_draw_poll(void* pool, int64_t ticket) {
     if (!pool || ticket < 1) return -ARCTOPK_EINVAL;
     DrawPool* p = static_cast<DrawPool*>(pool);
     std::lock_guard<std::mutex> lk(p->mu);
     auto it = p->done.find(ticket);
     if (it == p->done.end()) return 0;
+    const int rc = it->second;
     p->done.erase(it);
-    return 1;
+    return rc ? -rc : 1;
 }
 
 // Stream-ordered host -> device copy (hipMemcpyAsync) without a torch dispatch.

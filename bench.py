@@ -185,6 +185,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-events", action="store_true")
+    ap.add_argument("--system-events", action="store_true",
+                    help="time phases with torch (system-scope) events instead of device-scope ones")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (real runs); gloo lets N ranks share one GPU (rehearsal)")
     ap.add_argument("--host-staged", action="store_true",
@@ -250,6 +252,7 @@ def main():
     if not args.no_phase_events and args.hook == "arc":
         st.phase_events = []
         st.phase_event_every = 8  # sample HIP events on every 8th timed hook call
+        st.phase_event_device_scope = not args.system_events
 
     dist.barrier()
     torch.cuda.synchronize()
@@ -285,7 +288,8 @@ def main():
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "algorithmic_bytes_per_launch": alg["encode"],
-                "avg_launch_us": round(phase_ms["encode"] * 1e3, 2)}
+                "avg_launch_us": round(phase_ms["encode"] * 1e3, 2),
+                "event_scope": "system" if args.system_events else "device"}
         hook_s = phase_ms["hook_device_total"] / 1e3
         roof["hook"] = {"algorithmic_bytes": alg["total"], "device_us": round(hook_s * 1e6, 1),
                         "achieved": round(alg["total"] / hook_s / 1e9, 1),

@@ -269,7 +269,8 @@ int arctopk_draw_normal(uint64_t seed, int32_t dtype, int32_t ntensors, const in
  * Host-only: a pool of native threads drawing projections ahead (arctopk_draw_normal into
  * caller-owned buffers that must stay alive until the draw is waited or polled complete).
  * submit returns a ticket (> 0) or -status; wait blocks until that draw is done and returns
- * its status; poll returns 1 when done (ticket then forgotten), 0 if still pending.
+ * its status; poll returns 1 when done, -status if the draw failed (ticket then forgotten
+ * either way), 0 if still pending.
  * destroy drops queued draws and joins the threads (running draws finish).
  */
 int arctopk_draw_pool_create(int32_t nthreads, void** pool);
@@ -295,6 +296,12 @@ int arctopk_event_destroy(void* event);
 int arctopk_event_record(void* event, void* stream);
 int arctopk_event_wait(void* stream, void* event);
 int arctopk_event_query(void* event);
+/* Timing variant (hipEventReleaseToDevice, timing enabled) for per-kernel durations in
+ * bench.py: a torch event between two kernels writes back the L2 to system scope, which
+ * adds several microseconds to the interval it brackets; these measure what the kernel
+ * trace measures.  elapsed: milliseconds between two completed records. */
+int arctopk_event_create_timed(void** event);
+int arctopk_event_elapsed_ms(float* ms, void* start, void* end);
 
 /* Test entry point: the kernels' fp32 -> bf16 rounding (RNE, NaN -> 0x7FC0) of n device
  * values, to check it against c10::BFloat16 on the host. */
