@@ -107,16 +107,21 @@ class BucketPlan:
         self.slotmap = torch.empty(max(1, info.rows_total), dtype=torch.int32, device=dev)
         # projections: device slots filled by H2D copies on a side stream, so the copy for a
         # call overlaps the kernels before it.  A slot is reused (least recently used first)
-        # only once the host sees its last reader complete; otherwise another slot is
+        # only once the host knows its last reader complete; otherwise another slot is
         # added: the copy stream never waits for the caller's stream (such a wait makes
         # hipMemcpyAsync block the host until that stream drains, starving the GPU).
+        # Completion is tracked by a checkpoint event every V_CHECK_EVERY calls, not per
+        # call: any event recorded between two kernels idles the GPU ~6 us.
         self.V_ring = [torch.empty(max(1, info.v_len), dtype=dtype, device=dev)
                        for _ in range(self.V_RING)]
-        self._v_used = [None] * self.V_RING    # event after the encode that last read slot i
-        self._v_ready = [None] * self.V_RING   # event after slot i's H2D copy
-        self._v_live = [False] * self.V_RING   # _v_used[i] is pending or done
+        self._v_call = [0] * self.V_RING      # plan call whose encode last read slot i (0: none)
+        self._v_ready = [None] * self.V_RING  # event after slot i's H2D copy
         self._v_streams = [None] * self.V_RING
         self._v_order = collections.deque(range(self.V_RING))  # least recently used first
+        self._ncalls = 0                      # encodes that read a ring slot
+        self._checks = collections.deque()    # (call number, DeviceEvent after its encode)
+        self._done_upto = 0                   # every such encode up to this call is complete
+        self._ev_free = []                    # completed checkpoint events, for reuse
         self.decode_done = None  # recorded after this bucket's side-stream decode
         self.prestaged = None    # (seed, ring slot) of the next call's V, copied a call early
         self.groups = self._make_groups()
@@ -129,42 +134,60 @@ class BucketPlan:
     PIPELINE_MIN_BYTES = 4 << 20    # ... each at least this large (RCCL efficiency)
     V_RING = 4        # projection slots allocated up front per bucket
     V_RING_MAX = 32   # ... and at most (then the copy stream waits for the oldest reader)
+    V_CHECK_EVERY = 8  # calls per slot-reuse checkpoint event
 
-    def _take_v_slot(self, copy_stream) -> int:
+    def _checkpoint(self, stream):
+        ev = self._ev_free.pop() if self._ev_free else N.DeviceEvent()
+        ev.record(stream.cuda_stream)
+        self._checks.append((self._ncalls, ev))
+        return ev
+
+    def _known_done(self, call: int) -> bool:
+        while self._checks and self._checks[0][1].query():
+            c, ev = self._checks.popleft()
+            self._done_upto = c
+            self._ev_free.append(ev)
+        return call <= self._done_upto
+
+    def _take_v_slot(self, copy_stream, stream) -> int:
         order = self._v_order
         i = order[0]
-        if self._v_live[i] and not self._v_used[i].query():  # LRU slot still being read
+        last = self._v_call[i]
+        if last and not self._known_done(last):  # LRU slot may still be read
             if len(self.V_ring) < self.V_RING_MAX:
                 i = len(self.V_ring)
                 self.V_ring.append(torch.empty_like(self.V_ring[0]))
-                self._v_used.append(None)
+                self._v_call.append(0)
                 self._v_ready.append(None)
-                self._v_live.append(False)
                 self._v_streams.append(None)
-                order.append(i)
+                order.append(i)  # most recently used
                 return i
-            self._v_used[i].wait(copy_stream.cuda_stream)
+            ev = next((e for c, e in self._checks if c >= last), None)
+            if ev is None:  # read after the last checkpoint: record one now
+                ev = self._checkpoint(stream)
+            ev.wait(copy_stream.cuda_stream)
         order.rotate(-1)
-        self._v_live[i] = False
+        self._v_call[i] = 0
         return i
 
     def stage_projection(self, host: torch.Tensor, copy_stream, stream):
         """Copy this call's projections `host` (pinned) into the next ring slot on
-        `copy_stream`; `stream` waits for the copy.  Returns (slot index, device buffer)."""
+        `copy_stream`; `stream` waits for the copy.  Returns (slot index, device buffer);
+        slot -1: copied in order on `stream` itself (no ring bookkeeping)."""
         if copy_stream is stream:  # in order on the caller's stream: no cross-stream events
             buf = self.V_ring[0]
             N.check(N.lib().arctopk_memcpy_h2d_async(buf.data_ptr(), host.data_ptr(),
                                                      int(self.info.v_len) * buf.element_size(),
                                                      stream.cuda_stream), "arctopk_memcpy_h2d_async")
-            self._v_live[0] = False
-            return 0, buf
-        i = self.copy_projection(host, copy_stream)
+            return -1, buf
+        i = self.copy_projection(host, copy_stream, stream)
         return i, self.await_projection(i, stream)
 
-    def copy_projection(self, host: torch.Tensor, copy_stream) -> int:
+    def copy_projection(self, host: torch.Tensor, copy_stream, stream) -> int:
         """Issue the H2D copy of `host` into a free ring slot on `copy_stream`; returns the
-        slot.  The copy may be issued a call early (see `group_topk_hook`'s pre-staging)."""
-        i = self._take_v_slot(copy_stream)
+        slot.  The copy may be issued a call early (see `group_topk_hook`'s pre-staging);
+        `stream` is the caller's stream (the encodes that read the ring)."""
+        i = self._take_v_slot(copy_stream, stream)
         buf = self.V_ring[i]
         _ht("stage_pre")
         if self._v_streams[i] is not copy_stream:  # allocator: the slot is also used there
@@ -175,23 +198,22 @@ class BucketPlan:
                                                  copy_stream.cuda_stream), "arctopk_memcpy_h2d_async")
         if self._v_ready[i] is None:
             self._v_ready[i] = torch.cuda.Event()
-            # device scope: only the host's query and a copy-stream wait depend on it
-            self._v_used[i] = N.DeviceEvent()
         self._v_ready[i].record(copy_stream)
         return i
 
     def await_projection(self, i: int, stream) -> torch.Tensor:
         """Order `stream` after slot i's copy.  A copy the host already sees complete needs
-        no stream wait: that wait (a barrier packet) idles the GPU ~18 us before encode."""
+        no stream wait (a wait packet between two kernels idles the GPU)."""
         if not self._v_ready[i].query():
             stream.wait_event(self._v_ready[i])
         return self.V_ring[i]
 
     def projection_consumed(self, i: int, stream) -> None:
-        if self._v_used[i] is None:  # the slot was filled on the caller's stream
-            return
-        self._v_used[i].record(stream.cuda_stream)
-        self._v_live[i] = True
+        """The encode just enqueued on `stream` reads slot i."""
+        self._ncalls += 1
+        self._v_call[i] = self._ncalls
+        if self._ncalls % self.V_CHECK_EVERY == 0:
+            self._checkpoint(stream)
 
     def _make_groups(self):
         """Contiguous segment ranges with roughly equal packed bytes: (b, e, lo, hi)."""
@@ -396,7 +418,7 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
     if slot is None:  # not drawn yet (or drawn synchronously): staged at its call
         return
     cs = state._side_stream(state._copy_streams, dev)
-    i = nplan.copy_projection(slot.host, cs)
+    i = nplan.copy_projection(slot.host, cs, torch.cuda.current_stream(dev))
     state._proj.release(slot, cs)
     nplan.prestaged = (seed, i)
 
