@@ -122,6 +122,7 @@ class BucketPlan:
         self._checks = collections.deque()    # (call number, DeviceEvent after its encode)
         self._done_upto = 0                   # every such encode up to this call is complete
         self._ev_free = []                    # completed checkpoint events, for reuse
+        self.v_waits = 0                      # calls whose encode had to wait for its copy
         self.decode_done = None  # recorded after this bucket's side-stream decode
         self.prestaged = None    # (seed, ring slot) of the next call's V, copied a call early
         self.groups = self._make_groups()
@@ -206,6 +207,7 @@ class BucketPlan:
         no stream wait (a wait packet between two kernels idles the GPU)."""
         if not self._v_ready[i].query():
             stream.wait_event(self._v_ready[i])
+            self.v_waits += 1
         return self.V_ring[i]
 
     def projection_consumed(self, i: int, stream) -> None:
@@ -335,11 +337,12 @@ class GroupTopKState(HookState):
         self._pending: Dict[int, torch.cuda.Event] = {}  # bucket -> its decode-done event
         self._sketch_groups: Dict[object, object] = {}
 
-    def _side_stream(self, table: Dict[int, "torch.cuda.Stream"], device) -> "torch.cuda.Stream":
+    def _side_stream(self, table: Dict[int, "torch.cuda.Stream"], device,
+                     priority: int = 0) -> "torch.cuda.Stream":
         idx = torch.device(device).index or 0
         s = table.get(idx)
         if s is None:
-            s = torch.cuda.Stream(device=device)
+            s = torch.cuda.Stream(device=device, priority=priority)
             table[idx] = s
         return s
 
@@ -417,7 +420,7 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
     slot = state._proj.try_get(seed, nplan.ms, dtype)
     if slot is None:  # not drawn yet (or drawn synchronously): staged at its call
         return
-    cs = state._side_stream(state._copy_streams, dev)
+    cs = state._side_stream(state._copy_streams, dev, COPY_PRIORITY)
     i = nplan.copy_projection(slot.host, cs, torch.cuda.current_stream(dev))
     state._proj.release(slot, cs)
     nplan.prestaged = (seed, i)
@@ -426,6 +429,12 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
 _RESEED_FAST = None
 
 # optional host-time breakdown of the hook (diagnostics; ARCTOPK_HOST_TIMING=1)
+# Priority of the projection copy stream.  HIP maps a process's streams onto a few HW
+# queues (4 on MI355X); a normal-priority copy stream can share one with the caller's
+# stream, and its completion marker then waits behind the queued kernels, so the encode
+# always had to wait for the copy (~17 us idle per call).  A high-priority stream gets a
+# queue of its own: the copy is seen complete a call later and no wait is needed.
+COPY_PRIORITY = int(os.environ.get("ARCTOPK_COPY_PRIORITY", "-1"))
 HOST_TIMES = {} if os.environ.get("ARCTOPK_HOST_TIMING") == "1" else None
 _ht_last = [0.0]
 
@@ -495,7 +504,7 @@ def _stage_through_host(state: GroupTopKState, pv: torch.Tensor, stream, dev,
     if state._host_buf is None or state._host_buf.numel() < n:
         state._host_buf = torch.empty(n, dtype=pv.dtype, pin_memory=True)
     hb = state._host_buf[:n]
-    d2h = state._side_stream(state._copy_streams, dev)
+    d2h = state._side_stream(state._copy_streams, dev, COPY_PRIORITY)
     h2d = state._side_stream(state._decode_streams, dev)
     d2h.wait_stream(stream)
     h2d.wait_stream(stream)
@@ -584,7 +593,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         slot = state._proj.get(seed, plan.ms, dtype)
         _ht("proj_get")
         if plan.info.v_len:  # 512 KiB pinned H2D at headline, on a side stream, ahead of encode
-            cs = state._side_stream(state._copy_streams, dev) if state.v_copy_side_stream else stream
+            cs = state._side_stream(state._copy_streams, dev, COPY_PRIORITY) if state.v_copy_side_stream else stream
             vslot, V = plan.stage_projection(slot.host, cs, stream)
             _ht("stage_copy")
             state._proj.release(slot, cs)  # refilled only after this copy completed

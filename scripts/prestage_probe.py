@@ -31,12 +31,15 @@ def loop(n):
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"  host enqueue {(t1 - t0) / n / 4 * 1e6:.1f} us/call, wall {(t2 - t0) / n / 4 * 1e6:.1f} us/call, "
-          f"prestaged {st.prestage_hits - h0}/{4 * n}, draw hits {st._proj.hits - p0} misses {st._proj.misses}",
+          f"prestaged {st.prestage_hits - h0}/{4 * n}, v_waits {sum(p[1].v_waits for p in st._plans.values())}, draw hits {st._proj.hits - p0} misses {st._proj.misses}",
           flush=True)
 
 
 for _ in range(3):
     loop(5)
+if os.environ.get("ONLY_ON"):
+    loop(40)
+    sys.exit(0)
 print("prestaging on:")
 loop(40)
 orig = H._prestage_next
