@@ -41,7 +41,7 @@ import torch.distributed as dist
 
 from allreducetopk_amd import _native as N
 from allreducetopk_amd.comm_hooks import default_hooks
-from allreducetopk_amd.comm_hooks.projections import ProjectionSource
+from allreducetopk_amd.comm_hooks.projections import SYNC_MAX_VALUES, ProjectionSource
 from allreducetopk_amd.comm_hooks.utils import HookState, dtype_bits, tensor_bits
 
 logger = logging.getLogger(__name__)
@@ -418,8 +418,10 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
     if seed is None:
         return
     slot = state._proj.try_get(seed, nplan.ms, dtype)
-    if slot is None:  # not drawn yet (or drawn synchronously): staged at its call
-        return
+    if slot is None:
+        if sum(nplan.ms) * nplan.r >= SYNC_MAX_VALUES:  # prefetched draw not done: at its call
+            return
+        slot = state._proj.get(seed, nplan.ms, dtype)  # small: drawn here instead of next call
     cs = state._side_stream(state._copy_streams, dev, COPY_PRIORITY)
     i = nplan.copy_projection(slot.host, cs, torch.cuda.current_stream(dev))
     state._proj.release(slot, cs)
