@@ -1157,7 +1157,11 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
     if (p->n_small) {
         // one block per segment: 1024 threads once a segment has more than 4096 rows (the
         // radix rounds and the compaction are per-block latency chains)
-        if (p->small_lds > 4096 * 4 + 16)
+        static const int64_t big_rows = [] {  // tuning switch (A/B): rows for 1024 threads
+            const char* env = std::getenv("ARCTOPK_SEL_BIG_ROWS");
+            return env ? std::max<int64_t>(1, std::atoll(env)) : (int64_t)4096;
+        }();
+        if (p->small_lds > big_rows * 4 + 16)
             hipLaunchKernelGGL((k_select_small<T, 1024>), dim3(p->n_small), dim3(1024), (size_t)p->small_lds,
                                st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
         else
