@@ -13,7 +13,9 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uin
 import torch
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("ARCTOPK_LIB", os.path.join(PKG, "lib", "libarctopk.so"))
+# ARCTOPK_LIB: an explicitly named library (A/B tuning variants) skips the source-hash check
+LIB_OVERRIDE = os.environ.get("ARCTOPK_LIB")
+LIB_PATH = LIB_OVERRIDE or os.path.join(PKG, "lib", "libarctopk.so")
 
 EF_NONE, EF14, EF21 = 0, 1, 2
 EF_CODE = {"noef": EF_NONE, "ef14": EF14, "ef21": EF21}
@@ -117,8 +119,29 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if not LIB_OVERRIDE:
+            _check_build(L)
         _lib = L
     return _lib
+
+
+class StaleNativeLibrary(ImportError):
+    pass
+
+
+def _check_build(L) -> None:
+    """Refuse a library built from other sources than the ones in this tree (the hash
+    the build embedded in arctopk_version() vs the hash of csrc/ + arctopk.h now)."""
+    from allreducetopk_amd import build as B
+    ver = L.arctopk_version().decode()
+    m = B.HASH_RE.search(ver.encode())
+    if not os.path.isdir(B.CSRC):  # sources not shipped: nothing to compare against
+        return
+    want = B.source_hash()
+    if m is None or m.group(1).decode() != want:
+        raise StaleNativeLibrary(
+            f"{LIB_PATH} was built from other sources ({ver!r}; sources hash {want}): rebuild "
+            "with `python -m allreducetopk_amd.build` (or name a variant via ARCTOPK_LIB)")
 
 
 def check(status: int, what: str) -> None:

@@ -3,10 +3,19 @@
     python -m allreducetopk_amd.build        # -> allreducetopk_amd/lib/libarctopk.so
 
 The library is built in-tree so it travels with the repo snapshot to the GPU box.
+
+Build integrity: every build embeds ``source_hash()`` -- a SHA-256 over the sources,
+the public header, this recipe's compiler flags and any ``-D`` defines -- in the string
+``arctopk_version()`` returns.  ``build()`` rebuilds whenever the hash of the tree
+differs from the one the library carries, and ``_native.lib()`` refuses a library whose
+hash does not match the sources next to it (unless ``ARCTOPK_LIB`` names a library
+explicitly, e.g. an A/B tuning variant).
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -17,8 +26,12 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libarctopk.so")
-SOURCES = ["plan.hip", "arctopk_kernels.hip", "sparse_kernels.hip", "mselect.hip", "projection.cpp"]
+SOURCES = ["plan.hip", "arctopk_kernels.hip", "sparse_kernels.hip", "mselect.hip", "codec.hip",
+           "projection.cpp"]
 ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+         "-Wno-unused-function"]
+HASH_RE = re.compile(rb"src:([0-9a-f]{16})")
 
 
 def hipcc() -> str:
@@ -28,13 +41,33 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build libarctopk)")
 
 
+def source_hash(defines=()) -> str:
+    """16 hex digits of SHA-256 over every file in csrc/, include/arctopk.h, the
+    compiler flags and the defines (what determines the built machine code)."""
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if not f.startswith("."))
+    for f in files:
+        h.update(f.encode() + b"\0")
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(INCLUDE, "arctopk.h"), "rb") as fh:
+        h.update(fh.read())
+    h.update(" ".join([ARCH, *FLAGS, *sorted(defines)]).encode())
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(path: str = LIB):
+    """The source hash a built library carries (read from its bytes; no loading)."""
+    try:
+        with open(path, "rb") as fh:
+            m = HASH_RE.search(fh.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "arctopk.h"),
-                                                              os.path.abspath(__file__)]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return embedded_hash(LIB) != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
@@ -45,9 +78,9 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     os.makedirs(os.path.dirname(out), exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     tmp = out + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], f"-I{INCLUDE}", f"-I{CSRC}",
-           *srcs, "-o", tmp]
+    digest = source_hash(defines)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *[f"-D{d}" for d in defines],
+           f'-DARCTOPK_SRC_HASH="{digest}"', f"-I{INCLUDE}", f"-I{CSRC}", *srcs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -126,6 +126,10 @@ class BucketPlan:
         self.decode_done = None  # recorded after this bucket's side-stream decode
         self.prestaged = None    # (seed, ring slot) of the next call's V, copied a call early
         self.groups = self._make_groups()
+        # the device generator's Philox offset after the reference's per-tensor
+        # torch.randn(m, r, device=...) draws of one call (see _reseed_global)
+        self.philox_advance = sum(philox_step(s.m * r, dtype, self.device)
+                                  for s in self.segments if s.kind == N.SEG_SKETCH)
         bits = dtype_bits(dtype)
         # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
         self.bits_sum = sum(((s.n if s.kind == N.SEG_RAW else s.n * r) + s.k_rows * s.m) * bits
@@ -335,7 +339,45 @@ class GroupTopKState(HookState):
         self._copy_streams: Dict[int, torch.cuda.Stream] = {}
         self._decode_streams: Dict[int, torch.cuda.Stream] = {}
         self._pending: Dict[int, torch.cuda.Event] = {}  # bucket -> its decode-done event
-        self._sketch_groups: Dict[object, object] = {}
+        # Sketch all-reduces on a communicator of their own ("separate", created here,
+        # before any backward) or on the packed values' communicator ("shared": no second
+        # communicator; a sketch then queues behind the previous bucket's packed
+        # all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
+        self.sketch_comm = os.environ.get("ARCTOPK_SKETCH_COMM", "separate")
+        if self.sketch_comm not in ("separate", "shared"):
+            raise ValueError("ARCTOPK_SKETCH_COMM must be 'separate' or 'shared'")
+        self._sketch_pg = None
+        self.init_sketch_comm()
+        # The plan of a bucket is found by its buffer's identity (no gradients() walk per
+        # call).  DDP rebuilds its buckets once, after the first iteration, and the caching
+        # allocator may hand a rebuilt bucket the same block: for the first
+        # `layout_check_iters` iterations after compression starts every call re-checks
+        # the gradient shapes against its plan.
+        self.layout_check_iters = 3
+        self._first_compressed_iter = None
+
+    def init_sketch_comm(self) -> None:
+        """Create the sketch communicator now (a collective over every rank of the default
+        group; register_comm_hook_for_ddp_model constructs the state on every rank).
+        Called by the constructor; a state built before init_process_group runs with the
+        shared communicator unless this is called once the group exists.  The hook itself
+        never creates a process group."""
+        if self.sketch_comm != "separate" or self._sketch_pg is not None:
+            return
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        group = self.process_group if self.process_group is not None else dist.group.WORLD
+        ws = dist.get_world_size()
+        if ws <= 1 or group.size() != ws:  # a subgroup: its ranks alone run this hook
+            return
+        kw = {}
+        try:  # a default group bound to a device initialises the new communicator eagerly
+            dev = dist.distributed_c10d._get_default_group().bound_device_id
+            if dev is not None:
+                kw["device_id"] = dev
+        except AttributeError:
+            pass
+        self._sketch_pg = dist.new_group(ranks=list(range(ws)), **kw)
 
     def _side_stream(self, table: Dict[int, "torch.cuda.Stream"], device,
                      priority: int = 0) -> "torch.cuda.Stream":
@@ -347,16 +389,9 @@ class GroupTopKState(HookState):
         return s
 
     def _sketch_group(self, group):
-        """A second communicator over the same ranks for the sketch all-reduces (created
-        collectively on the first compressed call; only for the world group, whose every
-        rank runs this hook)."""
-        if group is not dist.group.WORLD and group.size() != dist.get_world_size():
-            return group
-        g = self._sketch_groups.get(group)
-        if g is None:
-            g = dist.new_group(ranks=list(range(dist.get_world_size())))
-            self._sketch_groups[group] = g
-        return g
+        """The communicator of the sketch all-reduces: the separate one made at
+        construction, else the packed values' own."""
+        return self._sketch_pg if self._sketch_pg is not None else group
 
     def _after_load(self) -> None:
         # prefetched projections were keyed on seeds of the old rng position
@@ -364,11 +399,14 @@ class GroupTopKState(HookState):
 
     def _plan_for(self, bucket) -> BucketPlan:
         buf = bucket.buffer()
+        if self._first_compressed_iter is None:
+            self._first_compressed_iter = self.iter
         # fast path: the bucket's flat buffer is the one this plan was built for (DDP keeps a
-        # bucket's buffer across iterations; a bucket rebuild allocates new buffers)
+        # bucket's buffer across iterations; its one-time rebuild falls in the check window)
         ident = (buf.data_ptr(), buf.numel(), buf.dtype, self.r, float(self.compress_ratio))
         hit = self._plans.get(bucket.index())
-        if hit is not None and hit[2] == ident:
+        if (hit is not None and hit[2] == ident
+                and self.iter >= self._first_compressed_iter + self.layout_check_iters):
             return hit[1]
         grads = bucket.gradients()
         shapes = [tuple(g.shape) for g in grads]
@@ -450,12 +488,18 @@ def _ht(name=None):
     _ht_last[0] = t
 
 
-def _reseed_global(seed: int) -> None:
-    """``torch.manual_seed(seed)`` (ref :255) without its per-call Python overhead.
+def _reseed_global(seed: int, device_index: int = 0, advance: int = 0) -> None:
+    """``torch.manual_seed(seed)`` (ref :255) and the reference's projection draws'
+    effect on the device generator, without their per-call cost.
 
     torch.manual_seed reseeds the CPU generator and every CUDA device's default
     generator (plus MPS/XPU/custom devices, absent on ROCm builds).  When only CPU and
-    CUDA exist this does exactly that; otherwise it defers to torch.manual_seed.
+    CUDA exist this does exactly that; otherwise it defers to torch.manual_seed.  The
+    reference then draws ``torch.randn(m, r, device=tensor.device)`` per 2-D/ND tensor
+    (:49, :79), which moves that device generator's Philox offset by `advance` (summed
+    per draw, BucketPlan.philox_advance); the codec draws V from the CPU stream instead
+    (DESIGN.md deviation 3), so the offset is set directly: afterwards the global
+    generators stand exactly where the reference leaves them.
     """
     global _RESEED_FAST
     if _RESEED_FAST is None:
@@ -466,10 +510,32 @@ def _reseed_global(seed: int) -> None:
             if fast else False
     if _RESEED_FAST is False or not torch.cuda.is_initialized():
         torch.manual_seed(seed)
+        if advance and torch.cuda.is_initialized():
+            torch.cuda.default_generators[device_index].set_offset(advance)
         return
     for g in _RESEED_FAST:
         g.manual_seed(seed)
     torch.default_generator.manual_seed(seed)
+    if advance:
+        _RESEED_FAST[device_index].set_offset(advance)
+
+
+_PHILOX_STEP: Dict[tuple, int] = {}
+
+
+def philox_step(numel: int, dtype, device) -> int:
+    """Philox offset one ``torch.randn(numel, dtype, device)`` consumes, measured once per
+    (numel, dtype, device) on a private generator (the global ones are not touched)."""
+    dev = torch.device(device)
+    key = (int(numel), dtype, dev.index or 0)
+    v = _PHILOX_STEP.get(key)
+    if v is None:
+        g = torch.Generator(device=dev)
+        g.manual_seed(0)
+        torch.randn(int(numel), dtype=dtype, device=dev, generator=g)
+        v = int(g.get_offset())
+        _PHILOX_STEP[key] = v
+    return v
 
 
 def cal_k(state, tensor) -> int:
@@ -494,6 +560,24 @@ def _check_bucket_layout(buf: torch.Tensor, grads) -> None:
         off += g.numel()
     if off != buf.numel():
         raise RuntimeError("bucket gradient views do not cover the buffer")
+
+
+def _residual_on(table: Dict[int, torch.Tensor], b: int, bucket: torch.Tensor,
+                 name: str) -> torch.Tensor:
+    """The residual of bucket b, checked before its pointer reaches a kernel: same numel and
+    dtype as the bucket (else RuntimeError, as the reference's add_ raises), contiguous, on
+    the bucket's device (a checkpoint loaded with map_location='cpu' or onto another rank's
+    device is moved there once and kept)."""
+    t = table[b]
+    if t.numel() != bucket.numel():
+        raise RuntimeError(f"bucket {b} changed size ({t.numel()} -> {bucket.numel()}) after its "
+                           f"residual ({name}) was created")
+    if t.dtype != bucket.dtype:
+        raise RuntimeError(f"{name}[{b}] is {t.dtype} but the bucket is {bucket.dtype}")
+    if t.device != bucket.device or not t.is_contiguous():
+        t = t.to(bucket.device).contiguous()
+        table[b] = t
+    return t
 
 
 def _stage_through_host(state: GroupTopKState, pv: torch.Tensor, stream, dev,
@@ -565,18 +649,19 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             return fut
         err = state.error_dict[b]
         gerr = state.global_error_dict[b]
-    if err is not None and err.numel() != total:
-        raise RuntimeError(f"bucket {b} changed size ({err.numel()} -> {total}) after its "
-                           "residual was created")
+    if err is not None:
+        err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
+        if gerr is not None:
+            gerr = _residual_on(state.global_error_dict, b, input_tensor, "global_error_dict")
 
     # per-call projection seed, and the reference's global reseed side effect (:254-255)
     _ht()
     seed = state._proj.consume_seed(state.rng)
-    _reseed_global(seed)
-    _ht("seed")
-
     plan = state._plan_for(bucket)
     dev = input_tensor.device
+    _reseed_global(seed, dev.index or 0, plan.philox_advance)
+    _ht("seed+plan")
+
     stream = torch.cuda.current_stream(dev)
     sid = stream.cuda_stream
     pend = state._pending.pop(b, None)

@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 from allreducetopk_amd import _native as N
 from allreducetopk_amd.comm_hooks import default_hooks
+from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import _residual_on
 from allreducetopk_amd.comm_hooks.utils import (HookState, _get_allgather_out_list, dtype_bits,
                                                 tensor_bits)
 
@@ -98,8 +99,16 @@ def _workspace(state, device, numels) -> torch.Tensor:
 
 def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch.Tensor]":
     if state.use_error_feedback == "ef21" and state.large_batch_init:
-        raise NotImplementedError("large_batch_init EF21 (dead code in the reference, "
-                                  "sparse_hook.py:156) is not provided")
+        # reference: sparse_hook_sync_large_batch_ef21 (sparse_hook.py:331-416,
+        # sparse_hook_c4.py:353-457), reached only when large_batch_init is set by hand
+        # (both constructors hard-code False)
+        raise NotImplementedError("the large_batch_init EF21 path is not implemented by the "
+                                  "MI355X codec")
+    if state.use_error_feedback == "ef21" and state.error_decay != 1.0:
+        # the reference scales the EF21 residual updates by error_decay (sparse_hook.py:265,
+        # :296); the fused kernels implement the default error_decay = 1.0 only
+        raise NotImplementedError(f"error_decay={state.error_decay} (EF21 residual scaling) is "
+                                  "not implemented by the MI355X codec; only 1.0")
     state.maybe_accumulate_momentum_on_bucket(bucket)
     group = state.process_group if state.process_group is not None else dist.group.WORLD
     world_size = group.size()
@@ -129,11 +138,14 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
         if not err_in:
             logger.info("A zero tensor of length %s that represents local error is created.", total)
             state.error_dict[b] = torch.zeros(total, device=device, dtype=dtype)
-        N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), state.error_dict[b].data_ptr(), total,
+        err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
+        N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), err.data_ptr(), total,
                                    N.EF14, int(err_in), stream), "arctopk_ef_apply")
     elif ef == N.EF21:
         if b in state.error_dict:
-            N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), state.error_dict[b].data_ptr(),
+            err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
+            _residual_on(state.global_error_dict, b, input_tensor, "global_error_dict")
+            N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), err.data_ptr(),
                                        total, N.EF21, 1, stream), "arctopk_ef_apply")
         else:  # (:213-226)
             logger.info("A tensor of length %s that represents local/global error is created.", total)
@@ -190,6 +202,9 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
                 "arctopk_topk_select")
         bits_sum = sum_k * (dtype_bits(dtype) + 32)
 
+    # the call's selection, for inspection and tests (int32 indices per tensor, concatenated
+    # in bucket order at the k offsets; TopK: ascending within a tensor)
+    state.last_indices, state.last_k = indices, ks
     if ef != N.EF_NONE:  # residual persistence (:257-267)
         N.check(L.arctopk_sparse_residual(state.error_dict[b].data_ptr(), nt, a_off, a_k, a_ko,
                                           indices.data_ptr(), values.data_ptr(), ef, stream),

@@ -375,6 +375,11 @@ extern "C" int arctopk_event_query(void* event) {
     return (int)st;
 }
 
+#ifndef ARCTOPK_SRC_HASH
+#define ARCTOPK_SRC_HASH "unknown0000000000"
+#endif
+// "src:<hash>" is the build recipe's source hash (allreducetopk_amd/build.py): the loader
+// refuses a library built from other sources than the ones next to it
 extern "C" const char* arctopk_version(void) {
-    return "libarctopk 0.1 gfx950 (ARC-TopK encode/select/pack/decode, TopK/RandK)";
+    return "libarctopk 0.2 gfx950 (ARC-TopK encode/select/pack/decode, TopK/RandK) src:" ARCTOPK_SRC_HASH;
 }

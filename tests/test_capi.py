@@ -113,3 +113,38 @@ def test_compute_entry_points_reject_null_without_touching_device(lib):
     assert lib.arctopk_sparse_workspace_bytes(2, N.i64_array([10, 4_000_000])) > 500_000 * 8
     assert lib.arctopk_sparse_workspace_bytes(0, None) == -1001
     assert lib.arctopk_sparse_workspace_bytes(1, N.i64_array([0])) == -1001
+
+
+def test_library_matches_its_sources(lib):
+    """Build integrity: the loaded library carries the hash of the sources next to it, and
+    the loader refuses a library whose embedded hash differs (a stale or foreign build)."""
+    from allreducetopk_amd import build as B
+    assert B.embedded_hash(LIB) == B.source_hash()
+    assert f"src:{B.source_hash()}".encode() in lib.arctopk_version()
+
+    class Fake:
+        def __init__(self, ver):
+            self.arctopk_version = lambda: ver
+    with pytest.raises(N.StaleNativeLibrary):
+        N._check_build(Fake(b"libarctopk 0.2 gfx950 src:0123456789abcdef"))
+    with pytest.raises(N.StaleNativeLibrary):
+        N._check_build(Fake(b"libarctopk 0.1 gfx950 (no hash)"))
+    N._check_build(Fake(f"libarctopk src:{B.source_hash()}".encode()))
+
+
+def test_residual_checks_before_any_kernel():
+    """A residual on the wrong device is moved to the bucket's; a wrong size or dtype
+    raises (a host pointer must never reach a kernel)."""
+    import torch
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import _residual_on
+    bucket = torch.zeros(12)
+    table = {0: torch.ones(12, dtype=torch.float64)}
+    with pytest.raises(RuntimeError, match="dtype|float64"):
+        _residual_on(table, 0, bucket, "error_dict")
+    table = {0: torch.ones(13)}
+    with pytest.raises(RuntimeError, match="changed size"):
+        _residual_on(table, 0, bucket, "error_dict")
+    t = torch.arange(24.0)[::2]  # non-contiguous
+    table = {0: t}
+    got = _residual_on(table, 0, bucket, "error_dict")
+    assert got.is_contiguous() and table[0] is got and torch.equal(got, t)

@@ -194,3 +194,28 @@ def _product_host_paths_worker(rank, ws, port, td):
 
 def test_product_host_paths_ws2():
     _spawn(_product_host_paths_worker)
+
+
+# ---------------------------------------------------------------------------
+def _sketch_comm_worker(rank, ws, port, td, mode):
+    os.environ["ARCTOPK_SKETCH_COMM"] = mode
+    _setup(rank, ws, port)
+    from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
+    st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0)
+    world = dist.group.WORLD
+    if mode == "separate":  # created by the constructor, collectively, before any backward
+        assert st._sketch_pg is not None and st._sketch_pg is not world
+        assert st._sketch_group(world) is st._sketch_pg
+        t = torch.ones(3) * (rank + 1)
+        dist.all_reduce(t, group=st._sketch_pg)
+        assert torch.equal(t, torch.full((3,), 3.0))
+    else:
+        assert st._sketch_pg is None and st._sketch_group(world) is world
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["separate", "shared"])
+def test_sketch_communicator_created_at_construction(mode):
+    """The hook never calls new_group: the separate sketch communicator is made by the
+    state's constructor (on every rank, as register_comm_hook_for_ddp_model does)."""
+    _spawn(_sketch_comm_worker, mode)

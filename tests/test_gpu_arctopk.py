@@ -291,6 +291,85 @@ def test_resume_from_state_dict_is_bit_identical(ef, tmp_path):
     assert b.iter == ref.iter
 
 
+def test_resume_from_cpu_checkpoint_without_device():
+    """A checkpoint loaded with map_location='cpu' and no device argument: the hook moves
+    the residuals to the bucket's device on first use (never hands a host pointer to a
+    kernel) and continues bit-identically."""
+    shapes = MIX
+
+    def mk():
+        return GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                              use_error_feedback="ef21", seed=56)
+
+    def call(st, it):
+        G = _rand_bucket(shapes, 400 + it).to(DEV)
+        out = group_topk_hook(st, SyntheticBucket(G, shapes, index=0, is_last=True)).wait()
+        torch.cuda.synchronize()
+        return out.clone()
+
+    ref = mk()
+    ref_outs = [call(ref, it) for it in range(4)]
+    a = mk()
+    for it in range(2):
+        call(a, it)
+    sd = {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in a.state_dict().items()}
+    sd["error_dict"] = {b: t.cpu() for b, t in sd["error_dict"].items()}
+    sd["global_error_dict"] = {b: t.cpu() for b, t in sd["global_error_dict"].items()}
+    b = mk()
+    b.load_state_dict(sd)
+    assert b.error_dict[0].device.type == "cpu"
+    for it in range(2, 4):
+        assert_bitwise(call(b, it), ref_outs[it], f"resumed it{it}")
+    assert b.error_dict[0].is_cuda and b.global_error_dict[0].is_cuda
+
+
+def test_plan_follows_a_rebuilt_bucket_on_the_same_buffer():
+    """DDP rebuilds its buckets after the first iteration and the caching allocator may
+    give the new bucket the old buffer: same pointer and numel, other tensors.  The hook
+    must notice the new layout (shapes re-checked during the first iterations after
+    compression starts) and encode with a plan of the new geometry."""
+    shapes_a = [[64, 256], [128], [32, 16, 3, 3], [200, 96]]
+    shapes_b = [[200, 96], [32, 16, 3, 3], [64, 256], [128]]  # same numel, other order
+    assert bucket_numel(shapes_a) == bucket_numel(shapes_b)
+    st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                        use_error_feedback="noef", seed=8)
+    ost = A.OracleState(seed=8)
+    buf = torch.empty(bucket_numel(shapes_a), device=DEV)
+    for it, shapes in enumerate([shapes_a, shapes_b, shapes_b]):
+        G = _rand_bucket(shapes, 600 + it)
+        buf.copy_(G)
+        out = group_topk_hook(st, SyntheticBucket(buf, shapes, index=0, is_last=True)).wait()
+        torch.cuda.synchronize()
+        plan = st._plans[0][1]
+        assert [tuple(s) for s in plan.shapes] == [tuple(s) for s in shapes]
+        seed = ost.next_seed()
+        rows = _gpu_rows(plan)
+        res = A.simulate_step([G], [None], None, shapes, 0.2, 4, "noef", seed, rows_override=rows)
+        assert_bitwise(out, res["out"], f"call {it} output")
+
+
+def test_device_rng_left_where_the_reference_leaves_it():
+    """After a compressed call the global generators sit where the reference's would: the
+    CPU generator freshly seeded with the call's seed, the bucket device's generator
+    seeded and advanced past one torch.randn(m, r) per 2-D/ND tensor (ref :49, :79, :255)."""
+    shapes = [[64, 256], [128], [32, 16, 3, 3], [200, 96], [40000, 4]]
+    st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                        use_error_feedback="noef", seed=12)
+    seed = A.OracleState(seed=12).next_seed()
+    group_topk_hook(st, SyntheticBucket(_rand_bucket(shapes, 1).to(DEV), shapes)).wait()
+    torch.cuda.synchronize()
+    after_hook = (torch.cuda.default_generators[0].get_offset(),
+                  torch.randn(3, device=DEV).cpu(), torch.randn(3).clone())
+    torch.manual_seed(seed)  # the reference's draws, on the device
+    for s in A.segments(shapes, 0.2):
+        if s.kind == A.SKETCH:
+            torch.randn(s.m, 4, device=DEV)
+    ref = (torch.cuda.default_generators[0].get_offset(), torch.randn(3, device=DEV).cpu(),
+           torch.randn(3).clone())
+    assert after_hook[0] == ref[0]
+    assert torch.equal(after_hook[1], ref[1]) and torch.equal(after_hook[2], ref[2])
+
+
 @pytest.mark.parametrize("fill", ["zero", "two_levels"])
 def test_select_degenerate_energies(fill):
     """All-equal energies (zero gradients) and two energy levels on large segments: the
