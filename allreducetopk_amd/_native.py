@@ -52,11 +52,12 @@ _SIGS = {
                                  c_void_p]),
     "arctopk_select": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "arctopk_row_energy": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
-    "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                               c_void_p]),
     "arctopk_decode": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                  c_void_p]),
     "arctopk_pack_segments": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int32,
-                                        c_void_p, c_void_p, c_void_p]),
+                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "arctopk_decode_segments": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int32,
                                           c_int32, c_void_p, c_void_p, c_void_p]),
     "arctopk_sparse_workspace_bytes": (c_int64, [c_int32, POINTER(c_int64)]),

@@ -238,8 +238,8 @@ class BucketPlan:
 
     def pack_range(self, b: int, e: int, grad, err, ef: int, stream: int):
         N.check(N.lib().arctopk_pack_segments(self.handle, b, e, N.ptr(grad), N.ptr(err), ef,
-                                              self.rowlist.data_ptr(), self.packed.data_ptr(),
-                                              stream), "arctopk_pack_segments")
+                                              self.rowlist.data_ptr(), self.slotmap.data_ptr(),
+                                              self.packed.data_ptr(), stream), "arctopk_pack_segments")
 
     def decode_range(self, b: int, e: int, world_size: int, ef: int, gerr, out, stream: int):
         N.check(N.lib().arctopk_decode_segments(self.handle, b, e, self.packed.data_ptr(),
@@ -283,8 +283,8 @@ class BucketPlan:
 
     def pack(self, grad, err, ef: int, stream: int):
         N.check(N.lib().arctopk_pack(self.handle, N.ptr(grad), N.ptr(err), ef,
-                                     self.rowlist.data_ptr(), self.packed.data_ptr(), stream),
-                "arctopk_pack")
+                                     self.rowlist.data_ptr(), self.slotmap.data_ptr(),
+                                     self.packed.data_ptr(), stream), "arctopk_pack")
 
     def decode(self, world_size: int, ef: int, gerr, out, stream: int):
         N.check(N.lib().arctopk_decode(self.handle, self.packed.data_ptr(), self.slotmap.data_ptr(),

@@ -17,6 +17,12 @@
 
 using namespace arctopk;
 
+#ifndef ARCTOPK_DIAG_KEYS
+#define ARCTOPK_DIAG_KEYS 0  // diagnostic builds only (scripts/selbench.hip): 1 = key pass without
+#endif                       // the histogram merge, 2 = also without the LDS histogram
+#ifndef ARCTOPK_DIAG_STOP
+#define ARCTOPK_DIAG_STOP 0  // diagnostic builds only: 1 = large-segment select stops after the key pass
+#endif
 #ifdef ARCTOPK_SEL_STAMPS  // diagnostic build only (scripts/seltest.hip): phase timestamps
 __device__ unsigned long long g_sel_stamps[64];
 #define SEL_STAMP(i)                                                        \
@@ -118,9 +124,9 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     const T* __restrict__ Vs = V + s.v_off;  // [m][R]
 
     if (t.mode == ENC_TILE) {
-        // LDS: tile [nrows*m] then V [m][R]
-        float* tile = lds;
-        float* vl = lds + kTileRows * m;
+        // LDS: V [m][R] (padded to 16 B), then the tile [nrows*m]
+        float* vl = lds;
+        float* tile = lds + ((m * R + 3) & ~3);
         for (int i = tid; i < m * R; i += 256) vl[i] = to_f(Vs[i]);
         const int64_t base = s.offset + t.row0 * m;
         const int cnt = (int)t.nrows * m;
@@ -160,17 +166,25 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
             tile[i] = x;
         }
         __syncthreads();
-        if (tid < t.nrows) {
+        // thread per row (tiles of up to a few thousand rows for the smallest m)
+        const bool vec_out = (R == 4) && sizeof(T) == 4 && ((s.sketch_off & 3) == 0);
+        for (int rr = tid; rr < t.nrows; rr += 256) {
             float acc[R];
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[j] = 0.f;
-            const float* row = tile + tid * m;
+            const float* row = tile + rr * m;
             for (int c = 0; c < m; ++c) {
                 const float x = row[c];
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = fmaf(x, vl[c * R + j], acc[j]);
             }
-            T* out = sketch + s.sketch_off + (t.row0 + tid) * R;
+            T* out = sketch + s.sketch_off + (t.row0 + rr) * R;
+            if constexpr (R == 4 && sizeof(T) == 4) {
+                if (vec_out) {
+                    *reinterpret_cast<float4*>(out) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+                    continue;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < R; ++j) st1<T>(out + j, acc[j]);
         }
@@ -321,6 +335,145 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     }
 }
 
+// Sum each of R per-lane values over the 64 lanes of a wave.  R = 4: halving exchange (2 +
+// 1 + 4 = 7 cross-lane steps instead of 4 x 6); afterwards lane 16 * j holds sum j
+// (j = 2 * (lane >> 5) + ((lane >> 4) & 1)).  Generic R: every lane holds every sum.
+template <int R>
+__device__ __forceinline__ void wave_sum_r(float (&a)[R], int lane) {
+    if constexpr (R == 4) {
+        const bool hi = lane >= 32;
+        float k0 = hi ? a[2] : a[0], k1 = hi ? a[3] : a[1];
+        const float s0 = hi ? a[0] : a[2], s1 = hi ? a[1] : a[3];
+        k0 += __shfl_xor(s0, 32, 64);
+        k1 += __shfl_xor(s1, 32, 64);
+        const bool odd = (lane & 16) != 0;
+        float c = odd ? k1 : k0;
+        c += __shfl_xor(odd ? k0 : k1, 16, 64);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        a[0] = c;
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j) a[j] = wave_sum(a[j]);
+    }
+}
+
+// K1 encode, wave-per-row tiles (ENC_ROW_VEC: m and the offset 16-B aligned), in a launch of
+// its own so the register budget is this loop's alone.  A wave streams a whole row (up to
+// 64 * kEncRowUnits 16-B units per pass) with every load of the pass issued before its first
+// use, stores E := X with nontemporal stores, and forms the R dot products from V^T in LDS;
+// the other waves of the CU cover the latency (occupancy, not double buffers).
+#ifndef ARCTOPK_ENC_ROW_UNITS
+#define ARCTOPK_ENC_ROW_UNITS 8
+#endif
+#ifndef ARCTOPK_ENC_ROW_WPE
+#define ARCTOPK_ENC_ROW_WPE 4
+#endif
+constexpr int kEncRowUnits = ARCTOPK_ENC_ROW_UNITS;
+template <typename T, int R, int EF, bool ERR_IN>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ARCTOPK_ENC_ROW_WPE)))
+k_encode_rows(const SegDev* __restrict__ segs, const EncTile* __restrict__ tiles,
+              const T* __restrict__ G, T* __restrict__ E, const T* __restrict__ V,
+              T* __restrict__ sketch, float* __restrict__ part_buf) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const EncTile t = tiles[blockIdx.x];
+    const SegDev s = segs[t.seg];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr bool WRITE_E = (EF == ARCTOPK_EF14);
+    constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
+    constexpr int PQ = kQuadsPer16<T>;
+    constexpr int U = kEncRowUnits;
+    const int m = (int)s.m;
+    const int c0 = t.c0, cl = t.clen;
+    const T* __restrict__ Vs = V + s.v_off;
+    if constexpr (R == 4) {
+        for (int c = tid; c < cl; c += 256) {
+            const float4 v = ldq<T, false>(Vs, c0 + c);
+            lds[c] = v.x;
+            lds[cl + c] = v.y;
+            lds[2 * cl + c] = v.z;
+            lds[3 * cl + c] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            for (int c = tid; c < cl; c += 256) lds[j * cl + c] = to_f(Vs[(int64_t)(c0 + c) * R + j]);
+    }
+    __syncthreads();
+    T* const sk_out = sketch + s.sketch_off;
+    float* const pt_out = t.part < 0 ? nullptr : part_buf + s.part_off + (int64_t)t.part * s.n * R;
+    const int m4 = cl >> 2;
+    const int mu = m4 / PQ;
+    const float4* vt4 = reinterpret_cast<const float4*>(lds);
+    for (int64_t q = wave; q < t.nrows; q += 4) {
+        const int64_t row = t.row0 + q * t.rstride;
+        const T* gp = G + s.offset + row * m + c0;
+        T* ep = E + s.offset + row * m + c0;
+        float acc[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[j] = 0.f;
+        for (int cb = 0; cb < mu; cb += 64 * U) {
+            float4 g[U][PQ], e[U][PQ];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (cb + u * 64 < mu) {  // wave-uniform: no loads past the row
+                    const int c = min(cb + u * 64 + lane, mu - 1);
+                    ld16<T, true>(gp, c, g[u]);
+                    if constexpr (LOAD_E) ld16<T, true>(ep, c, e[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (cb + u * 64 < mu) {
+                    const int cu = cb + u * 64 + lane;
+                    const bool ok = cu < mu;
+                    const int c = ok ? cu : mu - 1;
+                    float4 x[PQ];
+#pragma unroll
+                    for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(g[u][h], e[u][h]);
+                    if constexpr (WRITE_E) {
+                        if (ok) st16<T, true>(ep, c, x);
+                    }
+                    if (!ok) {
+#pragma unroll
+                        for (int h = 0; h < PQ; ++h) x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        float a = acc[j];
+#pragma unroll
+                        for (int h = 0; h < PQ; ++h) {
+                            const float4 v = vt4[j * m4 + c * PQ + h];
+                            a = fmaf(x[h].x, v.x, a);
+                            a = fmaf(x[h].y, v.y, a);
+                            a = fmaf(x[h].z, v.z, a);
+                            a = fmaf(x[h].w, v.w, a);
+                        }
+                        acc[j] = a;
+                    }
+                }
+            }
+        }
+        wave_sum_r<R>(acc, lane);
+        if constexpr (R == 4) {
+            if ((lane & 15) == 0) {
+                const int j = ((lane >> 5) << 1) | ((lane >> 4) & 1);
+                if (pt_out) pt_out[row * R + j] = acc[0];
+                else st1<T>(sk_out + row * R + j, acc[0]);
+            }
+        } else {
+            if (lane < R) {
+                float v = acc[0];
+#pragma unroll
+                for (int j = 1; j < R; ++j)
+                    if (lane == j) v = acc[j];
+                if (pt_out) pt_out[row * R + lane] = v;
+                else st1<T>(sk_out + row * R + lane, v);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K2 select
 // ---------------------------------------------------------------------------
@@ -373,7 +526,7 @@ __device__ __forceinline__ float row_energy(const T* __restrict__ p, int R, cons
 // ordered, and every NaN (either sign) maps above +inf, as torch.topk ranks NaN largest.
 __device__ __forceinline__ uint32_t energy_key(float e) {
     uint32_t u = __float_as_uint(e);
-    if (e != e) u = 0xFFFFFFFFu;  // NaN largest
+    if (e != e) u = 0x7FFFFFFFu;  // NaN largest (above +inf 0x7F800000; bit 31 stays clear)
     return u & 0x7FFFFFFFu ? u : 0u;  // -0 cannot occur; keep +0 = 0
 }
 
@@ -432,14 +585,13 @@ __device__ __forceinline__ int64_t block_exscan_s(int64_t v, int64_t* wsum) {
 }
 
 template <typename T, int NT>
-__global__ void __launch_bounds__(NT) k_select_small(const SegDev* __restrict__ segs,
-                                                      const int32_t* __restrict__ seg_ids,
-                                                      const T* __restrict__ sketch, int R,
-                                                      Scale sc, int32_t* __restrict__ rowlist,
-                                                      int32_t* __restrict__ slotmap) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
+__device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs, int32_t seg_id,
+                                                 const T* __restrict__ sketch, int R, Scale sc,
+                                                 int32_t* __restrict__ rowlist,
+                                                 int32_t* __restrict__ slotmap,
+                                                 uint32_t* __restrict__ keys /* LDS, n + 4 */) {
     __shared__ SmallSel sh;
-    const SegDev s = segs[seg_ids[blockIdx.x]];
+    const SegDev s = segs[seg_id];
     const int n = (int)s.n;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
@@ -645,6 +797,201 @@ __global__ void __launch_bounds__(NT) k_select_small(const SegDev* __restrict__ 
     SEL_STAMP(4);
 }
 
+template <typename T, int NT>
+__global__ void __launch_bounds__(NT) k_select_small(const SegDev* __restrict__ segs,
+                                                      const int32_t* __restrict__ seg_ids,
+                                                      const T* __restrict__ sketch, int R,
+                                                      Scale sc, int32_t* __restrict__ rowlist,
+                                                      int32_t* __restrict__ slotmap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
+    select_small_seg<T, NT>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, keys);
+}
+
+// exclusive block scan of one uint32 per thread (NW waves); *total = block sum
+template <int NW>
+__device__ __forceinline__ uint32_t blk_exscan_u32(uint32_t v, uint32_t* lds, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint32_t v2 = lds[w];
+        before += w < wave ? v2 : 0u;
+        tot += v2;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + x - v;
+}
+
+// ARC refine of one large segment (after ms_arc_compact), one 1024-thread block.  The
+// candidates (every key of the first-pass bin, with its index) are staged in LDS (the
+// indices too when they fit); two 10-bit LDS histogram rounds fix the remaining bits of the
+// threshold T; the candidates above / equal to T are counted per range and, with the keys
+// above the bin (compact pass), turned into per-range T-equal allowances (lowest ranges
+// first) and output offsets for ms_arc_write.
+constexpr int kRefineThreads = 1024;
+static_assert(kRefineThreads == kMMaxRanges, "one range per thread in the offset scan");
+__device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspace* ws,
+                                                const uint32_t* __restrict__ ckey,
+                                                const uint32_t* __restrict__ cidx,
+                                                uint32_t* __restrict__ stage /* LDS */) {
+    constexpr int NT = kRefineThreads, NW = NT / 64, U = 8, W2 = 10;
+    constexpr int HALF = kRefineLdsCap / 2;
+    __shared__ uint32_t h[1 << W2];
+    __shared__ uint32_t cgt[kMMaxRanges], ceq[kMMaxRanges];
+    __shared__ uint32_t lds[NW], s_digit, s_acc;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const MItem it = b.it[t];
+    MState s = ws->st[t];
+    const int nr = it.nranges;
+    const uint32_t gt_above = tid < nr ? ws->cnt_gt[t][tid] : 0u;  // prefetched: keys above the bin
+    const int64_t nc = (int64_t)ws->ncand[t].v;
+    const uint32_t* ck = ckey + it.cand_off;
+    const uint32_t* ci = cidx + it.cand_off;
+    cgt[tid] = 0u;
+    ceq[tid] = 0u;
+    if (nc <= kRefineLdsCap) {  // usual case: one round trip, then everything from LDS
+        const bool with_idx = nc <= HALF;
+        for (int64_t base = 0; base < nc; base += (int64_t)NT * U) {
+            uint32_t kv[U], iv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = base + u * NT + tid;
+                kv[u] = i < nc ? ck[i] : 0u;
+                iv[u] = (with_idx && i < nc) ? ci[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = base + u * NT + tid;
+                if (i < nc) {
+                    stage[i] = kv[u];
+                    if (with_idx) stage[HALF + i] = iv[u];
+                }
+            }
+        }
+        __syncthreads();
+        ck = stage;
+        if (with_idx) ci = stage + HALF;
+    }
+    while (s.bit > 0) {
+        const int w = s.bit < W2 ? s.bit : W2;
+        const int shift = s.bit - w;
+        const uint32_t dmask = (1u << w) - 1u;
+        h[tid] = 0u;  // 1 << W2 == NT bins
+        __syncthreads();
+        for (int64_t base = 0; base < nc; base += (int64_t)NT * U) {
+            uint32_t kv[U];  // all loads of a batch in flight before the LDS atomics
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = base + u * NT + tid;
+                kv[u] = i < nc ? ck[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = base + u * NT + tid;
+                if (i < nc && (kv[u] & s.mask) == s.prefix) atomicAdd(&h[(kv[u] >> shift) & dmask], 1u);
+            }
+        }
+        __syncthreads();
+        const int nb = 1 << w;
+        const uint32_t c = tid < nb ? h[nb - 1 - tid] : 0u;  // descending bins
+        uint32_t total;
+        const uint32_t excl = blk_exscan_u32<NW>(c, lds, &total);
+        if ((uint64_t)excl < (uint64_t)s.kk && (uint64_t)excl + c >= (uint64_t)s.kk) {
+            s_digit = (uint32_t)(nb - 1 - tid);
+            s_acc = excl;
+        }
+        __syncthreads();
+        s.prefix |= s_digit << shift;
+        s.mask |= dmask << shift;
+        s.kk -= (int64_t)s_acc;
+        s.bit = shift;
+        __syncthreads();  // s_digit / s_acc / h are rewritten by the next round
+    }
+    const uint32_t T = s.prefix;
+    for (int64_t base = 0; base < nc; base += (int64_t)NT * U) {
+        uint32_t kv[U], iv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + u * NT + tid;
+            kv[u] = i < nc ? ck[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // indices only of the keys that count
+            const int64_t i = base + u * NT + tid;
+            iv[u] = (i < nc && kv[u] >= T) ? ci[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            // segmented wave reduction: a wave's 64 consecutive candidates come from one or
+            // two block tiles of the compact pass, so one LDS atomic pair per distinct range
+            const int64_t i = base + u * NT + tid;
+            const bool valid = i < nc && kv[u] >= T;
+            const int r = valid ? (int)(iv[u] / (uint32_t)it.range) : -1;
+            const bool gt = valid && kv[u] > T;
+            uint64_t pending = __ballot(valid);
+            while (pending) {
+                const int leader = __ffsll((long long)pending) - 1;
+                const int rl = __shfl(r, leader, 64);
+                const bool mine = valid && r == rl;
+                const uint32_t ng = (uint32_t)__popcll(__ballot(mine && gt));
+                const uint32_t ne = (uint32_t)__popcll(__ballot(mine && !gt));
+                if (lane == leader) {
+                    if (ng) atomicAdd(&cgt[rl], ng);
+                    if (ne) atomicAdd(&ceq[rl], ne);
+                }
+                pending &= ~__ballot(mine);
+            }
+        }
+    }
+    __syncthreads();
+    const int r = tid;
+    const uint32_t eq = r < nr ? ceq[r] : 0u;
+    const uint32_t gt = r < nr ? gt_above + cgt[r] : 0u;
+    uint32_t tot;
+    const uint32_t eq_before = blk_exscan_u32<NW>(eq, lds, &tot);
+    int64_t take = s.kk - (int64_t)eq_before;
+    take = take < 0 ? 0 : (take > (int64_t)eq ? (int64_t)eq : take);
+    const uint32_t sel_before = blk_exscan_u32<NW>(gt + (uint32_t)take, lds, &tot);
+    if (r < nr) {
+        ws->take_eq[t][r] = (uint32_t)take;
+        ws->sel_before[t][r] = sel_before;
+    }
+    if (tid == 0) ws->st[t] = s;  // the write pass reads the threshold (prefix)
+}
+
+// The refine of a batch's large segments and, in the same launch, the single-block selects
+// of the small segments (blocks b.cnt ..): both are latency-bound and independent, so they
+// overlap instead of running back to back.
+template <typename T>
+__global__ void __launch_bounds__(kRefineThreads) k_arc_refine(MBatch b, MWorkspace* ws,
+                                                               const uint32_t* __restrict__ ckey,
+                                                               const uint32_t* __restrict__ cidx,
+                                                               const SegDev* __restrict__ segs,
+                                                               const int32_t* __restrict__ small_ids,
+                                                               const T* __restrict__ sketch, int R,
+                                                               Scale sc, int32_t* __restrict__ rowlist,
+                                                               int32_t* __restrict__ slotmap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    if ((int)blockIdx.x < b.cnt)
+        arc_refine_item(b, (int)blockIdx.x, ws, ckey, cidx, dyn);
+    else
+        select_small_seg<T, kRefineThreads>(segs, small_ids[blockIdx.x - b.cnt], sketch, R, sc, rowlist,
+                                            slotmap, dyn);
+}
+
+struct KeysGrid {
+    int32_t first[kMB + 1];  // first block of each item in the flat key-pass grid
+};
+
 // Larger segments: energy keys into global memory, fused with the first radix pass of
 // the multi-block select (mselect.h): each block histograms its keys' top 12 bits in LDS
 // and merges the non-empty bins into the segment's global histogram; the last block to
@@ -653,39 +1000,92 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ segs,
                                                   const int32_t* __restrict__ ids, int first,
                                                   const T* __restrict__ sketch, int R, Scale sc,
-                                                  uint32_t* __restrict__ keys, MWorkspace* ws) {
-    __shared__ uint32_t h[kMBins];
-    const int t = blockIdx.y;
+                                                  uint32_t* __restrict__ keys, MWorkspace* ws,
+                                                  KeysGrid kg) {
+    __shared__ uint32_t h[kMBins], hc[kMBins];
+    __shared__ uint32_t s_nnz;
+    // flat grid: item t owns blocks [kg.first[t], kg.first[t + 1])
+    int t = 0;
+    while ((int)blockIdx.x >= kg.first[t + 1]) ++t;
+    const int bx = (int)blockIdx.x - kg.first[t];
+    const uint32_t nblk = (uint32_t)(kg.first[t + 1] - kg.first[t]);
     const SegDev s = segs[ids[first + t]];
     for (int i = threadIdx.x; i < kMBins; i += 256) h[i] = 0u;
+    if (threadIdx.x == 0) s_nnz = 0u;
     __syncthreads();
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
-    const int64_t gs = (int64_t)gridDim.x * 256;
-    int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t gs = (int64_t)nblk * 256;
+    int64_t row = (int64_t)bx * 256 + threadIdx.x;
     const T* sk = sketch + s.sketch_off;
     uint32_t* kout = keys + s.row_off;
-    if (stride == 4 && (s.sketch_off & 3) == 0) {  // r = 4: one quad load per row, 4 rows in flight
-        for (; row + 3 * gs < s.n; row += 4 * gs) {
-            float4 v[4];
+    if (stride == 4 && (s.sketch_off & 3) == 0) {  // r = 4: one quad load per row, UK rows in flight
+        constexpr int UK = 8;
+        for (; row < s.n; row += UK * gs) {
+            float4 v[UK];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = ldq<T, false>(sk, row + u * gs);
+            for (int u = 0; u < UK; ++u) v[u] = ldq<T, false>(sk, min(row + u * gs, s.n - 1));
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
-                kout[row + u * gs] = key;
+            for (int u = 0; u < UK; ++u) {
+                const int64_t rr = row + u * gs;
+                if (rr < s.n) {
+                    const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
+                    kout[rr] = key;
+#if ARCTOPK_DIAG_KEYS < 2
+                    atomicAdd(&h[key >> kArcShift], 1u);
+#endif
+                }
+            }
+        }
+    }
+    for (; row < s.n; row += 8 * gs) {  // other r / 1-D tensors: 8 rows in flight as well
+        float e[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) e[u] = row_energy(sk + min(row + u * gs, s.n - 1) * stride, R, sc, s.kind);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t rr = row + u * gs;
+            if (rr < s.n) {
+                const uint32_t key = energy_key(e[u]);
+                kout[rr] = key;
                 atomicAdd(&h[key >> kArcShift], 1u);
             }
         }
     }
-    for (; row < s.n; row += gs) {
-        const uint32_t key = energy_key(row_energy(sk + row * stride, R, sc, s.kind));
-        kout[row] = key;
-        atomicAdd(&h[key >> kArcShift], 1u);
-    }
     __syncthreads();
-    for (int i = threadIdx.x; i < kMBins; i += 256)
-        if (h[i]) atomicAdd(&ws->hist[t][hist_slot(i)], h[i]);
-    if (!ms_arrive_last(&ws->done[t].v, gridDim.x)) return;
+#if ARCTOPK_DIAG_KEYS >= 1  // diagnostic builds (scripts/selbench.hip): stop after the LDS pass
+    if (h[threadIdx.x] == 12345678u) kout[0] = 0u;
+    return;
+#endif
+    // Merge into the item's global histogram.  Memory-side atomics cost about one wave
+    // instruction per 50 ns per CU whatever their lane count, so the non-empty bins are first
+    // compacted into a dense LDS list (bins in h, counts in hc) and merged by full wave
+    // instructions: a few per block instead of 64.
+    {
+        constexpr int PB = kMBins / 256;
+        const int lane = threadIdx.x & 63;
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        uint32_t c[PB];
+#pragma unroll
+        for (int q = 0; q < PB; ++q) c[q] = h[q * 256 + threadIdx.x];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+            const bool ne = c[q] != 0u;
+            const uint64_t bm = __ballot(ne);
+            uint32_t base = 0;
+            if (lane == 0 && bm) base = atomicAdd(&s_nnz, (uint32_t)__popcll(bm));
+            base = __shfl(base, 0, 64);
+            if (ne) {
+                const uint32_t pos = base + (uint32_t)__popcll(bm & lt);
+                h[pos] = (uint32_t)(q * 256 + threadIdx.x);
+                hc[pos] = c[q];
+            }
+        }
+        __syncthreads();
+        const uint32_t nnz = s_nnz;
+        for (uint32_t i = threadIdx.x; i < nnz; i += 256) atomicAdd(&ws->hist[t][hist_slot((int)h[i])], hc[i]);
+    }
+    if (!ms_arrive_last(&ws->done[t].v, nblk)) return;
     ms_arc_first_digit(ws, t, s.k_rows);
 }
 
@@ -719,15 +1119,102 @@ __device__ __forceinline__ float4 pack4(const T* __restrict__ G, T* __restrict__
     return v;
 }
 
+// Pack of a row range of an m in {1, 2} fp32 segment (Chunk mode 1): lane per 16-B quad of
+// the segment (4 / 2 rows), slot map read alongside; selected rows go to packed[slot * m],
+// and (EF14 / EF21) the quad of E is rewritten whole when it holds a selected row.
+template <int EF>
+__device__ __forceinline__ void pack_stream_small(const SegDev& s, const Chunk& ch,
+                                                  const float* __restrict__ G, float* __restrict__ E,
+                                                  const int32_t* __restrict__ slotmap,
+                                                  float* __restrict__ packed) {
+    const int m = (int)s.m;
+    const int64_t e0 = s.offset + ch.row0 * m;    // first element (16-B aligned)
+    const int nq = (int)((ch.nrows * m + 3) >> 2);  // quads (the last may run past the segment)
+    const int64_t seg_end = s.offset + s.n * m;
+    const int32_t* sm = slotmap + s.row_off;
+    float* pk = packed + s.packed_off;
+    constexpr int UQ = 4;
+    for (int q0 = threadIdx.x; q0 < nq; q0 += 256 * UQ) {
+        float4 g[UQ], e[UQ];
+        int32_t sl[UQ][4];
+#pragma unroll
+        for (int u = 0; u < UQ; ++u) {
+            const int q = min(q0 + u * 256, nq - 1);
+            const int64_t el = e0 + 4 * (int64_t)q;
+            if (el + 4 <= seg_end) {
+                if constexpr (EF != ARCTOPK_EF14) g[u] = *reinterpret_cast<const float4*>(G + el);
+                if constexpr (EF != ARCTOPK_EF_NONE) e[u] = *reinterpret_cast<const float4*>(E + el);
+            } else {  // segment tail: scalar, zero-filled
+                float gv[4] = {0.f, 0.f, 0.f, 0.f}, ev[4] = {0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < 4 && el + j < seg_end; ++j) {
+                    if constexpr (EF != ARCTOPK_EF14) gv[j] = G[el + j];
+                    if constexpr (EF != ARCTOPK_EF_NONE) ev[j] = E[el + j];
+                }
+                g[u] = make_float4(gv[0], gv[1], gv[2], gv[3]);
+                e[u] = make_float4(ev[0], ev[1], ev[2], ev[3]);
+            }
+            const int64_t r0 = (el - s.offset) / m;  // first row of the quad
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sl[u][j] = (j < 4 / m && r0 + j < s.n) ? sm[r0 + j] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < UQ; ++u) {
+            const int q = q0 + u * 256;
+            if (q >= nq) break;
+            const int64_t el = e0 + 4 * (int64_t)q;
+            const float gv[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+            const float ev[4] = {e[u].x, e[u].y, e[u].z, e[u].w};
+            float en[4] = {ev[0], ev[1], ev[2], ev[3]};
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int rj = j / m;  // row of element j within the quad
+                const int32_t slot = sl[u][rj];
+                if (slot >= 0) {
+                    float v;
+                    if constexpr (EF == ARCTOPK_EF_NONE) {
+                        v = gv[j];
+                    } else if constexpr (EF == ARCTOPK_EF14) {
+                        v = ev[j];
+                        en[j] = 0.f;
+                    } else {
+                        v = gv[j] - ev[j];
+                        en[j] = ev[j] + v;
+                    }
+                    pk[(int64_t)slot * m + (j - rj * m)] = v;
+                    any = true;
+                }
+            }
+            if constexpr (EF != ARCTOPK_EF_NONE) {
+                if (any) {
+                    if (el + 4 <= seg_end) {
+                        *reinterpret_cast<float4*>(E + el) = make_float4(en[0], en[1], en[2], en[3]);
+                    } else {
+                        for (int j = 0; j < 4 && el + j < seg_end; ++j) E[el + j] = en[j];
+                    }
+                }
+            }
+        }
+    }
+}
+
 template <typename T, int EF>
 __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                                               const Chunk* __restrict__ chunks,
                                               const T* __restrict__ G, T* __restrict__ E,
                                               const int32_t* __restrict__ rowlist,
+                                              const int32_t* __restrict__ slotmap,
                                               T* __restrict__ packed) {
     const Chunk ch = chunks[blockIdx.x];
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
+    if constexpr (sizeof(T) == 4) {
+        if (ch.mode == 1) {  // m in {1, 2}: stream every row's quad of E / G with the slot map
+            pack_stream_small<EF>(s, ch, reinterpret_cast<const float*>(G), reinterpret_cast<float*>(E),
+                                  slotmap, reinterpret_cast<float*>(packed));
+            return;
+        }
+    }
     const int32_t* rl = rowlist + s.sel_off + ch.row0;
     T* dst = packed + s.packed_off + ch.row0 * m;
     if (row_path(s)) {  // wave per selected row: all of a row's loads first, then stores
@@ -843,6 +1330,47 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
         for (uint32_t e = (uint32_t)pre + (body << 2) + threadIdx.x; e < cnt; e += 256) st1<T>(dst + e, one(e));
         return;
     }
+    if (m <= 3) {  // 1-D tensors (m = 1) and 1x1-conv rows (m = 2): thread per selected row,
+                   // every gather load of a round issued before its stores
+        constexpr int UR = 8;
+        const int nr = (int)ch.nrows;
+        for (int j0 = threadIdx.x; j0 < nr; j0 += 256 * UR) {
+            int64_t src[UR];
+            float va[UR][3], vb[UR][3];
+#pragma unroll
+            for (int u = 0; u < UR; ++u) {
+                src[u] = s.offset + (int64_t)rl[min(j0 + u * 256, nr - 1)] * m;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (c < m) {
+                        if constexpr (EF == ARCTOPK_EF_NONE) va[u][c] = ld1<T>(G + src[u] + c);
+                        else if constexpr (EF == ARCTOPK_EF14) va[u][c] = ld1<T>(E + src[u] + c);
+                        else { va[u][c] = ld1<T>(G + src[u] + c); vb[u][c] = ld1<T>(E + src[u] + c); }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UR; ++u) {
+                const int j = j0 + u * 256;
+                if (j < nr) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        if (c < m) {
+                            float v = va[u][c];
+                            if constexpr (EF == ARCTOPK_EF14) {
+                                st1<T>(E + src[u] + c, 0.f);
+                            } else if constexpr (EF == ARCTOPK_EF21) {
+                                v = rnd<T>(va[u][c] - vb[u][c]);
+                                st1<T>(E + src[u] + c, vb[u][c] + v);
+                            }
+                            st1<T>(dst + (int64_t)j * m + c, v);
+                        }
+                    }
+                }
+            }
+        }
+        return;
+    }
     const uint32_t cnt = (uint32_t)(ch.nrows * m);
     if (s.vec) {
         const uint32_t cnt4 = cnt >> 2;
@@ -893,6 +1421,57 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
     const int64_t base = s.offset + ch.row0 * m;
     const int32_t* sm = slotmap + s.row_off + ch.row0;
     const T* pk = packed + s.packed_off;
+    if constexpr (sizeof(T) == 4) {
+        if (ch.mode == 1) {  // m in {1, 2}, 16-B aligned: lane per output quad
+            const int nq = (int)((ch.nrows * m + 3) >> 2);
+            const int64_t seg_end = s.offset + s.n * m;
+            constexpr int UQ = 4;
+            for (int q0 = threadIdx.x; q0 < nq; q0 += 256 * UQ) {
+                int32_t sl[UQ][4];
+                float pv[UQ][4], gv[UQ][4];
+#pragma unroll
+                for (int u = 0; u < UQ; ++u) {
+                    const int q = min(q0 + u * 256, nq - 1);
+                    const int rq = (4 * q) / m;  // first row of the quad within the chunk
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) sl[u][j] = (j < 4 / m && ch.row0 + rq + j < s.n) ? sm[rq + j] : -1;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int32_t slot = sl[u][j / m];
+                        pv[u][j] = slot >= 0 ? to_f(pk[(int64_t)slot * m + (j % m)]) : 0.f;
+                    }
+                    if constexpr (EF == ARCTOPK_EF21) {
+                        const int64_t el = base + 4 * (int64_t)q;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) gv[u][j] = el + j < seg_end ? to_f(gE[el + j]) : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UQ; ++u) {
+                    const int q = q0 + u * 256;
+                    if (q >= nq) break;
+                    const int64_t el = base + 4 * (int64_t)q;
+                    float o[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const bool sel = sl[u][j / m] >= 0;
+                        float v = sel ? mean1(pv[u][j]) : 0.f;
+                        if constexpr (EF == ARCTOPK_EF21) {
+                            v = rnd<T>(gv[u][j] + v);
+                            if (sel && el + j < seg_end) st1<T>(gE + el + j, v);
+                        }
+                        o[j] = v;
+                    }
+                    if (el + 4 <= seg_end) {
+                        stq<T, kNtDecode>(out + el, 0, make_float4(o[0], o[1], o[2], o[3]));
+                    } else {
+                        for (int j = 0; j < 4 && el + j < seg_end; ++j) st1<T>(out + el + j, o[j]);
+                    }
+                }
+            }
+            return;
+        }
+    }
     if (row_path(s)) {  // wave per row: one slot lookup per row, float4 streams
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const int m4 = m >> 2;
@@ -1014,6 +1593,40 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
         }
         return;
     }
+    if (m <= 3) {  // 1-D tensors and 1x1-conv rows: thread per row, slot lookups batched
+        constexpr int UR = 4;
+        const int nr = (int)ch.nrows;
+        for (int r0 = threadIdx.x; r0 < nr; r0 += 256 * UR) {
+            int32_t sl[UR];
+            float pv[UR][3];
+#pragma unroll
+            for (int u = 0; u < UR; ++u) sl[u] = sm[min(r0 + u * 256, nr - 1)];
+#pragma unroll
+            for (int u = 0; u < UR; ++u)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    pv[u][c] = (c < m && sl[u] >= 0) ? to_f(pk[(int64_t)sl[u] * m + c]) : 0.f;
+#pragma unroll
+            for (int u = 0; u < UR; ++u) {
+                const int r = r0 + u * 256;
+                if (r < nr) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        if (c < m) {
+                            const int64_t e = base + (int64_t)r * m + c;
+                            float v = sl[u] >= 0 ? mean1(pv[u][c]) : 0.f;
+                            if constexpr (EF == ARCTOPK_EF21) {
+                                v = rnd<T>(ld1<T>(gE + e) + v);
+                                if (sl[u] >= 0) st1<T>(gE + e, v);
+                            }
+                            st1<T>(out + e, v);
+                        }
+                    }
+                }
+            }
+        }
+        return;
+    }
     const uint32_t cnt = (uint32_t)(ch.nrows * m);
     if (s.vec) {
         const uint32_t cnt4 = cnt >> 2;
@@ -1087,6 +1700,22 @@ __global__ void __launch_bounds__(256) k_sketch_combine(const SegDev* __restrict
 template <typename T, int R>
 int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
                     hipStream_t st) {
+    if (p->n_enc_rows > 0) {  // wave-per-row tiles
+        dim3 grid(p->n_enc_rows), block(256);
+        const size_t lds = (size_t)p->enc_rows_lds_bytes;
+        const EncTile* tiles = p->d_enc_rows;
+        float* pb = p->d_part;
+        if (ef == ARCTOPK_EF_NONE)
+            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        else if (ef == ARCTOPK_EF14 && err_in)
+            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        else if (ef == ARCTOPK_EF14)
+            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        else
+            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+        const int e = (int)hipGetLastError();
+        if (e) return e;
+    }
     if (p->n_enc > 0) {
         dim3 grid(p->n_enc), block(256);
         const size_t lds = (size_t)p->enc_lds_bytes;
@@ -1154,7 +1783,11 @@ template <typename T>
 int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_t* rowlist, int32_t* slotmap,
                   hipStream_t st) {
     const T* sketch = static_cast<const T*>(sketch_);
-    if (p->n_small) {
+#ifndef ARCTOPK_DIAG_NOSMALL
+#define ARCTOPK_DIAG_NOSMALL 0  // diagnostic builds only: skip the single-block select
+#endif
+    // with large segments, the small segments' selects run inside the first batch's refine
+    if (p->n_small && !ARCTOPK_DIAG_NOSMALL && p->n_large_batches == 0) {
         // one block per segment: 1024 threads once a segment has more than 4096 rows (the
         // radix rounds and the compaction are per-block latency chains)
         static const int64_t big_rows = [] {  // tuning switch (A/B): rows for 1024 threads
@@ -1174,12 +1807,43 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         for (int i = 0; i < b.cnt; ++i) maxn = std::max<int64_t>(maxn, b.it[i].n);
         // >= 32 rows per lane: few blocks per segment keep the global histogram merge
         // (one memory-side atomic per non-empty bin and block) short
-        int64_t rpb = 8192;  // tuning switch (A/B): rows per block
-        if (const char* env = std::getenv("ARCTOPK_KEYS_ROWS_PER_BLOCK")) rpb = std::max(256, std::atoi(env));
-        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + rpb - 1) / rpb));
-        hipLaunchKernelGGL(k_arc_keys<T>, dim3(gx, b.cnt), dim3(256), 0, st, p->d_segs, p->d_large,
-                           bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws);
-        int e = ms_select_arc(b, p->d_keys, p->d_mws, p->mws_cap, rowlist, slotmap, st);
+        // rows per block: 8 per lane (one round of loads in flight) for latency; the histogram
+        // merge is a few compacted atomic instructions per block, so many blocks are cheap
+        static const int64_t rpb_env = [] {  // tuning switch (A/B): rows per block
+            const char* env = std::getenv("ARCTOPK_KEYS_ROWS_PER_BLOCK");
+            return env ? std::max(256, std::atoi(env)) : 2048;
+        }();
+        // ... but every block merges the same hot bins, and memory-side atomics serialise per
+        // word: an item gets at most kmax blocks (measured: 2048 rows per block for a 131 K-row
+        // item 36 vs 47 us at 8192; a 1 M-row item wants ~8192)
+        static const int64_t kmax = [] {  // tuning switch (A/B): blocks per item
+            const char* env = std::getenv("ARCTOPK_KEYS_MAX_BLOCKS");
+            return env ? std::max(1, std::atoi(env)) : 128;
+        }();
+        KeysGrid kg;
+        kg.first[0] = 0;
+        for (int i = 0; i < b.cnt; ++i)
+            kg.first[i + 1] = kg.first[i] + (int32_t)std::max<int64_t>(
+                1, std::min<int64_t>(std::min<int64_t>(kmax, kMHistBlocks), (b.it[i].n + rpb_env - 1) / rpb_env));
+        hipLaunchKernelGGL(k_arc_keys<T>, dim3(kg.first[b.cnt]), dim3(256), 0, st, p->d_segs, p->d_large,
+                           bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg);
+#if ARCTOPK_DIAG_STOP == 1 || ARCTOPK_DIAG_KEYS >= 1  // diagnostic builds only
+        continue;
+#endif
+        int e = ms_arc_compact(b, p->d_keys, p->d_mws, p->mws_cap, st);
+        if (e) return e;
+        static const hipError_t lds_ok = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&k_arc_refine<T>), hipFuncAttributeMaxDynamicSharedMemorySize,
+            kRefineLdsCap * 4);
+        if (lds_ok != hipSuccess) return (int)lds_ok;
+        const int nsm = (bi == 0 && !ARCTOPK_DIAG_NOSMALL) ? p->n_small : 0;
+        uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
+        hipLaunchKernelGGL(k_arc_refine<T>, dim3(b.cnt + nsm), dim3(kRefineThreads), (size_t)kRefineLdsCap * 4,
+                           st, b, p->d_mws, ckey, ckey + p->mws_cap, p->d_segs, p->d_small, sketch, p->r,
+                           make_scale(ws), rowlist, slotmap);
+        e = (int)hipGetLastError();
+        if (e) return e;
+        e = ms_arc_write(b, p->d_keys, p->d_mws, p->mws_cap, rowlist, slotmap, st);
         if (e) return e;
     }
     return (int)hipGetLastError();
@@ -1187,18 +1851,18 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
 
 template <typename T>
 int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* err_, int32_t ef,
-                const int32_t* rowlist, void* packed_, hipStream_t st) {
+                const int32_t* rowlist, const int32_t* slotmap, void* packed_, hipStream_t st) {
     const T* grad = static_cast<const T*>(grad_);
     T* err = static_cast<T*>(err_);
     T* packed = static_cast<T*>(packed_);
     dim3 grid(c1 - c0), block(256);
     const Chunk* ch = p->d_pack + c0;
     if (ef == ARCTOPK_EF_NONE)
-        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF_NONE>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
+        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF_NONE>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
     else if (ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF14>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
+        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF14>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
     else if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF21>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, packed);
+        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF21>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -1254,8 +1918,9 @@ extern "C" int arctopk_select(const arctopk_plan* p, const void* sketch, int32_t
 
 extern "C" int arctopk_pack_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,
                                      const void* grad, void* err, int32_t ef,
-                                     const int32_t* rowlist, void* packed, void* stream) {
-    if (!p || !rowlist || !packed) return ARCTOPK_EINVAL;
+                                     const int32_t* rowlist, const int32_t* slotmap, void* packed,
+                                     void* stream) {
+    if (!p || !rowlist || !slotmap || !packed) return ARCTOPK_EINVAL;
     if (seg_begin < 0 || seg_end > p->nseg || seg_begin > seg_end) return ARCTOPK_EINVAL;
     if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF_NONE ? !grad : !err) return ARCTOPK_EINVAL;
@@ -1263,14 +1928,14 @@ extern "C" int arctopk_pack_segments(const arctopk_plan* p, int32_t seg_begin, i
     const int c0 = p->h_pack_begin[seg_begin], c1 = p->h_pack_begin[seg_end];
     if (c1 == c0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (p->dtype == ARCTOPK_BF16) return launch_pack<bf16_t>(p, c0, c1, grad, err, ef, rowlist, packed, st);
-    return launch_pack<float>(p, c0, c1, grad, err, ef, rowlist, packed, st);
+    if (p->dtype == ARCTOPK_BF16) return launch_pack<bf16_t>(p, c0, c1, grad, err, ef, rowlist, slotmap, packed, st);
+    return launch_pack<float>(p, c0, c1, grad, err, ef, rowlist, slotmap, packed, st);
 }
 
 extern "C" int arctopk_pack(const arctopk_plan* p, const void* grad, void* err, int32_t ef,
-                            const int32_t* rowlist, void* packed, void* stream) {
+                            const int32_t* rowlist, const int32_t* slotmap, void* packed, void* stream) {
     if (!p) return ARCTOPK_EINVAL;
-    return arctopk_pack_segments(p, 0, p->nseg, grad, err, ef, rowlist, packed, stream);
+    return arctopk_pack_segments(p, 0, p->nseg, grad, err, ef, rowlist, slotmap, packed, stream);
 }
 
 extern "C" int arctopk_decode_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,

@@ -8,7 +8,11 @@
 namespace arctopk {
 
 constexpr int kMaxR = 8;           // sketch rank supported by the kernels
-constexpr int kTileRows = 256;     // rows of one small-m encode tile (thread per row)
+constexpr int kTileRows = 256;     // row granule of a small-m encode tile (thread per row)
+#ifndef ARCTOPK_SMALL_TILE_BYTES
+#define ARCTOPK_SMALL_TILE_BYTES 32768
+#endif
+constexpr int kSmallTileBytes = ARCTOPK_SMALL_TILE_BYTES;  // tensor bytes per small-m encode tile
 constexpr int kSmallM = 64;        // m below this: thread-per-row tiles; else wave-per-row
 constexpr int kVLdsMaxBytes = 64 * 1024;  // V staged in LDS up to this size, else read from L2
 constexpr int kChunkElems = 8192;  // target elements per pack/decode work chunk (8192 beat
@@ -212,9 +216,9 @@ struct EncTile {
                        // advancing window of the tensor instead of scattered row ranges)
 };
 
-struct Chunk {         // pack: selected-row range; decode: row range
+struct Chunk {         // pack: selected-row range (mode 0) or row range (mode 1); decode: row range
     int32_t seg;
-    int32_t pad;
+    int32_t mode;      // 1: m in {1, 2}, fp32, 16-B aligned: quad streams over every row
     int64_t row0;
     int64_t nrows;
 };
@@ -232,9 +236,12 @@ struct arctopk_plan {
     arctopk_plan_info info;
     arctopk_segment* h_segs;      // host copy
     arctopk::SegDev* d_segs;
-    arctopk::EncTile* d_enc;
+    arctopk::EncTile* d_enc;      // RAW / small-m / scalar-row tiles (k_encode)
     int n_enc;
     int enc_lds_bytes;            // dynamic LDS of the encode launch
+    arctopk::EncTile* d_enc_rows; // 16-B aligned wave-per-row tiles (k_encode_rows)
+    int n_enc_rows;
+    int enc_rows_lds_bytes;
     float* d_part;                // partial sketches of column-split segments
     int32_t* d_split;             // ids of column-split segments
     int n_split;

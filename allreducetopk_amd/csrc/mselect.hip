@@ -34,6 +34,28 @@ __device__ __forceinline__ uint32_t key_of(uint32_t bits) {
 
 __device__ __forceinline__ uint32_t popc64(uint64_t v) { return (uint32_t)__popcll(v); }
 
+// Flat grids of the per-range kernels: block x is range r of item t, items back to back
+// (no idle blocks padding small items up to the largest item's range count).
+__device__ __forceinline__ bool ms_locate(const MBatch& b, int* t, int* r) {
+    int x = (int)blockIdx.x;
+    for (int i = 0; i < b.cnt; ++i) {
+        const int nr = b.it[i].nranges;
+        if (x < nr) {
+            *t = i;
+            *r = x;
+            return true;
+        }
+        x -= nr;
+    }
+    return false;
+}
+
+static int total_ranges(const MBatch& b) {
+    int n = 0;
+    for (int i = 0; i < b.cnt; ++i) n += b.it[i].nranges;
+    return n;
+}
+
 // exclusive block scan of one uint32 per thread (NW waves); *total = block sum
 template <int NW>
 __device__ __forceinline__ uint32_t block_exscan_u32(uint32_t v, uint32_t* lds, uint32_t* total) {
@@ -163,10 +185,9 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
                                                     uint32_t* __restrict__ ckey,
                                                     uint32_t* __restrict__ cidx) {
     __shared__ uint32_t lds[4], s_cnt[4], s_base;
-    const int t = blockIdx.y;
+    int t, r;
+    if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
-    const int r = blockIdx.x;
-    if (r >= it.nranges) return;
     const MState s = ws->st[t];
     const uint32_t hi = s.p1 | ~s.m1;  // largest key of the bin
     const int64_t r0 = (int64_t)r * it.range;
@@ -326,10 +347,9 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
                                                   float* __restrict__ out_val,
                                                   int32_t* __restrict__ out_slot) {
     __shared__ uint32_t s_eq[4], s_gt[4];
-    const int t = blockIdx.y;
+    int t, r;
+    if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
-    const int r = blockIdx.x;
-    if (r >= it.nranges) return;
     const uint32_t T = ws->st[t].prefix;
     uint32_t take_left = ws->take_eq[t][r];
     int64_t run = ws->sel_before[t][r];
@@ -394,142 +414,6 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
     }
 }
 
-// ARC, after compact: one 1024-thread block per item.  The candidates (every key of the
-// first-pass bin, with its index) are few and hot in L2: the block fixes the remaining
-// 20 bits in two 10-bit LDS histogram rounds, then counts the candidates above / equal to
-// the threshold per range and turns the counts into per-range T-equal allowances (lowest
-// ranges first) and output offsets, as k_ms_count's last block does.
-constexpr int kRefineThreads = 1024;
-constexpr int kRefineU = 8;  // candidates per thread in flight
-constexpr int kRefineLdsCap = 12288;  // candidate keys staged in LDS (48 KiB, + ~12 KiB static)
-static_assert(kRefineThreads == kMMaxRanges, "one range per thread in the offset scan");
-
-__global__ void __launch_bounds__(kRefineThreads) k_ms_refine(MBatch b, MWorkspace* ws,
-                                                              const uint32_t* __restrict__ ckey,
-                                                              const uint32_t* __restrict__ cidx) {
-    constexpr int NW = kRefineThreads / 64;
-    __shared__ uint32_t h[1 << kW2];
-    __shared__ uint32_t cgt[kMMaxRanges], ceq[kMMaxRanges];
-    __shared__ uint32_t lds[NW], s_digit, s_acc;
-    const int t = blockIdx.x;
-    const int tid = threadIdx.x;
-    const MItem it = b.it[t];
-    MState s = ws->st[t];
-    const int64_t nc = (int64_t)ws->ncand[t].v;
-    const uint32_t* ck = ckey + it.cand_off;
-    const uint32_t* ci = cidx + it.cand_off;
-    if (nc <= kRefineLdsCap) {  // usual case: stage the candidate keys in LDS, one round trip
-        extern __shared__ uint32_t stage[];
-        for (int64_t base = 0; base < nc; base += (int64_t)kRefineThreads * kRefineU) {
-            uint32_t kv[kRefineU];
-#pragma unroll
-            for (int u = 0; u < kRefineU; ++u) {
-                const int64_t i = base + u * kRefineThreads + tid;
-                kv[u] = i < nc ? ck[i] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < kRefineU; ++u) {
-                const int64_t i = base + u * kRefineThreads + tid;
-                if (i < nc) stage[i] = kv[u];
-            }
-        }
-        __syncthreads();
-        ck = stage;  // a flat pointer into LDS from here on
-    }
-    while (s.bit > 0) {
-        const int w = s.bit < kW2 ? s.bit : kW2;
-        const int shift = s.bit - w;
-        const uint32_t dmask = (1u << w) - 1u;
-        h[tid] = 0u;  // 1 << kW2 == kRefineThreads bins
-        __syncthreads();
-        for (int64_t base = 0; base < nc; base += (int64_t)kRefineThreads * kRefineU) {
-            uint32_t kv[kRefineU];  // all loads of a batch in flight before the LDS atomics
-#pragma unroll
-            for (int u = 0; u < kRefineU; ++u) {
-                const int64_t i = base + u * kRefineThreads + tid;
-                kv[u] = i < nc ? ck[i] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < kRefineU; ++u) {
-                const int64_t i = base + u * kRefineThreads + tid;
-                if (i < nc && (kv[u] & s.mask) == s.prefix) atomicAdd(&h[(kv[u] >> shift) & dmask], 1u);
-            }
-        }
-        __syncthreads();
-        const int nb = 1 << w;
-        const uint32_t c = tid < nb ? h[nb - 1 - tid] : 0u;  // descending bins
-        uint32_t total;
-        const uint32_t excl = block_exscan_u32<NW>(c, lds, &total);
-        if ((uint64_t)excl < (uint64_t)s.kk && (uint64_t)excl + c >= (uint64_t)s.kk) {
-            s_digit = (uint32_t)(nb - 1 - tid);
-            s_acc = excl;
-        }
-        __syncthreads();
-        s.prefix |= s_digit << shift;
-        s.mask |= dmask << shift;
-        s.kk -= (int64_t)s_acc;
-        s.bit = shift;
-        __syncthreads();  // s_digit / s_acc / h are rewritten by the next round
-    }
-    const uint32_t T = s.prefix;
-    const int nr = it.nranges;
-    for (int r = tid; r < kMMaxRanges; r += kRefineThreads) {
-        cgt[r] = 0u;
-        ceq[r] = 0u;
-    }
-    __syncthreads();
-    for (int64_t base = 0; base < nc; base += (int64_t)kRefineThreads * kRefineU) {
-        uint32_t kv[kRefineU], iv[kRefineU];
-#pragma unroll
-        for (int u = 0; u < kRefineU; ++u) {
-            const int64_t i = base + u * kRefineThreads + tid;
-            kv[u] = i < nc ? ck[i] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kRefineU; ++u) {  // indices only of the keys that count
-            const int64_t i = base + u * kRefineThreads + tid;
-            iv[u] = (i < nc && kv[u] >= T) ? ci[i] : 0u;
-        }
-        const int lane = tid & 63;
-#pragma unroll
-        for (int u = 0; u < kRefineU; ++u) {
-            // segmented wave reduction: a wave's 64 consecutive candidates come from one or
-            // two block tiles of the compact pass, so one LDS atomic pair per distinct range
-            const int64_t i = base + u * kRefineThreads + tid;
-            const bool valid = i < nc && kv[u] >= T;
-            const int r = valid ? (int)(iv[u] / (uint32_t)it.range) : -1;
-            const bool gt = valid && kv[u] > T;
-            uint64_t pending = __ballot(valid);
-            while (pending) {
-                const int leader = __ffsll((long long)pending) - 1;
-                const int rl = __shfl(r, leader, 64);
-                const bool mine = valid && r == rl;
-                const uint32_t ng = popc64(__ballot(mine && gt));
-                const uint32_t ne = popc64(__ballot(mine && !gt));
-                if (lane == leader) {
-                    if (ng) atomicAdd(&cgt[rl], ng);
-                    if (ne) atomicAdd(&ceq[rl], ne);
-                }
-                pending &= ~__ballot(mine);
-            }
-        }
-    }
-    __syncthreads();
-    const int r = tid;
-    const uint32_t eq = r < nr ? ceq[r] : 0u;
-    const uint32_t gt = r < nr ? ws->cnt_gt[t][r] + cgt[r] : 0u;  // + keys above the bin
-    uint32_t tot;
-    const uint32_t eq_before = block_exscan_u32<NW>(eq, lds, &tot);
-    int64_t take = s.kk - (int64_t)eq_before;
-    take = take < 0 ? 0 : (take > (int64_t)eq ? (int64_t)eq : take);
-    const uint32_t sel_before = block_exscan_u32<NW>(gt + (uint32_t)take, lds, &tot);
-    if (r < nr) {
-        ws->take_eq[t][r] = (uint32_t)take;
-        ws->sel_before[t][r] = sel_before;
-    }
-    if (tid == 0) ws->st[t] = s;  // the write pass reads the threshold (prefix)
-}
-
 }  // namespace
 
 void ms_item_geometry(MItem& it) {
@@ -562,16 +446,16 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
     uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
     uint32_t* cidx = ckey + cap_total;
     const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + 8191) / 8192));
-    const dim3 gh(hb, cnt), gt(gr, cnt);
+    const dim3 gh(hb, cnt), gt(gr, cnt), gflat(total_ranges(b));
 #define MS_LAUNCH(FF, AR)                                                                              \
     do {                                                                                               \
         if (!AR) hipLaunchKernelGGL(k_ms_init, dim3(cnt), dim3(256), 0, st, b, ws);                    \
         hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
-        hipLaunchKernelGGL(k_ms_compact<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);        \
+        hipLaunchKernelGGL(k_ms_compact<FF>, gflat, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);     \
         hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
         hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
         hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);          \
-        hipLaunchKernelGGL((k_ms_write<FF, AR>), gt, dim3(256), 0, st, b, keys, x, ws, out_idx,        \
+        hipLaunchKernelGGL((k_ms_write<FF, AR>), gflat, dim3(256), 0, st, b, keys, x, ws, out_idx,     \
                            out_val, out_slot);                                                         \
     } while (0)
     if (arc)
@@ -582,26 +466,37 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
     return (int)hipGetLastError();
 }
 
-int ms_select_arc(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
-                  int32_t* out_idx, int32_t* out_slot, hipStream_t st) {
-    const int cnt = b.cnt;
-    if (cnt < 1) return 0;
-    int gr = 1;
-    for (int i = 0; i < cnt; ++i) {
+static int arc_batch_check(const MBatch& b, int64_t cap_total, int* gr) {
+    *gr = 1;
+    for (int i = 0; i < b.cnt; ++i) {
         const MItem& it = b.it[i];
         if (it.nranges < 1 || it.nranges > kMMaxRanges || it.cand_off < 0 || it.cand_cap < it.n ||
             it.cand_off + it.cand_cap > cap_total || (int64_t)it.range * it.nranges < it.n)
             return 1001;  // ARCTOPK_EINVAL: ARC items need cand_cap >= n
-        gr = std::max(gr, it.nranges);
+        *gr = std::max(*gr, it.nranges);
     }
+    return 0;
+}
+
+int ms_arc_compact(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+                   hipStream_t st) {
+    if (b.cnt < 1) return 0;
+    int gr;
+    if (int e = arc_batch_check(b, cap_total, &gr)) return e;
     uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
     uint32_t* cidx = ckey + cap_total;
-    const dim3 gt(gr, cnt);
-    hipLaunchKernelGGL(k_ms_compact<false>, gt, dim3(256), 0, st, b, keys, nullptr, ws, ckey, cidx);
-    hipLaunchKernelGGL(k_ms_refine, dim3(cnt), dim3(kRefineThreads), (size_t)kRefineLdsCap * 4, st, b, ws,
-                       ckey, cidx);
-    hipLaunchKernelGGL((k_ms_write<false, true>), gt, dim3(256), 0, st, b, keys, nullptr, ws, out_idx,
-                       nullptr, out_slot);
+    hipLaunchKernelGGL(k_ms_compact<false>, dim3(total_ranges(b)), dim3(256), 0, st, b, keys, nullptr, ws, ckey,
+                       cidx);
+    return (int)hipGetLastError();
+}
+
+int ms_arc_write(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+                 int32_t* out_idx, int32_t* out_slot, hipStream_t st) {
+    if (b.cnt < 1) return 0;
+    int gr;
+    if (int e = arc_batch_check(b, cap_total, &gr)) return e;
+    hipLaunchKernelGGL((k_ms_write<false, true>), dim3(total_ranges(b)), dim3(256), 0, st, b, keys, nullptr, ws,
+                       out_idx, nullptr, out_slot);
     return (int)hipGetLastError();
 }
 

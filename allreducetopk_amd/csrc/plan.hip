@@ -12,6 +12,11 @@
 
 using namespace arctopk;
 
+#ifndef ARCTOPK_ENC_ROWS_KERNEL
+#define ARCTOPK_ENC_ROWS_KERNEL 1  // A/B switch: 0 = row tiles in the general encode kernel
+#endif
+constexpr bool kEncRowsKernel = ARCTOPK_ENC_ROWS_KERNEL != 0;
+
 namespace {
 
 int build_segments(const int64_t* dims, const int32_t* ndims, int32_t ntensors, int r, double ratio,
@@ -97,7 +102,8 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     std::vector<SegDev> dsegs(segs.size());
     std::vector<int32_t> small_ids, large_ids, split_ids;
     int64_t small_rows = 0;
-    std::vector<EncTile> enc;
+    std::vector<EncTile> enc, enc_rows;
+    int rows_lds = 0;
     std::vector<Chunk> pack, dec;
     std::vector<int32_t> pack_begin, dec_begin;
     int lds = 0;
@@ -144,10 +150,13 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             for (int64_t e = 0; e < s.n; e += per)
                 enc.push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e), 0, 1, -1, 1});
         } else if (s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536) {
-            for (int64_t row = 0; row < s.n; row += kTileRows)
-                enc.push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(kTileRows, s.n - row),
+            // rows per tile: ~kSmallTileBytes of the tensor (multiples of 256 rows), so the
+            // smallest m (1x1 convs, m = 2) does not run thousands of 2 KiB blocks
+            const int64_t tr = std::max<int64_t>(kTileRows, kSmallTileBytes / (4 * s.m) / kTileRows * kTileRows);
+            for (int64_t row = 0; row < s.n; row += tr)
+                enc.push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(tr, s.n - row),
                                       0, (int32_t)s.m, -1, 1});
-            lds = std::max<int>(lds, (int)(kTileRows * s.m * 4 + s.m * r * 4));
+            lds = std::max<int>(lds, (int)(std::min(tr, s.n) * s.m * 4 + ((s.m * r + 3) & ~3) * 4));
         } else {
             const int mode = g.vec ? ENC_ROW_VEC : ENC_ROW_SCALAR;
             // columns per part: V^T slice [r][clen] within kVLdsMaxBytes (multiple of 4)
@@ -167,16 +176,18 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             for (int part = 0; part < nparts; ++part) {
                 const int64_t c0 = part * clen;
                 const int64_t cl = std::min<int64_t>(clen, s.m - c0);
+                std::vector<EncTile>& dst = (mode == ENC_ROW_VEC && kEncRowsKernel) ? enc_rows : enc;
                 for (int64_t ti = 0; ti < ntiles; ++ti) {
                     if (interleave)  // rows ti, ti + ntiles, ...: consecutive blocks, adjacent rows
-                        enc.push_back(EncTile{(int32_t)i, mode, ti, (s.n - ti + ntiles - 1) / ntiles,
+                        dst.push_back(EncTile{(int32_t)i, mode, ti, (s.n - ti + ntiles - 1) / ntiles,
                                               (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1,
                                               (int32_t)ntiles});
                     else
-                        enc.push_back(EncTile{(int32_t)i, mode, ti * per, std::min(per, s.n - ti * per),
+                        dst.push_back(EncTile{(int32_t)i, mode, ti * per, std::min(per, s.n - ti * per),
                                               (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1, 1});
                 }
-                lds = std::max<int>(lds, (int)(cl * r * 4));
+                int& l = (mode == ENC_ROW_VEC && kEncRowsKernel) ? rows_lds : lds;
+                l = std::max<int>(l, (int)(cl * r * 4));
             }
         }
         // ---- pack chunks: selected rows, ~kChunkElems elements each (small m: at most
@@ -186,7 +197,15 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         const bool small_tile = s.m >= 4 && s.m < 256;
         // (rows of >= 256 elements go one per wave: at least 4 rows per chunk)
         const int64_t min_rows = s.m >= 256 ? 4 : 1;
-        {
+        // 1-D tensors and 1x1-conv rows (m = 1, 2) with 16-B aligned data stream over ALL rows
+        // with the slot map (mode 1: one 16-B quad of E per lane, whole quads rewritten):
+        // their 4- and 8-B rows are too short for per-row gathers
+        const bool stream_small = (s.m == 1 || s.m == 2) && s.offset % 4 == 0 && dtype == ARCTOPK_F32;
+        if (stream_small) {
+            const int64_t per = pack_elems / s.m;  // a multiple of 4 rows: quads never straddle chunks
+            for (int64_t row = 0; row < s.n; row += per)
+                pack.push_back(Chunk{(int32_t)i, 1, row, std::min(per, s.n - row)});
+        } else {
             int64_t per = std::max<int64_t>(min_rows, pack_elems / s.m);
             if (small_tile) per = std::min<int64_t>(per, kSmallTileRows);
             for (int64_t j = 0; j < s.k_rows; j += per)
@@ -198,7 +217,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             if (small_tile)  // the chunk tile lives in LDS: <= 64 KiB
                 per = std::min<int64_t>(std::min<int64_t>(per, kSmallTileRows), 16000 / s.m);
             for (int64_t row = 0; row < s.n; row += per)
-                dec.push_back(Chunk{(int32_t)i, 0, row, std::min(per, s.n - row)});
+                dec.push_back(Chunk{(int32_t)i, stream_small ? 1 : 0, row, std::min(per, s.n - row)});
             if (small_tile) dec_lds = std::max<int64_t>(dec_lds, (std::min(per, s.n) * s.m + 4) * 4);
         }
     }
@@ -217,6 +236,8 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     p->h_segs = new arctopk_segment[segs.size()];
     std::copy(segs.begin(), segs.end(), p->h_segs);
     p->n_enc = (int)enc.size();
+    p->n_enc_rows = (int)enc_rows.size();
+    p->enc_rows_lds_bytes = rows_lds;
     p->n_pack = (int)pack.size();
     p->n_dec = (int)dec.size();
     pack_begin.push_back((int32_t)pack.size());
@@ -239,6 +260,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     } while (0)
     ALLOC_COPY(p->d_segs, dsegs);
     ALLOC_COPY(p->d_enc, enc);
+    ALLOC_COPY(p->d_enc_rows, enc_rows);
     ALLOC_COPY(p->d_pack, pack);
     ALLOC_COPY(p->d_dec, dec);
     ALLOC_COPY(p->d_small, small_ids);
@@ -304,6 +326,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     (void)hipSetDevice(p->device);
     if (p->d_segs) (void)hipFree(p->d_segs);
     if (p->d_enc) (void)hipFree(p->d_enc);
+    if (p->d_enc_rows) (void)hipFree(p->d_enc_rows);
     if (p->d_pack) (void)hipFree(p->d_pack);
     if (p->d_dec) (void)hipFree(p->d_dec);
     if (p->d_keys) (void)hipFree(p->d_keys);

@@ -137,7 +137,9 @@ int arctopk_row_energy(const arctopk_plan* plan, const void* sketch, int32_t wor
 
 /*
  * K3 pack.  Gather the selected rows into the packed buffer (segment order,
- * ascending rows) and update the local residual:
+ * ascending rows) and update the local residual.  `rowlist` and `slotmap` are
+ * arctopk_select's outputs (rows of 1 or 2 elements are packed by a stream over the
+ * slot map, longer rows by gathering the row list):
  *   NONE : packed = G[sel]
  *   EF14 : packed = E[sel] (E holds X after encode); E[sel] = 0
  *   EF21 : D = G[sel] - E[sel]; packed = D; E[sel] = E[sel] + D
@@ -146,7 +148,7 @@ int arctopk_row_energy(const arctopk_plan* plan, const void* sketch, int32_t wor
  * EF21 zero_/index_put (:126-128) and the residual persistence (:270-275).
  */
 int arctopk_pack(const arctopk_plan* plan, const void* grad, void* err, int32_t ef,
-                 const int32_t* rowlist, void* packed, void* stream);
+                 const int32_t* rowlist, const int32_t* slotmap, void* packed, void* stream);
 
 /*
  * K4 decode.  From the all-reduced packed values:
@@ -167,7 +169,7 @@ int arctopk_decode(const arctopk_plan* plan, const void* packed, const int32_t* 
  */
 int arctopk_pack_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t seg_end,
                           const void* grad, void* err, int32_t ef, const int32_t* rowlist,
-                          void* packed, void* stream);
+                          const int32_t* slotmap, void* packed, void* stream);
 int arctopk_decode_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t seg_end,
                             const void* packed, const int32_t* slotmap, int32_t world_size,
                             int32_t ef, void* gerr, void* out, void* stream);
