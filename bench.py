@@ -32,60 +32,13 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel  # noqa: E402
+from workloads import HEADLINE, WORKLOADS, ddp_buckets, resnet18_cifar_shapes  # noqa: E402,F401
 from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import (GroupTopKState,  # noqa: E402
                                                                       group_topk_hook)
 
 METRIC = "compressed grad GB/s (device-resident) per GPU at k=0.2, r=4; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured float4 copy
-HEADLINE = [[2048, 2048]] * 16
-# secondary buckets: real DDP bucket shapes of the BASELINE configs
-WORKLOADS = {
-    "headline": ("bucket_16x2048x2048_fp32_256MiB", HEADLINE),
-    "llama_embed": ("bucket_llama1b_embed_32000x2048_fp32_250MiB", [[32000, 2048]]),
-    "roberta_embed": ("bucket_roberta_embed_50265x768_fp32_147MiB", [[50265, 768]]),
-    "resnet18_conv": ("bucket_28x512x512x3x3_fp32_252MiB", [[512, 512, 3, 3]] * 28),
-    "resnet50_mixed": ("bucket_resnet50_stage4_mixed_fp32",
-                       [[2048], [2048], [2048, 512, 1, 1], [512], [512], [512, 512, 3, 3], [512],
-                        [512], [512, 2048, 1, 1]] * 3 + [[2048, 1024, 1, 1]]),
-    "llama_layer_mixed": ("bucket_llama1b_layer_mixed_1d_fp32",
-                          [[2048], [5632, 2048], [2048, 5632], [5632, 2048], [2048]]
-                          + [[2048, 2048]] * 4 + [[2048]]),
-}
 PHASES = ["encode", "sketch_allreduce", "select", "pack", "packed_allreduce", "decode"]
-
-
-def resnet18_cifar_shapes():
-    """Parameter shapes of the CIFAR ResNet-18 of configs[1] in definition order (the
-    reference's cifar10/resnet.py: 3x3 stem, BasicBlock [2, 2, 2, 2], 1x1 shortcuts,
-    BatchNorm weight + bias, Linear(512, 10)); 62 tensors, 11.17 M parameters."""
-    shapes = [[64, 3, 3, 3], [64], [64]]
-    cin = 64
-    for planes, stride in ((64, 1), (128, 2), (256, 2), (512, 2)):
-        for b in range(2):
-            s_ = stride if b == 0 else 1
-            shapes += [[planes, cin, 3, 3], [planes], [planes], [planes, planes, 3, 3], [planes], [planes]]
-            if s_ != 1 or cin != planes:
-                shapes += [[planes, cin, 1, 1], [planes], [planes]]
-            cin = planes
-    return shapes + [[10, 512], [10]]
-
-
-def ddp_buckets(shapes, first_cap=1 << 20, cap=25 << 20, elem_bytes=4):
-    """DDP's bucketing as the Reducer sees it: parameters in reverse definition order (the
-    order gradients become ready), a first bucket of <= 1 MiB, then <= 25 MiB buckets
-    (DistributedDataParallel defaults; a tensor larger than the cap gets its own bucket)."""
-    out, cur, size = [], [], 0
-    for s_ in reversed(shapes):
-        nbytes = elem_bytes * bucket_numel([s_])
-        limit = first_cap if not out else cap
-        if cur and size + nbytes > limit:
-            out.append(cur)
-            cur, size = [], 0
-        cur.append(s_)
-        size += nbytes
-    if cur:
-        out.append(cur)
-    return out
 
 
 def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4):
@@ -134,34 +87,63 @@ def pmc_traffic(workload: str, ef: str, kernel: str):
     return ent["bytes_per_launch"], os.path.relpath(paths[-1], REPO)
 
 
-def cpu_baseline(ef: str, seconds: float, rank: int, shapes, label: str, hook: str = "arc"):
-    """Time the CPU oracle (a restatement of the reference hook) on the same bucket."""
-    from oracle import arctopk as A
-    from oracle import sparse as S
-    threads = torch.get_num_threads()
-    g = torch.Generator().manual_seed(1000 + rank)
-    n = bucket_numel(shapes)
-    G = torch.randn(n, generator=g)
-    E = torch.randn(n, generator=g) * 0.1 if ef != "noef" else None
-    gE = torch.zeros(n) if ef == "ef21" else None
-    st = A.OracleState(r=4, compress_ratio=0.2, use_error_feedback=ef, seed=1234)
-    times = []
-    t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end or len(times) < 2:
-        seed = st.next_seed()
-        t0 = time.perf_counter()
-        if hook == "arc":
-            A.simulate_step([G], [E], gE, shapes, 0.2, 4, ef, seed)
-        else:
-            S.simulate_step([G], [E], gE, shapes, 0.2, ef, hook == "randk", seed)
-        times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    fn = "group_topk_hook" if hook == "arc" else f"sparse_hook_sync ({hook})"
-    return {"value": round(4 * n / med / 1e9, 3), "unit": "GB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{len(times)} oracle calls (torch-CPU restatement of {fn}, "
-                      f"ws=1, {ef}) on one {label} bucket, median {med * 1e3:.1f} ms, "
-                      f"{os.cpu_count()} host CPUs visible"}
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share() -> int:
+    """Host CPU threads this job may use: the affinity mask, capped by OMP_NUM_THREADS (the
+    GPU box exports 16, its share of a many-core host)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(ef: str, seconds: float, workload: str, label: str, bucket_bytes: int,
+                 hook: str = "arc"):
+    """SURVEY.md section 8(d)'s CPU path: the oracle's restatement of the reference hook
+    (oracle/cpu_bench.py, torch CPU ops, collectives over gloo on 127.0.0.1) on the same
+    bucket at world size 1 and 2, threads = host CPU share // ws per rank, run in child
+    processes that see no GPU.  value = bucket GB/s per rank at ws = 1."""
+    if hook != "arc":
+        return None
+    import subprocess
+    threads = cpu_share()
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS=str(threads))
+    runs = {}
+    for ws in (1, 2):
+        per = max(1, threads // ws)
+        cmd = [sys.executable, "-m", "oracle.cpu_bench", "--ws", str(ws), "--threads", str(per),
+               "--seconds", str(seconds), "--ef", ef, "--workload", workload]
+        try:
+            r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+            runs[ws] = json.loads(line)
+        except (subprocess.SubprocessError, IndexError, ValueError) as e:
+            runs[ws] = {"error": f"{type(e).__name__}: {e}"[:200]}
+    if "median_s" not in runs.get(1, {}):
+        return {"value": None, "unit": "GB/s", "cores": threads, "kind": "port",
+                "sample": f"CPU oracle failed: {runs}"}
+    gbs = {ws: round(bucket_bytes / r["median_s"] / 1e9, 3) for ws, r in runs.items() if "median_s" in r}
+    return {"value": gbs[1], "unit": "GB/s", "cores": threads, "kind": "port",
+            "ws2_per_rank": gbs.get(2), "ws2_cores_per_rank": max(1, threads // 2),
+            "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": f"oracle restatement of group_topk_hook ({ef}, steady state) over gloo on "
+                      f"127.0.0.1 on one {label} bucket per rank: ws=1 {runs[1]['calls']} calls "
+                      f"(median {runs[1]['median_s'] * 1e3:.1f} ms, {threads} threads), ws=2 "
+                      + (f"{runs[2]['calls']} calls (median {runs[2]['median_s'] * 1e3:.1f} ms, "
+                         f"{max(1, threads // 2)} threads per rank)" if "median_s" in runs.get(2, {})
+                         else f"failed ({runs.get(2)})")
+                      + f"; host CPU share {threads} of {os.cpu_count()} visible"}
 
 
 def main():
@@ -182,7 +164,7 @@ def main():
                     help="bucket dtype (f32: every BASELINE config; bf16: the Llama driver's default)")
     ap.add_argument("--ratio", type=float, default=0.2)
     ap.add_argument("--r", type=int, default=4)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-events", action="store_true")
     ap.add_argument("--system-events", action="store_true",
@@ -318,8 +300,8 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, rank, shapes, label,
-                                           args.hook)
+        out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, args.workload, label,
+                                           eb * bucket_numel(shapes), args.hook)
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as _G
     if _G.HOST_TIMES is not None and rank == 0:  # ARCTOPK_HOST_TIMING=1: host us per hook call
         calls = max(1, (args.steps + args.warmup) * nb)

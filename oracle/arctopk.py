@@ -192,7 +192,12 @@ def _dtype_bits(dtype) -> int:
 
 
 def oracle_group_topk_hook(state: OracleState, bucket, group=None) -> torch.Tensor:
-    """The full reference hook restated over a real process group.  Returns the bucket."""
+    """The full reference hook restated over a real process group, in the reference's
+    in-place op order (group_topk_hook_no_reshape.py:190-297): EF pre-apply into the bucket,
+    per-tensor sketches, select, gather + EF14 zero / EF21 keep-only in the bucket, residual
+    persistence, packed all-reduce, bucket.zero_() + scatter, EF21 gE.  (bench.py's CPU
+    baseline times this; the one sketch all-reduce per bucket sums the same elements as the
+    reference's one per tensor.)  Returns the bucket."""
     group = group if group is not None else dist.group.WORLD
     ws = dist.get_world_size(group)
     buf = bucket.buffer()
@@ -206,16 +211,15 @@ def oracle_group_topk_hook(state: OracleState, bucket, group=None) -> torch.Tens
         return buf
     b = bucket.index()
     ef = state.use_error_feedback
-    E = None
-    if ef == "ef14":
+    if ef == "ef14":  # (:224-230)
         if b in state.error_dict:
-            E = state.error_dict[b]
+            buf.add_(state.error_dict[b], alpha=1.0)
         else:
             state.error_dict[b] = torch.zeros_like(buf)
-    elif ef == "ef21":
+    elif ef == "ef21":  # (:231-250)
         if b in state.error_dict:
-            E = state.error_dict[b]
-        else:  # EF21 init (ref :236-250)
+            buf.add_(state.error_dict[b], alpha=-1.0)
+        else:
             state.error_dict[b] = buf.clone()
             state.comm_bits_this_round += buf.numel() * _dtype_bits(buf.dtype)
             dist.all_reduce(buf, group=group)
@@ -224,11 +228,12 @@ def oracle_group_topk_hook(state: OracleState, bucket, group=None) -> torch.Tens
             if bucket.is_last():
                 state.iter += 1
             return buf
-    seed = state.next_seed()
+    seed = state.next_seed()  # (:254-255)
     torch.manual_seed(seed)
     segs = segments(shapes, state.compress_ratio)
     Vs = draw_projections(seed, segs, state.r, buf.dtype)
-    X, Ps = encode(buf, E, ef, segs, Vs)
+    Ps = [buf[s.offset:s.offset + s.numel].clone() if s.kind == RAW
+          else buf[s.offset:s.offset + s.numel].view(s.n, s.m) @ V for s, V in zip(segs, Vs)]
     flat = torch.cat([p.flatten() for p in Ps])
     dist.all_reduce(flat, group=group)
     P_sum, off = [], 0
@@ -236,18 +241,22 @@ def oracle_group_topk_hook(state: OracleState, bucket, group=None) -> torch.Tens
         P_sum.append(flat[off:off + p.numel()].view_as(p))
         off += p.numel()
     _, rows = select(P_sum, ws, segs)
-    vals = pack(X, rows, segs, ef)
-    if ef == "ef14":
-        state.error_dict[b].copy_(X)
+    vals = pack(buf, rows, segs, ef)  # gathers; EF14 zeroes / EF21 keeps only the selection, in place
+    if ef == "ef14":  # (:270-275)
+        state.error_dict[b].copy_(buf)
     elif ef == "ef21":
-        state.error_dict[b].add_(X)
+        state.error_dict[b].add_(buf)
     state.comm_bits_this_round += 2 * (ws - 1) * bits_per_call(segs, state.r, _dtype_bits(buf.dtype))
-    dist.all_reduce(vals, group=group)
-    out = decode(vals, ws, rows, segs, buf.numel(), buf.dtype)
-    if ef == "ef21":
-        state.global_error_dict[b].add_(out)
-        out = state.global_error_dict[b]
-    buf.copy_(out)
+    dist.all_reduce(vals, group=group)  # (:280-285)
+    vals.div_(ws)
+    buf.zero_()
+    off = 0
+    for s_, idx in zip(segs, rows):
+        buf[s_.offset:s_.offset + s_.numel].view(s_.n, s_.m)[idx] = vals[off:off + s_.k].view(-1, s_.m)
+        off += s_.k
+    if ef == "ef21":  # (:288-290)
+        state.global_error_dict[b].add_(buf)
+        buf.copy_(state.global_error_dict[b])
     if bucket.is_last():
         state.iter += 1
     return buf

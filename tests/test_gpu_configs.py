@@ -28,7 +28,7 @@ from allreducetopk_amd import _native as N
 from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
 from allreducetopk_amd.comm_hooks import sparse_hook
 from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import GroupTopKState, group_topk_hook
-from bench import WORKLOADS, ddp_buckets, resnet18_cifar_shapes
+from workloads import WORKLOADS, ddp_buckets, resnet18_cifar_shapes
 from oracle import arctopk as A
 from oracle import sparse as S
 from parity import assert_bitwise, check_rows_tie_aware, ensure_group
