@@ -15,9 +15,12 @@ no host synchronisation:
 
 Semantics kept from the reference: same state attributes (``iter``,
 ``error_dict``, ``global_error_dict``, ``rng``, ``comm_bits_this_round`` ...),
-same warm-up and EF21-init paths, the same seed draw and global reseed, the
-same projections V (torch CPU generator), the same k per tensor, the same
-output bucket and residuals.  Selected rows are identical to the reference's
+same warm-up and EF21-init paths, the same seed draw and global reseed (the
+global generators are left exactly where the reference's leave them), the same
+projections V (``state.projections``: "device" = the reference's
+torch.randn(..., device=tensor.device) Philox stream, drawn by a HIP kernel;
+"host" = torch's CPU generator stream, as when the reference runs on CPU), the
+same k per tensor, the same output bucket and residuals.  Selected rows are identical to the reference's
 except where two rows' sketch energies are equal within fp32 rounding of the
 sketch (the GPU sums G.V in a different order than CPU sgemm); exact ties at
 the k-th energy are resolved lowest-row-first.  Buckets may be float32 or
@@ -128,8 +131,9 @@ class BucketPlan:
         self.groups = self._make_groups()
         # the device generator's Philox offset after the reference's per-tensor
         # torch.randn(m, r, device=...) draws of one call (see _reseed_global)
-        self.philox_advance = sum(philox_step(s.m * r, dtype, self.device)
-                                  for s in self.segments if s.kind == N.SEG_SKETCH)
+        adv = N.c_uint64()
+        N.check(L.arctopk_plan_philox_advance(handle, N.ctypes.byref(adv)), "arctopk_plan_philox_advance")
+        self.philox_advance = int(adv.value)
         bits = dtype_bits(dtype)
         # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
         self.bits_sum = sum(((s.n if s.kind == N.SEG_RAW else s.n * r) + s.k_rows * s.m) * bits
@@ -355,6 +359,15 @@ class GroupTopKState(HookState):
         # the gradient shapes against its plan.
         self.layout_check_iters = 3
         self._first_compressed_iter = None
+        # Where V comes from.  "device" (default): drawn on the bucket's GPU by
+        # arctopk_draw_projections, bit-identical to the reference's own
+        # torch.randn(m, r, device=tensor.device) after torch.manual_seed(seed) -- what the
+        # reference computes when it runs on GPUs, as every BASELINE config does.  "host":
+        # the CPU generator's stream (the reference run on CPU, which is how this container's
+        # golden vectors were produced), drawn natively ahead of time and copied to the GPU.
+        self.projections = os.environ.get("ARCTOPK_PROJECTIONS", "device")
+        if self.projections not in ("device", "host"):
+            raise ValueError("projections must be 'device' or 'host'")
 
     def init_sketch_comm(self) -> None:
         """Create the sketch communicator now (a collective over every rank of the default
@@ -466,6 +479,35 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
     nplan.prestaged = (seed, i)
 
 
+def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
+    """The "host" projection source: V from the CPU generator's stream (drawn natively,
+    ahead of time) copied to a device slot on a side stream.  Returns (ring slot, V)."""
+    vslot, V = -1, plan.V_ring[0]
+    pre, plan.prestaged = plan.prestaged, None
+    if pre is not None and pre[0] == seed and state.v_copy_side_stream:
+        # copied during the previous call: usually complete by now, so no stream wait
+        vslot, V = pre[1], plan.await_projection(pre[1], stream)
+        state.prestage_hits += 1
+        _ht("prestaged")
+    else:
+        slot = state._proj.get(seed, plan.ms, dtype)
+        _ht("proj_get")
+        if plan.info.v_len:  # 512 KiB pinned H2D at headline, on a side stream, ahead of encode
+            cs = state._side_stream(state._copy_streams, dev, COPY_PRIORITY) if state.v_copy_side_stream else stream
+            vslot, V = plan.stage_projection(slot.host, cs, stream)
+            _ht("stage_copy")
+            state._proj.release(slot, cs)  # refilled only after this copy completed
+        else:
+            state._proj.release(slot)
+    _ht("stage_v")
+    state._proj.prefetch(state._upcoming_ms(bucket), dtype)
+    _ht("prefetch")
+    if state.v_copy_side_stream:
+        _prestage_next(state, bucket, dtype, dev)
+        _ht("prestage_next")
+    return vslot, V
+
+
 _RESEED_FAST = None
 
 # optional host-time breakdown of the hook (diagnostics; ARCTOPK_HOST_TIMING=1)
@@ -518,24 +560,6 @@ def _reseed_global(seed: int, device_index: int = 0, advance: int = 0) -> None:
     torch.default_generator.manual_seed(seed)
     if advance:
         _RESEED_FAST[device_index].set_offset(advance)
-
-
-_PHILOX_STEP: Dict[tuple, int] = {}
-
-
-def philox_step(numel: int, dtype, device) -> int:
-    """Philox offset one ``torch.randn(numel, dtype, device)`` consumes, measured once per
-    (numel, dtype, device) on a private generator (the global ones are not touched)."""
-    dev = torch.device(device)
-    key = (int(numel), dtype, dev.index or 0)
-    v = _PHILOX_STEP.get(key)
-    if v is None:
-        g = torch.Generator(device=dev)
-        g.manual_seed(0)
-        torch.randn(int(numel), dtype=dtype, device=dev, generator=g)
-        v = int(g.get_offset())
-        _PHILOX_STEP[key] = v
-    return v
 
 
 def cal_k(state, tensor) -> int:
@@ -656,7 +680,11 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
 
     # per-call projection seed, and the reference's global reseed side effect (:254-255)
     _ht()
-    seed = state._proj.consume_seed(state.rng)
+    device_v = state.projections == "device"
+    if device_v:  # (:254); the host path keeps a look-ahead of the seed sequence
+        seed = int(torch.randint(0, 1_000_000_000, (1,), generator=state.rng).item())
+    else:
+        seed = state._proj.consume_seed(state.rng)
     plan = state._plan_for(bucket)
     dev = input_tensor.device
     _reseed_global(seed, dev.index or 0, plan.philox_advance)
@@ -670,28 +698,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     dtype = input_tensor.dtype
     _ht("plan+pending")
     vslot, V = -1, plan.V_ring[0]
-    pre, plan.prestaged = plan.prestaged, None
-    if pre is not None and pre[0] == seed and state.v_copy_side_stream:
-        # copied during the previous call: usually complete by now, so no stream wait
-        vslot, V = pre[1], plan.await_projection(pre[1], stream)
-        state.prestage_hits += 1
-        _ht("prestaged")
-    else:
-        slot = state._proj.get(seed, plan.ms, dtype)
-        _ht("proj_get")
-        if plan.info.v_len:  # 512 KiB pinned H2D at headline, on a side stream, ahead of encode
-            cs = state._side_stream(state._copy_streams, dev, COPY_PRIORITY) if state.v_copy_side_stream else stream
-            vslot, V = plan.stage_projection(slot.host, cs, stream)
-            _ht("stage_copy")
-            state._proj.release(slot, cs)  # refilled only after this copy completed
-        else:
-            state._proj.release(slot)
-    _ht("stage_v")
-    state._proj.prefetch(state._upcoming_ms(bucket), dtype)
-    _ht("prefetch")
-    if state.v_copy_side_stream:
-        _prestage_next(state, bucket, dtype, dev)
-        _ht("prestage_next")
+    if not device_v:
+        vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, stream)
 
     evs = None
     if state.phase_events is not None:
@@ -712,6 +720,10 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             evs[name] = e
 
     mark("start")
+    if device_v and plan.info.v_len:  # V on this stream, right before the encode that reads it
+        N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid),
+                "arctopk_draw_projections")
+        _ht("draw_v")
     _ht("events")
     plan.encode(input_tensor, err, ef, err_in, V, sid)
     _ht("encode")

@@ -216,6 +216,15 @@ struct EncTile {
                        // advancing window of the tensor instead of scattered row ranges)
 };
 
+struct VDraw {         // one SKETCH tensor's torch.randn(m, r, device=...) draw (vdraw.hip)
+    int64_t v_off;     // element offset in the projection buffer
+    int64_t numel;     // m * r
+    uint64_t stride;   // threads of torch's grid-stride launch: 256 * grid
+    uint64_t offset;   // Philox offset at this draw (after the bucket's manual_seed)
+};
+int vdraw_table(const arctopk_segment* segs, int nseg, int r, int device, VDraw* out, int* nout,
+                uint64_t* advance);
+
 struct Chunk {         // pack: selected-row range (mode 0) or row range (mode 1); decode: row range
     int32_t seg;
     int32_t mode;      // 1: m in {1, 2}, fp32, 16-B aligned: quad streams over every row
@@ -263,4 +272,8 @@ struct arctopk_plan {
     int n_large_batches;
     arctopk::MWorkspace* d_mws;         // multi-block select workspace
     int64_t mws_cap;                    // its candidate slots
+    arctopk::VDraw* d_vdraw;            // device projection draws (vdraw.hip)
+    int n_vdraw;
+    int64_t vdraw_max;                  // largest m * r
+    uint64_t vdraw_advance;             // Philox offset after the bucket's draws
 };

@@ -300,6 +300,18 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         e = hipMemset(p->d_mws, 0, sizeof(MWorkspace));
         if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
     }
+    {  // device projection draws
+        std::vector<VDraw> vd(segs.size());
+        int nvd = 0;
+        uint64_t adv = 0;
+        const int ve = vdraw_table(segs.data(), (int)segs.size(), r, device, vd.data(), &nvd, &adv);
+        if (ve) { arctopk_plan_destroy(p); return ve; }
+        vd.resize(nvd);
+        p->n_vdraw = nvd;
+        p->vdraw_advance = adv;
+        for (const VDraw& d : vd) p->vdraw_max = std::max<int64_t>(p->vdraw_max, d.numel);
+        ALLOC_COPY(p->d_vdraw, vd);
+    }
 #undef ALLOC_COPY
     e = hipMalloc((void**)&p->d_keys, std::max<size_t>(4, info.rows_total * sizeof(uint32_t)));
     if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
@@ -338,6 +350,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     delete[] p->h_pack_begin;
     delete[] p->h_large_batches;
     if (p->d_mws) (void)hipFree(p->d_mws);
+    if (p->d_vdraw) (void)hipFree(p->d_vdraw);
     delete[] p->h_dec_begin;
     delete p;
     return 0;

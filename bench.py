@@ -236,6 +236,9 @@ def main():
         st.phase_event_every = 16  # sample HIP events on every 16th timed hook call (each marker idles the GPU ~6 us)
         st.phase_event_device_scope = not args.system_events
 
+    from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as _G
+    if _G.HOST_TIMES is not None:  # ARCTOPK_HOST_TIMING=1: steady-state calls only
+        _G.HOST_TIMES.clear()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -302,9 +305,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, args.workload, label,
                                            eb * bucket_numel(shapes), args.hook)
-    from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as _G
     if _G.HOST_TIMES is not None and rank == 0:  # ARCTOPK_HOST_TIMING=1: host us per hook call
-        calls = max(1, (args.steps + args.warmup) * nb)
+        calls = max(1, args.steps * nb)
         print("host_us_per_call " + json.dumps({k: round(v / calls * 1e6, 1)
                                                 for k, v in _G.HOST_TIMES.items()}), flush=True)
     if rank == 0:

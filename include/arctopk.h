@@ -248,6 +248,17 @@ int arctopk_sparse_decode(float* out, int64_t numel, int32_t ntensors, const int
 int arctopk_ef_apply(float* x, float* E, int64_t numel, int32_t ef, int32_t err_in, void* stream);
 
 /*
+ * Device projections of one bucket call: for every SKETCH segment in bucket order,
+ * V[v_off ..] = torch.randn(m, r, device=dev, dtype) as drawn by the reference on the GPU
+ * right after torch.manual_seed(seed) (group_topk_hook_no_reshape.py:49, :79, :255):
+ * torch's Philox4x32-10 normal_ kernel (hiprand) reproduced element by element, bit for bit.
+ * Stream-ordered, one launch.  arctopk_plan_philox_advance: the device generator's Philox
+ * offset after those draws (what torch.manual_seed + the reference's draws leave behind).
+ */
+int arctopk_draw_projections(const arctopk_plan* plan, uint64_t seed, void* V, void* stream);
+int arctopk_plan_philox_advance(const arctopk_plan* plan, uint64_t* advance);
+
+/*
  * Host-only (no GPU): `total` (a multiple of 16) consecutive values of the reference's
  * bf16 projection stream -- torch.randn(..., dtype=bfloat16) on CPU after
  * torch.manual_seed(seed) (group_topk_hook_no_reshape.py:49, :79, :255) -- as bf16 bit

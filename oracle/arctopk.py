@@ -78,15 +78,22 @@ def segments(shapes, ratio: float) -> List[Segment]:
     return out
 
 
-def draw_projections(seed: int, segs: List[Segment], r: int, dtype=torch.float32):
-    """V per SKETCH tensor, in bucket order, from a generator reseeded with ``seed``.
+def draw_projections(seed: int, segs: List[Segment], r: int, dtype=torch.float32, device=None):
+    """V per SKETCH tensor, in bucket order, as the reference draws them after its global
+    reseed (``torch.manual_seed(seed)``, :255): ``torch.randn(m, r, device=tensor.device,
+    dtype)`` per 2-D/ND tensor in order (:49, :79).
 
-    The reference reseeds the global RNG (``torch.manual_seed(seed)``, :255) and
-    draws ``torch.randn(m, r)`` per 2-D/ND tensor in order (:49, :79); a private
-    CPU generator seeded the same way yields the same stream.
+    device None: the reference run on CPU -- a private CPU generator seeded the same way
+    yields the same stream.  device "cuda:i": the reference run on that GPU -- the same
+    global reseed and per-tensor torch.randn on the device (the device's Philox stream),
+    returned on the CPU for the oracle's arithmetic.
     """
-    g = torch.Generator().manual_seed(int(seed))
-    return [torch.randn(s.m, r, generator=g, dtype=dtype) if s.kind == SKETCH else None
+    if device is None:
+        g = torch.Generator().manual_seed(int(seed))
+        return [torch.randn(s.m, r, generator=g, dtype=dtype) if s.kind == SKETCH else None
+                for s in segs]
+    torch.manual_seed(int(seed))
+    return [torch.randn(s.m, r, device=device, dtype=dtype).cpu() if s.kind == SKETCH else None
             for s in segs]
 
 
@@ -263,18 +270,20 @@ def oracle_group_topk_hook(state: OracleState, bucket, group=None) -> torch.Tens
 
 
 def simulate_step(Gs: List[torch.Tensor], Es: List[Optional[torch.Tensor]], gE: Optional[torch.Tensor],
-                  shapes, ratio: float, r: int, ef: str, seed: int, rows_override=None):
+                  shapes, ratio: float, r: int, ef: str, seed: int, rows_override=None,
+                  proj_device=None):
     """One steady-state compressed call on ``len(Gs)`` ranks in one process.
 
     Collectives are sums in rank order.  Returns a dict of intermediates and
     per-rank results: V, P_local, P_sum, norms, rows, X (post-pack bucket
     contents), values, out, E_new, gE_new.  ``rows_override`` (list of row index
     tensors per segment) replaces the top-k choice -- used to compare a device
-    run's outputs bit for bit given the rows that run selected.
+    run's outputs bit for bit given the rows that run selected.  ``proj_device``: draw V
+    as the reference does on that GPU (see draw_projections).
     """
     ws = len(Gs)
     segs = segments(shapes, ratio)
-    Vs = draw_projections(seed, segs, r, Gs[0].dtype)
+    Vs = draw_projections(seed, segs, r, Gs[0].dtype, device=proj_device)
     Xs, Pls = [], []
     for G, E in zip(Gs, Es):
         X, Ps = encode(G, E, ef, segs, Vs)

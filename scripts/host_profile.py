@@ -16,7 +16,7 @@ os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29511")
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import WORKLOADS, ddp_buckets, resnet18_cifar_shapes  # noqa: E402
+from workloads import WORKLOADS, ddp_buckets, resnet18_cifar_shapes  # noqa: E402
 wl = os.environ.get("WORKLOAD", "headline")
 layouts = ddp_buckets(resnet18_cifar_shapes()) if wl == "resnet18_ddp" else [WORKLOADS[wl][1]]
 bks = [SyntheticBucket(torch.randn(bucket_numel(sh), device="cuda:0"), sh, index=i,

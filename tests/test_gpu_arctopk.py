@@ -158,7 +158,7 @@ def test_hook_end_to_end_vs_oracle(ef, which):
         rows = _gpu_rows(plan)
         first_ef14 = (ef == "ef14" and E is None)
         res = A.simulate_step([G], [None if first_ef14 else E], gE, shapes, 0.2, 4, ef, seed,
-                              rows_override=rows)
+                              rows_override=rows, proj_device=DEV)
         for r_, nrm, s in zip(rows, res["norms"], plan.segments):
             flips += check_rows_tie_aware(r_, nrm, int(s.k_rows), band=2e-4)
         assert_bitwise(out, res["out"], f"it{it} output bucket")
@@ -181,6 +181,7 @@ def test_golden_vectors_on_gpu(name):
     shapes = [tuple(s) for s in m["shapes"]]
     st = GroupTopKState(None, r=m["r"], compress_ratio=m["ratio"],
                         start_compress_iter=m["start"], use_error_feedback=m["ef"], seed=m["seed"])
+    st.projections = "host"  # the golden vectors come from the reference run on CPU
     for it in range(m["iters"]):
         G = g.t(0, it, "G")
         bucket = SyntheticBucket(G.to(DEV), shapes, index=0, is_last=True)
@@ -344,7 +345,8 @@ def test_plan_follows_a_rebuilt_bucket_on_the_same_buffer():
         assert [tuple(s) for s in plan.shapes] == [tuple(s) for s in shapes]
         seed = ost.next_seed()
         rows = _gpu_rows(plan)
-        res = A.simulate_step([G], [None], None, shapes, 0.2, 4, "noef", seed, rows_override=rows)
+        res = A.simulate_step([G], [None], None, shapes, 0.2, 4, "noef", seed, rows_override=rows,
+                              proj_device=DEV)
         assert_bitwise(out, res["out"], f"call {it} output")
 
 
@@ -413,6 +415,7 @@ def test_bf16_golden_on_gpu(name):
     segs = A.segments(shapes, m["ratio"])
     st = GroupTopKState(None, r=m["r"], compress_ratio=m["ratio"],
                         start_compress_iter=m["start"], use_error_feedback=ef, seed=m["seed"])
+    st.projections = "host"  # the golden vectors come from the reference run on CPU
     ost = A.OracleState(seed=m["seed"])
     E_prev = gE_prev = None
     stream = torch.cuda.current_stream().cuda_stream
@@ -521,6 +524,7 @@ def test_projection_prestaging_under_reordering_and_reseed():
     layouts = {0: shapes_a, 1: shapes_b, 2: shapes_a}
     st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                         use_error_feedback="noef", seed=99)
+    st.projections = "host"  # the pre-staged H2D path of the CPU-stream projections
     ost = A.OracleState(r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback="noef",
                         seed=99)
     order = [0, 1, 2] * 4 + [2, 0, 1, 1, 0] + [0, 1, 2] * 3 + ["reseed"] + [0, 1, 2] * 3 + [1, 2]
@@ -543,3 +547,35 @@ def test_projection_prestaging_under_reordering_and_reseed():
         assert_bitwise(out, res["out"], f"call {step} (bucket {b}) output")
     assert flips <= 2, f"{flips} rows differ from the oracle's selection (near-ties only)"
     assert st.prestage_hits > 10, f"pre-staged projections were used {st.prestage_hits} times"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_device_projection_draw_matches_torch_randn_on_device(dtype):
+    """arctopk_draw_projections reproduces the reference's projections as drawn on a GPU:
+    torch.manual_seed(seed) then torch.randn(m, r, device=cuda, dtype) per 2-D/ND tensor
+    in bucket order (group_topk_hook_no_reshape.py:49, :79, :255), bit for bit, including
+    draws large enough that torch's grid saturates (threads loop, components 1-3 used); and
+    arctopk_plan_philox_advance equals the device generator's offset after those draws."""
+    import ctypes
+    sets = [MIX, LARGE[:5], [[2048, 2048]] * 3 + [[7], [5632, 2048]],
+            [[8, 300000], [2, 3, 3, 3], [10], [2, 140000]]]
+    for si, shapes in enumerate(sets):
+        shapes = [tuple(s) for s in shapes]
+        plan = BucketPlan(shapes, 4, 0.2, dtype, DEV)
+        segs = A.segments(shapes, 0.2)
+        for seed in (0, 123456789, 999_999_999):
+            V = torch.empty(max(1, plan.info.v_len), dtype=dtype, device=DEV)
+            N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(),
+                                                     torch.cuda.current_stream().cuda_stream),
+                    "arctopk_draw_projections")
+            torch.manual_seed(seed)
+            ref = torch.cat([torch.randn(s.m, 4, device=DEV, dtype=dtype).flatten()
+                             for s in segs if s.kind == A.SKETCH])
+            off = torch.cuda.default_generators[0].get_offset()
+            iv = torch.int16 if dtype == torch.bfloat16 else torch.int32
+            got = V[:ref.numel()]
+            bad = (got.view(iv) != ref.view(iv)).sum().item()
+            assert bad == 0, f"set {si} seed {seed}: {bad} of {ref.numel()} values differ"
+            adv = ctypes.c_uint64()
+            N.check(N.lib().arctopk_plan_philox_advance(plan.handle, ctypes.byref(adv)), "advance")
+            assert adv.value == off, f"set {si}: philox advance {adv.value} vs torch {off}"

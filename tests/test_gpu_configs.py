@@ -84,7 +84,7 @@ class ArcRun:
             rows = _rows(plan)
             E_prev = self.E.get(b) if self.ef != "noef" else None
             res = A.simulate_step([G], [E_prev], self.gE.get(b), shapes, 0.2, 4, self.ef, seed,
-                                  rows_override=rows)
+                                  rows_override=rows, proj_device=DEV)
             for r_, nrm, s in zip(rows, res["norms"], plan.segments):
                 self.flips += check_rows_tie_aware(r_, nrm, int(s.k_rows), band=2e-4)
                 assert torch.all(r_[1:] > r_[:-1]), "row list must be ascending"

@@ -73,7 +73,7 @@ def _worker(rank, ws, port, td, ef, kind):
             dist.all_gather(other, rl)
             assert torch.equal(other[0], other[1]), "ranks selected different rows"
             res = A.simulate_step(allg, [None] * ws if (first or Es is None) else Es, gE, MIX, 0.2,
-                                  4, ef, seed, rows_override=rows)
+                                  4, ef, seed, rows_override=rows, proj_device=dev)
         else:
             idx = None
             seed = None
@@ -170,7 +170,8 @@ def _worker_multi(rank, ws, port, ef, sketch_comm, steps):
             assert torch.equal(other[0], other[1]), f"step{step} bucket{b}: ranks selected different rows"
             first = ef == "ef14" and E[b] is None
             Es = [None] * ws if (ef == "noef" or first) else E[b]
-            res = A.simulate_step(allg[b], Es, gE[b], shapes, 0.2, 4, ef, seed, rows_override=rows)
+            res = A.simulate_step(allg[b], Es, gE[b], shapes, 0.2, 4, ef, seed, rows_override=rows,
+                                  proj_device=dev)
             assert torch.equal(outs[b].cpu(), res["out"]), f"step{step} bucket{b} rank{rank} output"
             if ef != "noef":
                 assert torch.equal(st.error_dict[b].cpu(), res["E_new"][rank]), f"step{step} bucket{b} E"
@@ -245,7 +246,7 @@ def test_hook_inside_ddp_rccl():
             rl = plan.rowlist.cpu()
             rows = [rl[s.sel_off:s.sel_off + s.k_rows].long() for s in plan.segments]
             res = A.simulate_step([c["G"]], [c["E"]], None, c["shapes"], 0.2, 4, "ef14", seed,
-                                  rows_override=rows)
+                                  rows_override=rows, proj_device="cuda:0")
             for r_, nrm, s in zip(rows, res["norms"], plan.segments):
                 flips += check_rows_tie_aware(r_, nrm, int(s.k_rows), band=2e-4)
             off = 0
