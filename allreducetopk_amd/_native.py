@@ -51,6 +51,8 @@ _SIGS = {
     "arctopk_encode": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                  c_void_p]),
     "arctopk_select": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "arctopk_select_draw": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                      c_uint64, c_void_p, c_void_p]),
     "arctopk_row_energy": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                c_void_p]),

@@ -128,6 +128,10 @@ class BucketPlan:
         self.v_waits = 0                      # calls whose encode had to wait for its copy
         self.decode_done = None  # recorded after this bucket's side-stream decode
         self.prestaged = None    # (seed, ring slot) of the next call's V, copied a call early
+        # device projections: the seed whose V_ring[0] draw is already enqueued (drawn by the
+        # previous call's select launch), and the stream of V_ring[0]'s last writer / reader
+        self.v_drawn = None
+        self.v_stream = None
         self.groups = self._make_groups()
         # the device generator's Philox offset after the reference's per-tensor
         # torch.randn(m, r, device=...) draws of one call (see _reseed_global)
@@ -280,10 +284,19 @@ class BucketPlan:
                                        V.data_ptr(), self.sketch.data_ptr(), stream),
                 "arctopk_encode")
 
-    def select(self, world_size: int, stream: int):
-        N.check(N.lib().arctopk_select(self.handle, self.sketch.data_ptr(), world_size,
-                                       self.rowlist.data_ptr(), self.slotmap.data_ptr(), stream),
-                "arctopk_select")
+    def select(self, world_size: int, stream: int, next_plan=None, next_seed: int = 0):
+        """Select; with `next_plan`, its projections for `next_seed` are drawn into its
+        V_ring[0] by the same launch (arctopk_select_draw)."""
+        if next_plan is None:
+            N.check(N.lib().arctopk_select(self.handle, self.sketch.data_ptr(), world_size,
+                                           self.rowlist.data_ptr(), self.slotmap.data_ptr(), stream),
+                    "arctopk_select")
+            return
+        N.check(N.lib().arctopk_select_draw(self.handle, self.sketch.data_ptr(), world_size,
+                                            self.rowlist.data_ptr(), self.slotmap.data_ptr(),
+                                            next_plan.handle, next_seed,
+                                            next_plan.V_ring[0].data_ptr(), stream),
+                "arctopk_select_draw")
 
     def pack(self, grad, err, ef: int, stream: int):
         N.check(N.lib().arctopk_pack(self.handle, N.ptr(grad), N.ptr(err), ef,
@@ -322,9 +335,13 @@ class GroupTopKState(HookState):
         self._proj = ProjectionSource(r)
         self._order: List[int] = []  # bucket indices in call order within one backward
         # optional phase timing: a list that receives one dict of HIP events for every
-        # `phase_event_every`-th call (HIP events on the hook's stream)
+        # `phase_event_every`-th call (HIP events on the hook's stream); `hook_events` receives
+        # the light samples of every `hook_event_every`-th other call: only start, after the
+        # V draw, after encode and the decode end (each marker idles the GPU a few us)
         self.phase_events = None
         self.phase_event_every = 1
+        self.hook_events = None
+        self.hook_event_every = 0
         self.phase_event_device_scope = True  # False: torch (system-scope) timing events
         self.prestage_hits = 0  # calls whose projections were copied during the previous call
         self._ev_calls = 0
@@ -368,6 +385,14 @@ class GroupTopKState(HookState):
         self.projections = os.environ.get("ARCTOPK_PROJECTIONS", "device")
         if self.projections not in ("device", "host"):
             raise ValueError("projections must be 'device' or 'host'")
+        # device projections drawn a call early: each select launch also draws the
+        # predicted next call's V (next bucket in the observed order, next seed of the rng)
+        # in its trailing blocks, beside the latency-bound select; the next call uses it
+        # only if its seed is the predicted one, else draws its own.  Takes the draw
+        # launch off the critical path.
+        self.predraw = os.environ.get("ARCTOPK_PREDRAW", "1") != "0"
+        self.predraw_hits = 0
+        self._order_pos: Dict[int, int] = {}
 
     def init_sketch_comm(self) -> None:
         """Create the sketch communicator now (a collective over every rank of the default
@@ -432,6 +457,20 @@ class GroupTopKState(HookState):
         self._plans[bucket.index()] = (key, plan, ident)
         return plan
 
+    def _next_plan(self, b: int):
+        """The plan of the bucket predicted to come after bucket b (order repeats)."""
+        order = self._order
+        pos = self._order_pos.get(b)
+        if pos is None:
+            if b in order:
+                pos = order.index(b)
+            else:
+                pos = len(order)
+                order.append(b)
+            self._order_pos[b] = pos
+        ent = self._plans.get(order[(pos + 1) % len(order)])
+        return None if ent is None else ent[1]
+
     def _upcoming_ms(self, bucket) -> List[Tuple[int, ...]]:
         """Column lists of the next calls, assuming the bucket order repeats."""
         b = bucket.index()
@@ -477,6 +516,11 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
     i = nplan.copy_projection(slot.host, cs, torch.cuda.current_stream(dev))
     state._proj.release(slot, cs)
     nplan.prestaged = (seed, i)
+
+
+# light samples alternate between the whole hook (start .. decode end) and the encode
+# kernel alone (after the V draw .. after encode): two markers per sampled call
+_LIGHT_MARKS = (frozenset(("start", "decode")), frozenset(("draw", "encode")))
 
 
 def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
@@ -681,10 +725,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     # per-call projection seed, and the reference's global reseed side effect (:254-255)
     _ht()
     device_v = state.projections == "device"
-    if device_v:  # (:254); the host path keeps a look-ahead of the seed sequence
-        seed = int(torch.randint(0, 1_000_000_000, (1,), generator=state.rng).item())
-    else:
-        seed = state._proj.consume_seed(state.rng)
+    seed = state._proj.consume_seed(state.rng)  # (:254), with a look-ahead of the sequence
     plan = state._plan_for(bucket)
     dev = input_tensor.device
     _reseed_global(seed, dev.index or 0, plan.philox_advance)
@@ -702,14 +743,19 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, stream)
 
     evs = None
-    if state.phase_events is not None:
+    light = None
+    if state.phase_events is not None or state.hook_events is not None:
         state._ev_calls += 1
-        if (state._ev_calls - 1) % state.phase_event_every == 0:
+        c = state._ev_calls - 1
+        if state.phase_events is not None and c % state.phase_event_every == 0:
             evs = {}
             state.phase_events.append(evs)
+        elif state.hook_events is not None and state.hook_event_every and c % state.hook_event_every == 0:
+            evs, light = {}, _LIGHT_MARKS[(c // state.hook_event_every) % 2]
+            state.hook_events.append(evs)
 
     def mark(name, on=None):
-        if evs is not None:
+        if evs is not None and (light is None or name in light):
             s_ = on if on is not None else stream
             if state.phase_event_device_scope:  # no system-scope L2 writeback per marker
                 e = N.DeviceEvent(timing=True)
@@ -720,10 +766,18 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             evs[name] = e
 
     mark("start")
-    if device_v and plan.info.v_len:  # V on this stream, right before the encode that reads it
-        N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid),
-                "arctopk_draw_projections")
+    if device_v and plan.info.v_len:
+        if plan.v_stream is not None and plan.v_stream != stream:
+            stream.wait_stream(plan.v_stream)  # V_ring[0]'s last writer / reader ran there
+        plan.v_stream = stream
+        pre, plan.v_drawn = plan.v_drawn, None
+        if pre == seed:  # drawn by the previous call's select launch
+            state.predraw_hits += 1
+        else:  # V on this stream, right before the encode that reads it
+            N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid),
+                    "arctopk_draw_projections")
         _ht("draw_v")
+    mark("draw")
     _ht("events")
     plan.encode(input_tensor, err, ef, err_in, V, sid)
     _ht("encode")
@@ -737,7 +791,17 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         sk_group = state._sketch_group(group) if overlap else group
         dist.all_reduce(plan.sketch_view, group=sk_group, async_op=False)
     mark("sketch_allreduce")
-    plan.select(world_size, sid)
+    nplan = nseed = None
+    if device_v and state.predraw:
+        nplan = state._next_plan(b)
+        if (nplan is not None and nplan.info.v_len and nplan.dtype == dtype and nplan.device == dev
+                and (nplan.v_stream is None or nplan.v_stream == stream)):
+            nseed = state._proj.peek_next_seed()
+        if nseed is None:
+            nplan = None
+    plan.select(world_size, sid, nplan, nseed or 0)
+    if nplan is not None:
+        nplan.v_drawn, nplan.v_stream = nseed, stream
     mark("select")
     _ht("select")
     state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum

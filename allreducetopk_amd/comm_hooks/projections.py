@@ -199,10 +199,15 @@ class ProjectionSource:
         self._lookahead.set_state(rng.get_state())
         self._future_seeds.clear()
 
+    PEEK_BATCH = 16  # seeds drawn per look-ahead refill (one randint of 16 = 16 of 1, in order)
+
     def _peek_seeds(self, n: int):
-        while len(self._future_seeds) < n:
-            s = int(torch.randint(0, 1_000_000_000, (1,), generator=self._lookahead).item())
-            self._future_seeds.append(s)
+        if len(self._future_seeds) < n:
+            self._future_seeds.extend(torch.randint(
+                0, 1_000_000_000, (max(n - len(self._future_seeds), self.PEEK_BATCH),),
+                generator=self._lookahead).tolist())
+        if n == 1:
+            return [self._future_seeds[0]]
         return list(self._future_seeds)[:n]
 
     def consume_seed(self, rng: torch.Generator) -> int:

@@ -14,6 +14,7 @@
 
 #include "common.h"
 #include "mselect.h"
+#include "vdraw.h"  // (fast contraction inside, for rocrand only)
 
 using namespace arctopk;
 
@@ -558,6 +559,12 @@ __global__ void __launch_bounds__(256) k_energy(const SegDev* __restrict__ segs,
 constexpr int kST = 256;
 constexpr int kCandMax = 256;
 
+constexpr int kRegB = 8;  // register path: rows per thread (n <= kRegB * threads)
+#ifndef ARCTOPK_SEL_REG
+#define ARCTOPK_SEL_REG 1  // tuning switch (A/B builds): 0 = LDS-key path for every small segment
+#endif
+constexpr bool kSelRegPath = ARCTOPK_SEL_REG != 0;
+
 struct SmallSel {
     uint32_t hist[256];
     __attribute__((aligned(16))) uint32_t cand[kCandMax + 4];
@@ -566,6 +573,7 @@ struct SmallSel {
     int64_t wsum[16];
     uint32_t digit, dcount, T;
     int64_t kk, need_eq;
+    uint32_t tg[kRegB * 16], te[kRegB * 16];  // register path: per (round, wave) counts
 };
 
 __device__ __forceinline__ int64_t block_exscan_s(int64_t v, int64_t* wsum) {
@@ -584,6 +592,254 @@ __device__ __forceinline__ int64_t block_exscan_s(int64_t v, int64_t* wsum) {
     return before;
 }
 
+// register path, wave 0: exclusive prefix sums, in index order (round-major), of the
+// per-(round, wave) counts of rows above / equal to the threshold
+template <int NW>
+__device__ __forceinline__ void table_exscan2(uint32_t* ta, uint32_t* tb) {
+    constexpr int NE = kRegB * NW;
+    constexpr int PER = (NE + 63) / 64;
+    const int lane = threadIdx.x & 63;
+    uint32_t a[PER], b[PER], sa = 0, sb = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = lane * PER + q;
+        a[q] = i < NE ? ta[i] : 0u;
+        b[q] = i < NE ? tb[i] : 0u;
+        sa += a[q];
+        sb += b[q];
+    }
+    uint32_t ia = sa, ib = sb;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ya = __shfl_up(ia, o, 64), yb = __shfl_up(ib, o, 64);
+        if (lane >= o) {
+            ia += ya;
+            ib += yb;
+        }
+    }
+    uint32_t ea = ia - sa, eb = ib - sb;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = lane * PER + q;
+        if (i < NE) {
+            ta[i] = ea;
+            tb[i] = eb;
+        }
+        ea += a[q];
+        eb += b[q];
+    }
+}
+
+// Small segments of at most kRegB * NT rows: the same select with every key held in
+// registers (row = u * NT + tid, round u < kRegB).  No LDS key array: the histogram passes
+// read registers, the threshold-bin candidates are placed by wave ballots (no atomics), and
+// the index-ordered compaction is one scan of the per-(round, wave) counts of rows above /
+// equal to the threshold: slot(row) = #above before it + min(#equal before it, need_eq).
+template <typename T, int NT>
+__device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __restrict__ sketch, int R,
+                                                 const Scale& sc, int32_t* __restrict__ rowlist,
+                                                 int32_t* __restrict__ slotmap, SmallSel& sh) {
+    constexpr int B = kRegB, NW = NT / 64;
+    const int n = (int)s.n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const T* sk = sketch + s.sketch_off;
+    for (int i = tid; i < 256; i += NT) sh.hist[i] = 0;  // first pass's histogram
+    uint32_t key[B];
+    if (R == 4 && s.kind == ARCTOPK_SEG_SKETCH && (s.sketch_off & 3) == 0) {
+        float4 v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (u * NT < n) v[u] = ldq<T, false>(sk, min(u * NT + tid, n - 1));
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            key[u] = u * NT < n ? energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc)) : 0u;
+    } else {
+        const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            key[u] = u * NT < n ? energy_key(row_energy(sk + (int64_t)min(u * NT + tid, n - 1) * stride,
+                                                        R, sc, s.kind))
+                                : 0u;
+    }
+    SEL_STAMP(0);
+    uint32_t kor = 0u, kand = ~0u;
+#pragma unroll
+    for (int u = 0; u < B; ++u)
+        if (u * NT + tid < n) {
+            kor |= key[u];
+            kand &= key[u];
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 0) {
+        sh.wor[wave] = kor;
+        sh.wand[wave] = kand;
+    }
+    __syncthreads();
+    kor = 0u;
+    kand = ~0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        kor |= sh.wor[w];
+        kand &= sh.wand[w];
+    }
+    SEL_STAMP(1);
+    const uint32_t diff = kor ^ kand;
+    int bit = diff ? 32 - __clz(diff) : 0;
+    uint32_t prefix = kand & ~((bit == 32) ? 0xFFFFFFFFu : ((1u << bit) - 1u));
+    uint32_t mask = (bit == 32) ? 0u : ~((1u << bit) - 1u);
+    int64_t kk = s.k_rows;
+    bool ranked = false, first = true;
+    while (bit > 0) {
+        const int w = bit < 8 ? bit : 8;
+        const int shift = bit - w;
+        const uint32_t dmask = (1u << w) - 1u;
+        if (!first) {
+            for (int i = tid; i < 256; i += NT) sh.hist[i] = 0;
+            __syncthreads();
+        }
+        first = false;
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (u * NT + tid < n && (key[u] & mask) == prefix)
+                atomicAdd(&sh.hist[(key[u] >> shift) & dmask], 1u);
+        __syncthreads();
+        SEL_STAMP(5);
+        if (wave == 0) {  // lane l owns digits 255-4l .. 252-4l (descending)
+            uint32_t c[4], sum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = sh.hist[255 - 4 * lane - q];
+                sum += c[q];
+            }
+            uint32_t incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t excl = incl - sum;
+            if ((uint64_t)excl < (uint64_t)kk && (uint64_t)incl >= (uint64_t)kk) {
+                uint32_t acc = excl;
+                int q = 0;
+                for (; q < 3; ++q) {
+                    if ((uint64_t)(acc + c[q]) >= (uint64_t)kk) break;
+                    acc += c[q];
+                }
+                sh.digit = 255 - 4 * lane - q;
+                sh.dcount = c[q];
+                sh.kk = kk - acc;
+            }
+        }
+        __syncthreads();
+        prefix |= sh.digit << shift;
+        mask |= dmask << shift;
+        kk = sh.kk;
+        bit = shift;
+        const uint32_t dcount = sh.dcount;
+        __syncthreads();
+        if (bit > 0 && dcount <= (uint32_t)kCandMax) {
+            // the threshold bin's keys -> sh.cand, placed by ballots (wave totals, then lanes)
+            uint64_t bm[B];
+            uint32_t wtot = 0;
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                bm[u] = __ballot(u * NT + tid < n && (key[u] & mask) == prefix);
+                wtot += (uint32_t)__popcll(bm[u]);
+            }
+            if (lane == 0) sh.wor[wave] = wtot;
+            __syncthreads();
+            uint32_t base = 0, nc = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; ++w2) {
+                const uint32_t c = sh.wor[w2];
+                base += w2 < wave ? c : 0u;
+                nc += c;
+            }
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                if ((bm[u] >> lane) & 1ull) sh.cand[base + (uint32_t)__popcll(bm[u] & lt)] = key[u];
+                base += (uint32_t)__popcll(bm[u]);
+            }
+            for (int i = (int)nc + tid; i < (int)((nc + 3) & ~3u); i += NT) sh.cand[i] = 0u;  // pad to x4
+            __syncthreads();
+            SEL_STAMP(6);
+            const uint4* c4 = reinterpret_cast<const uint4*>(sh.cand);
+            for (int t = tid; t < (int)nc; t += NT) {
+                const uint32_t v = sh.cand[t];
+                int gt = 0, ge = 0;
+                const int nq = ((int)nc + 3) >> 2;
+#pragma unroll 4
+                for (int j = 0; j < nq; ++j) {  // 16-B broadcast reads, 4 candidates each
+                    const uint4 c = c4[j];
+                    gt += (c.x > v) + (c.y > v) + (c.z > v) + (c.w > v);
+                    ge += (c.x >= v) + (c.y >= v) + (c.z >= v) + (c.w >= v);
+                }
+                if (v == 0u) ge -= (int)((nc + 3) & ~3u) - (int)nc;  // zero padding equals v only when v == 0
+                if (gt < kk && kk <= ge) {  // every writer writes the same (T, need)
+                    sh.T = v;
+                    sh.need_eq = kk - gt;
+                }
+            }
+            __syncthreads();
+            SEL_STAMP(7);
+            ranked = true;
+            break;
+        }
+    }
+    uint32_t thr;
+    int64_t need_eq;
+    if (ranked) {
+        thr = sh.T;
+        need_eq = sh.need_eq;
+    } else {  // every bit fixed: the threshold is the prefix itself
+        thr = prefix;
+        need_eq = kk;
+    }
+    SEL_STAMP(2);
+    uint64_t bg[B], be[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+        const bool ok = u * NT + tid < n;
+        bg[u] = __ballot(ok && key[u] > thr);
+        be[u] = __ballot(ok && key[u] == thr);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            sh.tg[u * NW + wave] = (uint32_t)__popcll(bg[u]);
+            sh.te[u * NW + wave] = (uint32_t)__popcll(be[u]);
+        }
+    }
+    __syncthreads();
+    if (wave == 0) table_exscan2<NW>(sh.tg, sh.te);
+    __syncthreads();
+    SEL_STAMP(3);
+    int32_t* rl = rowlist + s.sel_off;
+    int32_t* sm = slotmap + s.row_off;
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+        const int row = u * NT + tid;
+        if (row < n) {
+            const bool g = (bg[u] >> lane) & 1ull, e = (be[u] >> lane) & 1ull;
+            const int64_t gp = sh.tg[u * NW + wave] + (uint32_t)__popcll(bg[u] & lt);
+            const int64_t ep = sh.te[u * NW + wave] + (uint32_t)__popcll(be[u] & lt);
+            if (g || (e && ep < need_eq)) {
+                const int64_t slot = gp + (ep < need_eq ? ep : need_eq);
+                if (slot < s.k_rows) rl[slot] = row;  // bound: never store past the row list
+                sm[row] = (int32_t)slot;
+            } else {
+                sm[row] = -1;
+            }
+        }
+    }
+    SEL_STAMP(4);
+}
+
 template <typename T, int NT>
 __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs, int32_t seg_id,
                                                  const T* __restrict__ sketch, int R, Scale sc,
@@ -593,6 +849,10 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
     __shared__ SmallSel sh;
     const SegDev s = segs[seg_id];
     const int n = (int)s.n;
+    if (kSelRegPath && n <= kRegB * NT) {
+        select_small_reg<T, NT>(s, sketch, R, sc, rowlist, slotmap, sh);
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
     const T* sk = sketch + s.sketch_off;
@@ -802,7 +1062,8 @@ __global__ void __launch_bounds__(NT) k_select_small(const SegDev* __restrict__ 
                                                       const int32_t* __restrict__ seg_ids,
                                                       const T* __restrict__ sketch, int R,
                                                       Scale sc, int32_t* __restrict__ rowlist,
-                                                      int32_t* __restrict__ slotmap) {
+                                                      int32_t* __restrict__ slotmap, VDrawJob job) {
+    if (maybe_draw_v<T>(job, NT)) return;  // trailing blocks: the next call's projections
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
     select_small_seg<T, NT>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, keys);
 }
@@ -970,7 +1231,8 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
 
 // The refine of a batch's large segments and, in the same launch, the single-block selects
 // of the small segments (blocks b.cnt ..): both are latency-bound and independent, so they
-// overlap instead of running back to back.
+// overlap instead of running back to back.  Trailing blocks may draw the next call's
+// projections (VDrawJob).
 template <typename T>
 __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(MBatch b, MWorkspace* ws,
                                                                const uint32_t* __restrict__ ckey,
@@ -979,7 +1241,9 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(MBatch b, MWorksp
                                                                const int32_t* __restrict__ small_ids,
                                                                const T* __restrict__ sketch, int R,
                                                                Scale sc, int32_t* __restrict__ rowlist,
-                                                               int32_t* __restrict__ slotmap) {
+                                                               int32_t* __restrict__ slotmap,
+                                                               VDrawJob job) {
+    if (maybe_draw_v<T>(job, kRefineThreads)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     if ((int)blockIdx.x < b.cnt)
         arc_refine_item(b, (int)blockIdx.x, ws, ckey, cidx, dyn);
@@ -1781,7 +2045,8 @@ int launch_energy(const arctopk_plan* p, const void* sketch, int32_t ws, uint32_
 
 template <typename T>
 int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_t* rowlist, int32_t* slotmap,
-                  hipStream_t st) {
+                  VDrawJob job, bool* drawn, hipStream_t st) {
+    *drawn = false;
     const T* sketch = static_cast<const T*>(sketch_);
 #ifndef ARCTOPK_DIAG_NOSMALL
 #define ARCTOPK_DIAG_NOSMALL 0  // diagnostic builds only: skip the single-block select
@@ -1794,12 +2059,14 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
             const char* env = std::getenv("ARCTOPK_SEL_BIG_ROWS");
             return env ? std::max<int64_t>(1, std::atoll(env)) : (int64_t)4096;
         }();
+        const dim3 grid(p->n_small + job.n);
         if (p->small_lds > big_rows * 4 + 16)
-            hipLaunchKernelGGL((k_select_small<T, 1024>), dim3(p->n_small), dim3(1024), (size_t)p->small_lds,
-                               st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
+            hipLaunchKernelGGL((k_select_small<T, 1024>), grid, dim3(1024), (size_t)p->small_lds,
+                               st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap, job);
         else
-            hipLaunchKernelGGL((k_select_small<T, kST>), dim3(p->n_small), dim3(kST), (size_t)p->small_lds,
-                               st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap);
+            hipLaunchKernelGGL((k_select_small<T, kST>), grid, dim3(kST), (size_t)p->small_lds,
+                               st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap, job);
+        *drawn = true;
     }
     for (int bi = 0; bi < p->n_large_batches; ++bi) {
         const MBatch& b = p->h_large_batches[bi];
@@ -1837,10 +2104,13 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
             kRefineLdsCap * 4);
         if (lds_ok != hipSuccess) return (int)lds_ok;
         const int nsm = (bi == 0 && !ARCTOPK_DIAG_NOSMALL) ? p->n_small : 0;
+        VDrawJob bj = job;
+        if (bi != 0) bj.n = 0;
         uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
-        hipLaunchKernelGGL(k_arc_refine<T>, dim3(b.cnt + nsm), dim3(kRefineThreads), (size_t)kRefineLdsCap * 4,
-                           st, b, p->d_mws, ckey, ckey + p->mws_cap, p->d_segs, p->d_small, sketch, p->r,
-                           make_scale(ws), rowlist, slotmap);
+        hipLaunchKernelGGL(k_arc_refine<T>, dim3(b.cnt + nsm + bj.n), dim3(kRefineThreads),
+                           (size_t)kRefineLdsCap * 4, st, b, p->d_mws, ckey, ckey + p->mws_cap, p->d_segs,
+                           p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap, bj);
+        if (bi == 0) *drawn = true;
         e = (int)hipGetLastError();
         if (e) return e;
         e = ms_arc_write(b, p->d_keys, p->d_mws, p->mws_cap, rowlist, slotmap, st);
@@ -1908,12 +2178,32 @@ extern "C" int arctopk_row_energy(const arctopk_plan* p, const void* sketch, int
     return launch_energy<float>(p, sketch, ws, nullptr, energy, st);
 }
 
+extern "C" int arctopk_select_draw(const arctopk_plan* p, const void* sketch, int32_t ws,
+                                   int32_t* rowlist, int32_t* slotmap, const arctopk_plan* next,
+                                   uint64_t next_seed, void* next_V, void* stream) {
+    if (!p || !sketch || !rowlist || !slotmap || ws < 1) return ARCTOPK_EINVAL;
+    if (next && (!next_V || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    VDrawJob job{};
+    if (next && next->n_vchunk) {
+        job.segs = next->d_vdraw;
+        job.chunks = next->d_vchunk;
+        job.V = next_V;
+        job.seed = next_seed;
+        job.n = next->n_vchunk;
+    }
+    bool drawn = false;
+    const int e = p->dtype == ARCTOPK_BF16
+                      ? launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, job, &drawn, st)
+                      : launch_select<float>(p, sketch, ws, rowlist, slotmap, job, &drawn, st);
+    if (e) return e;
+    if (job.n && !drawn) return arctopk_draw_projections(next, next_seed, next_V, stream);
+    return 0;
+}
+
 extern "C" int arctopk_select(const arctopk_plan* p, const void* sketch, int32_t ws,
                               int32_t* rowlist, int32_t* slotmap, void* stream) {
-    if (!p || !sketch || !rowlist || !slotmap || ws < 1) return ARCTOPK_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    if (p->dtype == ARCTOPK_BF16) return launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, st);
-    return launch_select<float>(p, sketch, ws, rowlist, slotmap, st);
+    return arctopk_select_draw(p, sketch, ws, rowlist, slotmap, nullptr, 0, nullptr, stream);
 }
 
 extern "C" int arctopk_pack_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,

@@ -224,6 +224,18 @@ struct VDraw {         // one SKETCH tensor's torch.randn(m, r, device=...) draw
 };
 int vdraw_table(const arctopk_segment* segs, int nseg, int r, int device, VDraw* out, int* nout,
                 uint64_t* advance);
+constexpr int kVChunk = 1024;  // elements of V per draw block
+struct VChunk {        // one draw block's element range [lo, hi) of draw `entry`
+    int32_t entry;
+    uint32_t lo, hi;
+};
+struct VDrawJob {      // a projection draw riding in the trailing blocks of another launch
+    const VDraw* segs;
+    const VChunk* chunks;
+    void* V;
+    uint64_t seed;
+    int32_t n;         // trailing blocks (one chunk each); 0: no draw
+};
 
 struct Chunk {         // pack: selected-row range (mode 0) or row range (mode 1); decode: row range
     int32_t seg;
@@ -276,4 +288,6 @@ struct arctopk_plan {
     int n_vdraw;
     int64_t vdraw_max;                  // largest m * r
     uint64_t vdraw_advance;             // Philox offset after the bucket's draws
+    arctopk::VChunk* d_vchunk;          // the draws cut into kVChunk-element blocks
+    int n_vchunk;
 };

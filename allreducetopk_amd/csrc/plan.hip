@@ -49,6 +49,7 @@ int build_segments(const int64_t* dims, const int32_t* ndims, int32_t ntensors, 
         }
         if (numel == 0 || s.n == 0 || s.m == 0) return ARCTOPK_EEMPTY;
         if (numel >= (int64_t(1) << 31)) return ARCTOPK_EINVAL;  // 32-bit in-segment indexing
+        if (s.kind == ARCTOPK_SEG_SKETCH && s.m * r >= (int64_t(1) << 31)) return ARCTOPK_EINVAL;  // V: m * r
         // k = max(1, int(n * ratio)): float64 product, truncation (ref cal_k :173-187)
         int64_t k = (int64_t)((double)s.n * ratio);
         if (k < 1) k = 1;
@@ -311,6 +312,12 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         p->vdraw_advance = adv;
         for (const VDraw& d : vd) p->vdraw_max = std::max<int64_t>(p->vdraw_max, d.numel);
         ALLOC_COPY(p->d_vdraw, vd);
+        std::vector<VChunk> vc;
+        for (int i = 0; i < nvd; ++i)
+            for (int64_t lo = 0; lo < vd[i].numel; lo += kVChunk)
+                vc.push_back({i, (uint32_t)lo, (uint32_t)std::min<int64_t>(vd[i].numel, lo + kVChunk)});
+        p->n_vchunk = (int)vc.size();
+        ALLOC_COPY(p->d_vchunk, vc);
     }
 #undef ALLOC_COPY
     e = hipMalloc((void**)&p->d_keys, std::max<size_t>(4, info.rows_total * sizeof(uint32_t)));
@@ -351,6 +358,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     delete[] p->h_large_batches;
     if (p->d_mws) (void)hipFree(p->d_mws);
     if (p->d_vdraw) (void)hipFree(p->d_vdraw);
+    if (p->d_vchunk) (void)hipFree(p->d_vchunk);
     delete[] p->h_dec_begin;
     delete p;
     return 0;

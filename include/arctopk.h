@@ -129,6 +129,18 @@ int arctopk_select(const arctopk_plan* plan, const void* sketch, int32_t world_s
                    int32_t* rowlist, int32_t* slotmap, void* stream);
 
 /*
+ * arctopk_select, and in the same launch (its trailing blocks, which run beside the
+ * latency-bound select blocks) the device projections of the NEXT call: V_next =
+ * arctopk_draw_projections(next, next_seed).  The caller predicts the next call (plan and
+ * seed) and keeps V_next only when that call's seed matches; otherwise it draws again.
+ * `next` must have `plan`'s dtype and device; `next` = NULL is arctopk_select.
+ * Removes the draw launch (and its kernel boundary) from the next call's critical path.
+ */
+int arctopk_select_draw(const arctopk_plan* plan, const void* sketch, int32_t world_size,
+                        int32_t* rowlist, int32_t* slotmap, const arctopk_plan* next,
+                        uint64_t next_seed, void* next_V, void* stream);
+
+/*
  * K2 variant for tests/bit-exact checks: the per-row energy keys only
  * (float bits of the energy the reference feeds torch.topk), keys[row_off + row].
  */

@@ -65,6 +65,7 @@ SHAPE_SETS = [
     [[512, 512, 3, 3], [512], [256, 128, 1, 1], [64, 3, 7, 7]],
     [[32000, 2048], [2048], [5461, 2048], [2048, 5461]],
     [[1], [3, 1], [5, 4, 2, 2], [2, 1, 1, 1]],
+    [[8, 300000], [2, 3, 3, 3], [10], [2, 140000]],  # wide rows: m * r < 2^31 only
 ]
 
 
@@ -96,6 +97,7 @@ def test_plan_errors(lib):
     assert _describe(lib, [[4, 4]], r=9)[0] == 1001
     assert _describe(lib, [[4, 4]], ratio=0.0)[0] == 1001
     assert _describe(lib, [[4, 4]], ratio=1.5)[0] == 1001
+    assert _describe(lib, [[1, 1 << 29]], r=4)[0] == 1001  # V = m x r past 32-bit indexing
 
 
 def test_nd_indivisible_matches_reference_error():

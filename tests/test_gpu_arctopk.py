@@ -514,39 +514,54 @@ def test_device_bf16_rounding_matches_torch():
                                hex(int(ref[i]) & 0xFFFF)) for i in bad[:5]]
 
 
-def test_projection_prestaging_under_reordering_and_reseed():
-    """Projections are copied a call early for the predicted next (bucket, seed).  Calls out
-    of the predicted order, and an rng repositioned between calls, must still encode with
-    the projections of their own seed: every call's rows are checked against the oracle's
-    energies (wrong projections would rank rows differently) and its output bit for bit."""
+@pytest.mark.parametrize("projections", ["host", "device"])
+def test_projection_prestaging_under_reordering_and_reseed(projections):
+    """Projections are prepared a call early for the predicted next (bucket, seed): host
+    mode copies the CPU-stream V a call early, device mode draws it in the previous call's
+    select launch (arctopk_select_draw).  Calls out of the predicted order, an rng
+    repositioned between calls, and calls on another stream must still encode with the
+    projections of their own seed: every call's rows are checked against the oracle's
+    energies (wrong projections would rank rows differently) and its output bit for bit.
+    Bucket 1 has a segment large enough for the multi-block select, so the draw also rides
+    in the refine launch."""
     shapes_a = [[256, 1024], [64, 512], [300], [32, 16, 3, 3]]
-    shapes_b = [[128, 2048], [16, 8, 1, 1], [40, 96]]
+    shapes_b = [[128, 2048], [16, 8, 1, 1], [40, 96], [24000, 12]]
     layouts = {0: shapes_a, 1: shapes_b, 2: shapes_a}
     st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                         use_error_feedback="noef", seed=99)
-    st.projections = "host"  # the pre-staged H2D path of the CPU-stream projections
+    st.projections = projections
     ost = A.OracleState(r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback="noef",
                         seed=99)
-    order = [0, 1, 2] * 4 + [2, 0, 1, 1, 0] + [0, 1, 2] * 3 + ["reseed"] + [0, 1, 2] * 3 + [1, 2]
+    order = ([0, 1, 2] * 4 + [2, 0, 1, 1, 0] + [0, 1, 2] * 3 + ["reseed"] + [0, 1, 2] * 3 + [1, 2]
+             + ["stream", 0, 1, "stream", 2, 0, "stream", 1, 2])
     flips = 0
+    side = torch.cuda.Stream()
+    on_side = False
     for step, b in enumerate(order):
         if b == "reseed":  # both rngs repositioned: the look-ahead's seeds no longer come true
             st.rng.manual_seed(4242)
             ost.rng.manual_seed(4242)
             continue
+        if b == "stream":  # the caller moves to another stream (and back)
+            on_side = not on_side
+            continue
         shapes = layouts[b]
         G = _rand_bucket(shapes, 1000 + step)
-        out = group_topk_hook(st, SyntheticBucket(G.to(DEV), shapes, index=b, is_last=(b == 2))).wait()
+        with torch.cuda.stream(side if on_side else torch.cuda.default_stream()):
+            Gd = G.to(DEV)
+            out = group_topk_hook(st, SyntheticBucket(Gd, shapes, index=b, is_last=(b == 2))).wait()
         torch.cuda.synchronize()
         seed = ost.next_seed()
         plan = st._plans[b][1]
         rows = _gpu_rows(plan)
-        res = A.simulate_step([G], [None], None, shapes, 0.2, 4, "noef", seed, rows_override=rows)
+        res = A.simulate_step([G], [None], None, shapes, 0.2, 4, "noef", seed, rows_override=rows,
+                              proj_device=DEV if projections == "device" else None)
         for r_, nrm, s in zip(rows, res["norms"], plan.segments):
             flips += check_rows_tie_aware(r_, nrm, int(s.k_rows), band=2e-4)
         assert_bitwise(out, res["out"], f"call {step} (bucket {b}) output")
     assert flips <= 2, f"{flips} rows differ from the oracle's selection (near-ties only)"
-    assert st.prestage_hits > 10, f"pre-staged projections were used {st.prestage_hits} times"
+    hits = st.prestage_hits if projections == "host" else st.predraw_hits
+    assert hits > 10, f"projections prepared a call early were used {hits} times"
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -58,6 +58,26 @@ def test_seed_sequence_matches_reference_golden():
             assert ps.consume_seed(rng) == int(g.np(0, it, "seed")[0])
 
 
+def test_seed_lookahead_predicts_and_resynchronises():
+    """peek_next_seed (batched look-ahead draws) always names the seed the next
+    consume_seed returns -- across look-ahead refills and after the rng is repositioned
+    (the pre-drawn projections of arctopk_select_draw are keyed on it)."""
+    ps = ProjectionSource(4, depth=3, workers=1)
+    rng = torch.Generator().manual_seed(7)
+    ref = torch.Generator().manual_seed(7)
+    hits = 0
+    for call in range(70):
+        if call in (23, 50):  # repositioned between calls, both generators alike
+            rng.manual_seed(1000 + call)
+            ref.manual_seed(1000 + call)
+        peek = ps.peek_next_seed()
+        seed = ps.consume_seed(rng)
+        assert seed == int(torch.randint(0, 1_000_000_000, (1,), generator=ref).item())
+        hits += peek == seed
+    assert hits >= 70 - 3  # first call and the two repositions
+    ps.close()
+
+
 @pytest.mark.parametrize("seed", [0, 1, 440527571, 999_999_999])
 def test_projection_draw_matches_reference_stream(seed):
     shapes = [(10,), (40, 16), (4, 3, 3, 3), (16, 8, 1, 1), (96, 40), (2048, 2048), (5461, 33),
