@@ -18,6 +18,15 @@
 
 using namespace arctopk;
 
+DIAG_STAMPS(g_st_keys)
+DIAG_STAMPS(g_st_refine)
+#ifdef ARCTOPK_STAMPS
+extern "C" int arctopk_diag_stamps_k(int which, unsigned long long* host) {
+    return (int)(which == 0 ? hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_keys), sizeof(g_st_keys))
+                            : hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_refine), sizeof(g_st_refine)));
+}
+#endif
+
 #ifndef ARCTOPK_DIAG_KEYS
 #define ARCTOPK_DIAG_KEYS 0  // diagnostic builds only (scripts/selbench.hip): 1 = key pass without
 #endif                       // the histogram merge, 2 = also without the LDS histogram
@@ -644,6 +653,7 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const T* sk = sketch + s.sketch_off;
+    SEL_STAMP(0);
     for (int i = tid; i < 256; i += NT) sh.hist[i] = 0;  // first pass's histogram
     uint32_t key[B];
     if (R == 4 && s.kind == ARCTOPK_SEG_SKETCH && (s.sketch_off & 3) == 0) {
@@ -662,7 +672,7 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
                                                         R, sc, s.kind))
                                 : 0u;
     }
-    SEL_STAMP(0);
+    SEL_STAMP(8);
     uint32_t kor = 0u, kand = ~0u;
 #pragma unroll
     for (int u = 0; u < B; ++u)
@@ -1065,6 +1075,10 @@ __global__ void __launch_bounds__(NT) k_select_small(const SegDev* __restrict__ 
                                                       int32_t* __restrict__ slotmap, VDrawJob job) {
     if (maybe_draw_v<T>(job, NT)) return;  // trailing blocks: the next call's projections
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
+#ifdef ARCTOPK_DIAG_SEL_TWICE  // diagnostic builds only: second pass runs with a warm I-cache
+    select_small_seg<T, NT>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, keys);
+    __syncthreads();
+#endif
     select_small_seg<T, NT>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, keys);
 }
 
@@ -1092,56 +1106,74 @@ __device__ __forceinline__ uint32_t blk_exscan_u32(uint32_t v, uint32_t* lds, ui
     return before + x - v;
 }
 
-// ARC refine of one large segment (after ms_arc_compact), one 1024-thread block.  The
-// candidates (every key of the first-pass bin, with its index) are staged in LDS (the
-// indices too when they fit); two 10-bit LDS histogram rounds fix the remaining bits of the
-// threshold T; the candidates above / equal to T are counted per range and, with the keys
-// above the bin (compact pass), turned into per-range T-equal allowances (lowest ranges
-// first) and output offsets for ms_arc_write.
+// ARC refine of one large segment (after ms_arc_compact), one 1024-thread block.  Range r's
+// candidates (every key of the first-pass bin in that range, in index order) sit in its
+// own region of the candidate list; a block scan of the per-range counts lays them out
+// back to back, and they are staged in LDS (read from their regions when they do not fit).
+// Two 10-bit LDS histogram rounds fix the remaining bits of the threshold T; each thread
+// then counts its range's candidates above / equal to T, and with the keys above the bin
+// (compact pass) these become per-range T-equal allowances (lowest ranges first) and
+// output offsets for ms_arc_write.  No atomics outside LDS histograms.
 constexpr int kRefineThreads = 1024;
 static_assert(kRefineThreads == kMMaxRanges, "one range per thread in the offset scan");
 __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspace* ws,
                                                 const uint32_t* __restrict__ ckey,
-                                                const uint32_t* __restrict__ cidx,
                                                 uint32_t* __restrict__ stage /* LDS */) {
     constexpr int NT = kRefineThreads, NW = NT / 64, U = 8, W2 = 10;
-    constexpr int HALF = kRefineLdsCap / 2;
     __shared__ uint32_t h[1 << W2];
-    __shared__ uint32_t cgt[kMMaxRanges], ceq[kMMaxRanges];
+    __shared__ uint32_t roff[kMMaxRanges], rcnt[kMMaxRanges];  // later: per-range (eq, gt) counts
     __shared__ uint32_t lds[NW], s_digit, s_acc;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     const MItem it = b.it[t];
     MState s = ws->st[t];
     const int nr = it.nranges;
-    const uint32_t gt_above = tid < nr ? ws->cnt_gt[t][tid] : 0u;  // prefetched: keys above the bin
-    const int64_t nc = (int64_t)ws->ncand[t].v;
-    const uint32_t* ck = ckey + it.cand_off;
-    const uint32_t* ci = cidx + it.cand_off;
-    cgt[tid] = 0u;
-    ceq[tid] = 0u;
-    if (nc <= kRefineLdsCap) {  // usual case: one round trip, then everything from LDS
-        const bool with_idx = nc <= HALF;
-        for (int64_t base = 0; base < nc; base += (int64_t)NT * U) {
-            uint32_t kv[U], iv[U];
+    const uint32_t gt_above = tid < nr ? ws->cnt_gt[t][tid] : 0u;  // keys above the bin
+    const uint32_t my_cnt = tid < nr ? ws->cnt_cand[t][tid] : 0u;
+    uint32_t nc32;
+    const uint32_t my_off = blk_exscan_u32<NW>(my_cnt, lds, &nc32);
+    roff[tid] = my_off;
+    rcnt[tid] = my_cnt;
+    __syncthreads();
+    const int64_t nc = nc32;
+    const uint32_t* src = ckey + it.cand_off;
+    // global index of candidate p (p-th in range order): range = last r with roff[r] <= p
+    auto gidx = [&](uint32_t p) -> int64_t {
+        int lo = 0, hi = nr - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (roff[mid] <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        return (int64_t)lo * it.range + (p - roff[lo]);
+    };
+    const bool staged = nc <= kRefineLdsCap;
+    const int lane = tid & 63, wave = tid >> 6;
+    if (staged) {
+        // usual case, one round trip: wave w copies ranges w, w + NW, ..., lane j candidate j
+        // of each (a range's first 64 in one load, every range's load in flight before the
+        // stores; longer ranges loop), then everything is read from LDS
+        constexpr int RB = 16;
+        for (int r0 = wave; r0 < nr; r0 += NW * RB) {
+            uint32_t v[RB];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t i = base + u * NT + tid;
-                kv[u] = i < nc ? ck[i] : 0u;
-                iv[u] = (with_idx && i < nc) ? ci[i] : 0u;
+            for (int q = 0; q < RB; ++q) {
+                const int r = r0 + q * NW;
+                v[q] = (r < nr && (uint32_t)lane < rcnt[r]) ? src[(int64_t)r * it.range + lane] : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t i = base + u * NT + tid;
-                if (i < nc) {
-                    stage[i] = kv[u];
-                    if (with_idx) stage[HALF + i] = iv[u];
+            for (int q = 0; q < RB; ++q) {
+                const int r = r0 + q * NW;
+                if (r < nr) {
+                    const uint32_t c = rcnt[r], o = roff[r];
+                    if ((uint32_t)lane < c) stage[o + lane] = v[q];
+                    for (uint32_t j = 64 + lane; j < c; j += 64) stage[o + j] = src[(int64_t)r * it.range + j];
                 }
             }
         }
         __syncthreads();
-        ck = stage;
-        if (with_idx) ci = stage + HALF;
     }
+    DIAG_STAMP(g_st_refine, 2);
+    auto key_at = [&](int64_t i) -> uint32_t { return staged ? stage[i] : src[gidx((uint32_t)i)]; };
     while (s.bit > 0) {
         const int w = s.bit < W2 ? s.bit : W2;
         const int shift = s.bit - w;
@@ -1153,7 +1185,7 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t i = base + u * NT + tid;
-                kv[u] = i < nc ? ck[i] : 0u;
+                kv[u] = i < nc ? key_at(i) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1177,46 +1209,29 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
         s.bit = shift;
         __syncthreads();  // s_digit / s_acc / h are rewritten by the next round
     }
+    DIAG_STAMP(g_st_refine, 3);
     const uint32_t T = s.prefix;
-    for (int64_t base = 0; base < nc; base += (int64_t)NT * U) {
-        uint32_t kv[U], iv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t i = base + u * NT + tid;
-            kv[u] = i < nc ? ck[i] : 0u;
+    // wave per range: its candidates above / equal to T by ballots; the counts replace the
+    // range's (count, offset) entries (read first, by the same wave)
+    for (int r = wave; r < nr; r += NW) {
+        const uint32_t c = rcnt[r], o = roff[r];
+        uint32_t g = 0, e = 0;
+        for (uint32_t j0 = 0; j0 < c; j0 += 64) {
+            const uint32_t j = j0 + (uint32_t)lane;
+            const uint32_t k = j < c ? (staged ? stage[o + j] : src[(int64_t)r * it.range + j]) : 0u;
+            g += (uint32_t)__popcll(__ballot(j < c && k > T));
+            e += (uint32_t)__popcll(__ballot(j < c && k == T));
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // indices only of the keys that count
-            const int64_t i = base + u * NT + tid;
-            iv[u] = (i < nc && kv[u] >= T) ? ci[i] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            // segmented wave reduction: a wave's 64 consecutive candidates come from one or
-            // two block tiles of the compact pass, so one LDS atomic pair per distinct range
-            const int64_t i = base + u * NT + tid;
-            const bool valid = i < nc && kv[u] >= T;
-            const int r = valid ? (int)(iv[u] / (uint32_t)it.range) : -1;
-            const bool gt = valid && kv[u] > T;
-            uint64_t pending = __ballot(valid);
-            while (pending) {
-                const int leader = __ffsll((long long)pending) - 1;
-                const int rl = __shfl(r, leader, 64);
-                const bool mine = valid && r == rl;
-                const uint32_t ng = (uint32_t)__popcll(__ballot(mine && gt));
-                const uint32_t ne = (uint32_t)__popcll(__ballot(mine && !gt));
-                if (lane == leader) {
-                    if (ng) atomicAdd(&cgt[rl], ng);
-                    if (ne) atomicAdd(&ceq[rl], ne);
-                }
-                pending &= ~__ballot(mine);
-            }
+        if (lane == 0) {
+            rcnt[r] = g;
+            roff[r] = e;
         }
     }
     __syncthreads();
+    DIAG_STAMP(g_st_refine, 4);
     const int r = tid;
-    const uint32_t eq = r < nr ? ceq[r] : 0u;
-    const uint32_t gt = r < nr ? gt_above + cgt[r] : 0u;
+    const uint32_t gt = (tid < nr ? rcnt[tid] : 0u) + gt_above;
+    const uint32_t eq = tid < nr ? roff[tid] : 0u;
     uint32_t tot;
     const uint32_t eq_before = blk_exscan_u32<NW>(eq, lds, &tot);
     int64_t take = s.kk - (int64_t)eq_before;
@@ -1236,50 +1251,61 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
 template <typename T>
 __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(MBatch b, MWorkspace* ws,
                                                                const uint32_t* __restrict__ ckey,
-                                                               const uint32_t* __restrict__ cidx,
                                                                const SegDev* __restrict__ segs,
                                                                const int32_t* __restrict__ small_ids,
                                                                const T* __restrict__ sketch, int R,
                                                                Scale sc, int32_t* __restrict__ rowlist,
                                                                int32_t* __restrict__ slotmap,
                                                                VDrawJob job) {
-    if (maybe_draw_v<T>(job, kRefineThreads)) return;
+    DIAG_STAMP(g_st_refine, 0);
+    if (maybe_draw_v<T>(job, kRefineThreads)) {
+        DIAG_STAMP(g_st_refine, 1);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     if ((int)blockIdx.x < b.cnt)
-        arc_refine_item(b, (int)blockIdx.x, ws, ckey, cidx, dyn);
+        arc_refine_item(b, (int)blockIdx.x, ws, ckey, dyn);
     else
         select_small_seg<T, kRefineThreads>(segs, small_ids[blockIdx.x - b.cnt], sketch, R, sc, rowlist,
                                             slotmap, dyn);
+    DIAG_STAMP(g_st_refine, 1);
 }
 
 struct KeysGrid {
     int32_t first[kMB + 1];  // first block of each item in the flat key-pass grid
 };
 
+
 // Larger segments: energy keys into global memory, fused with the first radix pass of
 // the multi-block select (mselect.h): each block histograms its keys' top 12 bits in LDS
 // and merges the non-empty bins into the segment's global histogram; the last block to
 // finish picks the bin holding the k-th largest key (ms_arc_first_digit).
-template <typename T>
-__global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ segs,
+template <typename T, int KT>
+__global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs,
                                                   const int32_t* __restrict__ ids, int first,
                                                   const T* __restrict__ sketch, int R, Scale sc,
                                                   uint32_t* __restrict__ keys, MWorkspace* ws,
                                                   KeysGrid kg) {
-    __shared__ uint32_t h[kMBins], hc[kMBins];
+    // one 16 KiB histogram (the compacted (bin, count) list is packed into it in place):
+    // LDS sets the occupancy, and every block of the grid must be resident in one round
+    __shared__ uint32_t h[kMBins];
     __shared__ uint32_t s_nnz;
+    DIAG_STAMP(g_st_keys, 0);
     // flat grid: item t owns blocks [kg.first[t], kg.first[t + 1])
     int t = 0;
     while ((int)blockIdx.x >= kg.first[t + 1]) ++t;
     const int bx = (int)blockIdx.x - kg.first[t];
     const uint32_t nblk = (uint32_t)(kg.first[t + 1] - kg.first[t]);
     const SegDev s = segs[ids[first + t]];
-    for (int i = threadIdx.x; i < kMBins; i += 256) h[i] = 0u;
+#ifdef ARCTOPK_STAMPS
+    if (threadIdx.x == 0) g_st_keys[blockIdx.x * 8 + 4] = (unsigned long long)t;
+#endif
+    for (int i = threadIdx.x; i < kMBins; i += KT) h[i] = 0u;
     if (threadIdx.x == 0) s_nnz = 0u;
     __syncthreads();
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
-    const int64_t gs = (int64_t)nblk * 256;
-    int64_t row = (int64_t)bx * 256 + threadIdx.x;
+    const int64_t gs = (int64_t)nblk * KT;
+    int64_t row = (int64_t)bx * KT + threadIdx.x;
     const T* sk = sketch + s.sketch_off;
     uint32_t* kout = keys + s.row_off;
     if (stride == 4 && (s.sketch_off & 3) == 0) {  // r = 4: one quad load per row, UK rows in flight
@@ -1316,21 +1342,23 @@ __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ seg
         }
     }
     __syncthreads();
+    DIAG_STAMP(g_st_keys, 1);
 #if ARCTOPK_DIAG_KEYS >= 1  // diagnostic builds (scripts/selbench.hip): stop after the LDS pass
     if (h[threadIdx.x] == 12345678u) kout[0] = 0u;
     return;
 #endif
     // Merge into the item's global histogram.  Memory-side atomics cost about one wave
     // instruction per 50 ns per CU whatever their lane count, so the non-empty bins are first
-    // compacted into a dense LDS list (bins in h, counts in hc) and merged by full wave
-    // instructions: a few per block instead of 64.
-    {
-        constexpr int PB = kMBins / 256;
+    // compacted into a dense LDS list (in place: bin << 20 | count, counts < 2^20 rows per
+    // block) and merged by full wave instructions: a few per block instead of 64.
+    constexpr int kCountBits = 32 - 12;
+    if ((uint64_t)(s.n + nblk - 1) / nblk < (1ull << kCountBits)) {
+        constexpr int PB = kMBins / KT;
         const int lane = threadIdx.x & 63;
         const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
         uint32_t c[PB];
 #pragma unroll
-        for (int q = 0; q < PB; ++q) c[q] = h[q * 256 + threadIdx.x];
+        for (int q = 0; q < PB; ++q) c[q] = h[q * KT + threadIdx.x];
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < PB; ++q) {
@@ -1339,18 +1367,25 @@ __global__ void __launch_bounds__(256) k_arc_keys(const SegDev* __restrict__ seg
             uint32_t base = 0;
             if (lane == 0 && bm) base = atomicAdd(&s_nnz, (uint32_t)__popcll(bm));
             base = __shfl(base, 0, 64);
-            if (ne) {
-                const uint32_t pos = base + (uint32_t)__popcll(bm & lt);
-                h[pos] = (uint32_t)(q * 256 + threadIdx.x);
-                hc[pos] = c[q];
-            }
+            if (ne) h[base + (uint32_t)__popcll(bm & lt)] = ((uint32_t)(q * KT + threadIdx.x) << kCountBits) | c[q];
         }
         __syncthreads();
         const uint32_t nnz = s_nnz;
-        for (uint32_t i = threadIdx.x; i < nnz; i += 256) atomicAdd(&ws->hist[t][hist_slot((int)h[i])], hc[i]);
+        for (uint32_t i = threadIdx.x; i < nnz; i += KT) {
+            const uint32_t e = h[i];
+            atomicAdd(&ws->hist[t][hist_slot((int)(e >> kCountBits))], e & ((1u << kCountBits) - 1u));
+        }
+    } else {  // > 2^20 rows per block: every non-empty bin on its own
+        for (int i = threadIdx.x; i < kMBins; i += KT)
+            if (h[i]) atomicAdd(&ws->hist[t][hist_slot(i)], h[i]);
     }
-    if (!ms_arrive_last(&ws->done[t].v, nblk)) return;
-    ms_arc_first_digit(ws, t, s.k_rows);
+    DIAG_STAMP(g_st_keys, 2);
+    if (!ms_arrive_last(&ws->done[t].v, nblk)) {
+        DIAG_STAMP(g_st_keys, 3);
+        return;
+    }
+    ms_arc_first_digit<KT>(ws, t, s.k_rows);
+    DIAG_STAMP(g_st_keys, 3);
 }
 
 __device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m >= 256; }
@@ -2072,28 +2107,38 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         const MBatch& b = p->h_large_batches[bi];
         int64_t maxn = 0;
         for (int i = 0; i < b.cnt; ++i) maxn = std::max<int64_t>(maxn, b.it[i].n);
-        // >= 32 rows per lane: few blocks per segment keep the global histogram merge
-        // (one memory-side atomic per non-empty bin and block) short
-        // rows per block: 8 per lane (one round of loads in flight) for latency; the histogram
-        // merge is a few compacted atomic instructions per block, so many blocks are cheap
-        static const int64_t rpb_env = [] {  // tuning switch (A/B): rows per block
-            const char* env = std::getenv("ARCTOPK_KEYS_ROWS_PER_BLOCK");
-            return env ? std::max(256, std::atoi(env)) : 2048;
+        // Rows per block and blocks per item: about one block per CU for the whole batch, every
+        // block resident at once, equal rows per block (the pass is bandwidth-bound: an item
+        // with fewer rows per block would finish early and leave its bandwidth share idle), and
+        // few blocks, since each block merges its histogram with memory-side atomics on the
+        // same hot words (measured on ResNet-50's bucket: 1120 x 256-thread blocks spent ~10 us
+        // in that merge tail)
+        static const int keys_threads = [] {  // tuning switch (A/B): key-pass block size
+            const char* env = std::getenv("ARCTOPK_KEYS_THREADS");
+            return env && std::atoi(env) == 256 ? 256 : 1024;
         }();
-        // ... but every block merges the same hot bins, and memory-side atomics serialise per
-        // word: an item gets at most kmax blocks (measured: 2048 rows per block for a 131 K-row
-        // item 36 vs 47 us at 8192; a 1 M-row item wants ~8192)
-        static const int64_t kmax = [] {  // tuning switch (A/B): blocks per item
-            const char* env = std::getenv("ARCTOPK_KEYS_MAX_BLOCKS");
-            return env ? std::max(1, std::atoi(env)) : 128;
+        static const int64_t target_blocks = [] {  // tuning switch (A/B): key-pass grid target
+            const char* env = std::getenv("ARCTOPK_KEYS_BLOCKS");  // 1024-thread blocks: ~one
+            return env ? std::max(1, std::atoi(env)) : 224;  // per CU fits (263 did not: 2 rounds)
         }();
+        static const int64_t min_rpb = [] {  // tuning switch (A/B): rows per block at least
+            const char* env = std::getenv("ARCTOPK_KEYS_MIN_ROWS");
+            return env ? std::max(256, std::atoi(env)) : 4096;
+        }();
+        int64_t rows = 0;
+        for (int i = 0; i < b.cnt; ++i) rows += b.it[i].n;
+        const int64_t rpb = std::max<int64_t>(min_rpb, (rows + target_blocks - 1) / target_blocks);
         KeysGrid kg;
         kg.first[0] = 0;
         for (int i = 0; i < b.cnt; ++i)
             kg.first[i + 1] = kg.first[i] + (int32_t)std::max<int64_t>(
-                1, std::min<int64_t>(std::min<int64_t>(kmax, kMHistBlocks), (b.it[i].n + rpb_env - 1) / rpb_env));
-        hipLaunchKernelGGL(k_arc_keys<T>, dim3(kg.first[b.cnt]), dim3(256), 0, st, p->d_segs, p->d_large,
-                           bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg);
+                1, std::min<int64_t>(kMHistBlocks, (b.it[i].n + rpb - 1) / rpb));
+        if (keys_threads == 256)
+            hipLaunchKernelGGL((k_arc_keys<T, 256>), dim3(kg.first[b.cnt]), dim3(256), 0, st, p->d_segs,
+                               p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg);
+        else
+            hipLaunchKernelGGL((k_arc_keys<T, 1024>), dim3(kg.first[b.cnt]), dim3(1024), 0, st, p->d_segs,
+                               p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg);
 #if ARCTOPK_DIAG_STOP == 1 || ARCTOPK_DIAG_KEYS >= 1  // diagnostic builds only
         continue;
 #endif
@@ -2108,7 +2153,7 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         if (bi != 0) bj.n = 0;
         uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
         hipLaunchKernelGGL(k_arc_refine<T>, dim3(b.cnt + nsm + bj.n), dim3(kRefineThreads),
-                           (size_t)kRefineLdsCap * 4, st, b, p->d_mws, ckey, ckey + p->mws_cap, p->d_segs,
+                           (size_t)kRefineLdsCap * 4, st, b, p->d_mws, ckey, p->d_segs,
                            p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap, bj);
         if (bi == 0) *drawn = true;
         e = (int)hipGetLastError();

@@ -5,6 +5,20 @@
 
 #include "arctopk.h"
 
+// Diagnostic builds only (-DARCTOPK_STAMPS, scripts/selbench.hip): per-block timestamps of
+// the multi-block select kernels, [block][8 slots] in 100 MHz ticks (s_memrealtime).
+#ifdef ARCTOPK_STAMPS
+#define DIAG_STAMPS(name) __device__ unsigned long long name[4096 * 8];
+#define DIAG_STAMP(arr, i)                                                                    \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                            \
+            arr[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
+#else
+#define DIAG_STAMPS(name)
+#define DIAG_STAMP(arr, i) do {} while (0)
+#endif
+
 namespace arctopk {
 
 constexpr int kMaxR = 8;           // sketch rank supported by the kernels

@@ -73,6 +73,7 @@ struct MWorkspace {
     uint32_t cnt_eq[kMB][kMMaxRanges];
     uint32_t take_eq[kMB][kMMaxRanges];
     uint32_t sel_before[kMB][kMMaxRanges];
+    uint32_t cnt_cand[kMB][kMMaxRanges];   // ARC: candidates of each range (k_arc_compact)
     // followed by the candidate lists: uint32 key[cap_total], uint32 index[cap_total]
 };
 
@@ -124,16 +125,17 @@ __device__ inline void ms_init_item(MWorkspace* ws, int t, int64_t k, uint32_t k
     }
 }
 
-// ARC first pass, run by the LAST block of the fused key kernel (256 threads) once every
+// ARC first pass, run by the LAST block of the fused key kernel (NT threads) once every
 // block merged its LDS histogram of the keys' top 12 value bits (bits 30..19: energies are
 // non-negative and NaN maps to 0x7FFFFFFF, so bit 31 is always clear) into
 // ws->hist[t]: read-and-clear the bins (leaving them zero for the next call), find the
 // bin holding the k-th largest key, and start the item in candidate mode on that bin
 // (cand_cap = n for ARC items: every key of the bin fits).
 constexpr int kArcShift = 31 - 12;
+template <int NT>
 __device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k) {
-    __shared__ uint32_t s_w[4], s_d, s_acc;
-    constexpr int PER = kMBins / 256;
+    __shared__ uint32_t s_w[NT / 64], s_d, s_acc;
+    constexpr int PER = kMBins / NT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t c[PER], sum = 0;
 #pragma unroll
@@ -194,16 +196,18 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
               int32_t* out_slot, hipStream_t st);
 
 // ARC selection after the fused key kernel (keys + first-pass histogram + digit, every
-// item in candidate mode), in three launches per batch: ms_arc_compact (the bin's keys ->
-// candidate list, per-range counts above the bin), then the refine (arctopk_kernels.hip:
-// one block per item fixes the remaining bits from the candidates and computes per-range
-// offsets; the single-block selects of the small segments share that launch), then
-// ms_arc_write (ascending row list and slot map).
+// item in candidate mode), in three launches per batch: ms_arc_compact (per range: the
+// bin's keys -> that range's own region of the candidate list, the counts of candidates
+// and of keys above the bin; no atomics), then the refine (arctopk_kernels.hip: one block
+// per item fixes the remaining bits from the candidates and computes per-range offsets;
+// the single-block selects of the small segments share that launch), then ms_arc_write
+// (ascending row list and slot map).  ARC candidate regions: range r of item t owns
+// ckey[cand_off + r * range, + range) (cand_cap = n).
 int ms_arc_compact(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
                    hipStream_t st);
 int ms_arc_write(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
                  int32_t* out_idx, int32_t* out_slot, hipStream_t st);
-// candidate keys the ARC refine stages in LDS (and their indices too, up to half of it)
+// candidate keys the ARC refine stages in LDS (more are read from their ranges' regions)
 constexpr int kRefineLdsCap = 32768;
 
 }  // namespace arctopk

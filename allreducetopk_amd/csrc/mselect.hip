@@ -50,6 +50,9 @@ __device__ __forceinline__ bool ms_locate(const MBatch& b, int* t, int* r) {
     return false;
 }
 
+DIAG_STAMPS(g_st_compact)
+DIAG_STAMPS(g_st_write)
+
 static int total_ranges(const MBatch& b) {
     int n = 0;
     for (int i = 0; i < b.cnt; ++i) n += b.it[i].nranges;
@@ -242,6 +245,63 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
     }
 }
 
+// ARC: one block per range, no atomics: the keys above the first-pass bin are counted and
+// the bin's keys are copied (in index order) into the range's own candidate region;
+// cnt_gt / cnt_cand per range for the refine.
+__global__ void __launch_bounds__(256) k_arc_compact(MBatch b, const uint32_t* __restrict__ keys,
+                                                     MWorkspace* ws, uint32_t* __restrict__ ckey) {
+    __shared__ uint32_t lds[4], s_cnt[4];
+    DIAG_STAMP(g_st_compact, 0);
+    int t, r;
+    if (!ms_locate(b, &t, &r)) return;
+    const MItem it = b.it[t];
+    const MState s = ws->st[t];
+    const uint32_t hi = s.p1 | ~s.m1;  // largest key of the bin
+    const int64_t r0 = (int64_t)r * it.range;
+    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t* dst = ckey + it.cand_off + r0;
+    uint32_t gt = 0, run = 0;
+    for (int64_t tile = r0; tile < r1; tile += kMTile) {
+        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
+        uint32_t kv[kPerLane];
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) kv[j] = keys[it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)];
+        uint64_t bm[kPerLane];
+        uint32_t nin = 0;
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const bool valid = wb + j * 64 + lane < r1;
+            gt += (valid && kv[j] > hi) ? 1u : 0u;
+            bm[j] = __ballot(valid && (kv[j] & s.m1) == s.p1);
+            nin += popc64(bm[j]);
+        }
+        if (lane == 0) s_cnt[wave] = nin;
+        __syncthreads();
+        uint32_t base = run, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            base += w < wave ? s_cnt[w] : 0u;
+            tot += s_cnt[w];
+        }
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            if ((bm[j] >> lane) & 1ull) dst[base + popc64(bm[j] & lt)] = kv[j];
+            base += popc64(bm[j]);
+        }
+        run += tot;
+        __syncthreads();  // s_cnt is rewritten by the next tile
+    }
+    uint32_t total;
+    (void)block_exscan_u32<4>(gt, lds, &total);
+    if (threadIdx.x == 0) {
+        ws->cnt_gt[t][r] = total;
+        ws->cnt_cand[t][r] = run;
+    }
+    DIAG_STAMP(g_st_compact, 1);
+}
+
 // Per-range counts of the bin's keys > T and == T (T = the final prefix), added to the
 // compact pass's counts: from the candidates or, in full mode, by rescanning each
 // range.  The last block then turns them into per-range T-equal allowances (lowest
@@ -347,6 +407,7 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
                                                   float* __restrict__ out_val,
                                                   int32_t* __restrict__ out_slot) {
     __shared__ uint32_t s_eq[4], s_gt[4];
+    DIAG_STAMP(g_st_write, 0);
     int t, r;
     if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
@@ -412,9 +473,20 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
         run += tgt + te;
         take_left -= te;
     }
+#ifdef ARCTOPK_STAMPS
+    __syncthreads();
+#endif
+    DIAG_STAMP(g_st_write, 1);
 }
 
 }  // namespace
+
+#ifdef ARCTOPK_STAMPS
+extern "C" int arctopk_diag_stamps_m(int which, unsigned long long* host) {
+    return (int)(which == 0 ? hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_compact), sizeof(g_st_compact))
+                            : hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_write), sizeof(g_st_write)));
+}
+#endif
 
 void ms_item_geometry(MItem& it) {
     const int64_t tiles = (it.n + kMTile - 1) / kMTile;
@@ -484,9 +556,7 @@ int ms_arc_compact(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_
     int gr;
     if (int e = arc_batch_check(b, cap_total, &gr)) return e;
     uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
-    uint32_t* cidx = ckey + cap_total;
-    hipLaunchKernelGGL(k_ms_compact<false>, dim3(total_ranges(b)), dim3(256), 0, st, b, keys, nullptr, ws, ckey,
-                       cidx);
+    hipLaunchKernelGGL(k_arc_compact, dim3(total_ranges(b)), dim3(256), 0, st, b, keys, ws, ckey);
     return (int)hipGetLastError();
 }
 

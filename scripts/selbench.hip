@@ -6,13 +6,20 @@
 //   ./scripts/selbench resnet50|resnet18b0|resnet18b1|llama|roberta|headline [reps]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <map>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
 #include <vector>
 
 #include "arctopk.h"
+#ifdef ARCTOPK_STAMPS
+extern "C" int arctopk_diag_stamps_k(int which, unsigned long long* host);
+extern "C" int arctopk_diag_stamps_m(int which, unsigned long long* host);
+#endif
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("hip %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
@@ -75,7 +82,11 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<float> ts;
+    const bool evict = getenv("EVICT") != nullptr;  // stream 512 MiB between selects (cold L2 / I-cache)
+    void* big = nullptr;
+    if (evict) CK(hipMalloc(&big, (size_t)512 << 20));
     for (int r = 0; r < reps; ++r) {
+        if (evict) CK(hipMemsetAsync(big, r & 0xFF, (size_t)512 << 20, nullptr));
         CK(hipEventRecord(e0, nullptr));
         st = arctopk_select(p, sk, 1, rl, sm, nullptr);
         CK(hipEventRecord(e1, nullptr));
@@ -99,5 +110,66 @@ int main(int argc, char** argv) {
     }
     printf("%-11s rows %9lld segs %3d select median %8.2f us  min %8.2f  %s\n", which.c_str(),
            (long long)info.rows_total, info.nseg, ts[ts.size() / 2], ts[0], bad ? "BAD COUNTS" : "ok");
+#ifdef ARCTOPK_STAMPS
+    {   // per-block timeline of the last select (ticks of 10 ns, relative to the key pass start)
+        const size_t NS = 4096 * 8;
+        std::vector<unsigned long long> st[4];
+        for (auto& v : st) v.assign(NS, 0ull);
+        for (int k = 0; k < 2; ++k) {
+            CK((hipError_t)arctopk_diag_stamps_k(k, st[k == 0 ? 0 : 2].data()));
+            CK((hipError_t)arctopk_diag_stamps_m(k, st[k == 0 ? 1 : 3].data()));
+        }
+        const char* names[4] = {"keys", "compact", "refine", "write"};
+        unsigned long long t0 = ~0ull;
+        for (size_t b = 0; b < 4096 && st[0][b * 8]; ++b) t0 = std::min(t0, st[0][b * 8]);
+        for (int k = 0; k < 4; ++k) {
+            std::vector<double> dur, s01, s12, s23;
+            unsigned long long smin = ~0ull, smax = 0, emax = 0;
+            int nb = 0;
+            for (size_t b = 0; b < 4096; ++b) {
+                const unsigned long long* e = &st[k][b * 8];
+                if (!e[0] || e[0] < t0) break;
+                ++nb;
+                const int last = (k == 0) ? 3 : 1;
+                smin = std::min(smin, e[0]);
+                smax = std::max(smax, e[0]);
+                emax = std::max(emax, e[last]);
+                dur.push_back((double)(e[last] - e[0]) * 0.01);
+                if (k == 0) {
+                    s01.push_back((e[1] - e[0]) * 0.01);
+                    s12.push_back((e[2] - e[1]) * 0.01);
+                    s23.push_back((e[3] - e[2]) * 0.01);
+                }
+            }
+            auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
+            auto mx = [](const std::vector<double>& v) { double m = 0; for (double x : v) m = std::max(m, x); return m; };
+            printf("  %-8s blocks %5d  start %7.2f .. %7.2f us  end %7.2f us  block med %6.2f max %6.2f",
+                   names[k], nb, (smin - t0) * 0.01, (smax - t0) * 0.01, (emax - t0) * 0.01, med(dur), mx(dur));
+            if (k == 2) {  // refine items (blocks 0 .. nitems-1 write slots 2-4)
+                for (size_t b = 0; b < 64; ++b) {
+                    const unsigned long long* e = &st[2][b * 8];
+                    if (!e[2] || e[2] < e[0]) break;
+                    printf("\n    item %2zu: stage %.2f rounds %.2f count %.2f offsets %.2f (start %.2f)", b,
+                           (e[2] - e[0]) * 0.01, (e[3] - e[2]) * 0.01, (e[4] - e[3]) * 0.01, (e[1] - e[4]) * 0.01,
+                           (e[0] - t0) * 0.01);
+                }
+            }
+            if (k == 0) {  // per item: blocks, median / max load+hist, max end
+                std::map<int, std::vector<double>> lh, en;
+                for (size_t b = 0; b < (size_t)nb; ++b) {
+                    const unsigned long long* e = &st[0][b * 8];
+                    lh[(int)e[4]].push_back((e[1] - e[0]) * 0.01);
+                    en[(int)e[4]].push_back((e[3] - t0) * 0.01);
+                }
+                for (auto& kv : lh)
+                    printf("\n    item %2d: blocks %4zu load+hist med %6.2f max %6.2f  end max %6.2f", kv.first,
+                           kv.second.size(), med(kv.second), mx(kv.second), mx(en[kv.first]));
+            }
+            if (k == 0) printf("  [load+hist med %.2f max %.2f | merge med %.2f max %.2f | arrive/digit max %.2f]",
+                               med(s01), mx(s01), med(s12), mx(s12), mx(s23));
+            printf("\n");
+        }
+    }
+#endif
     return 0;
 }

@@ -2,6 +2,8 @@
 // hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -DARCTOPK_SEL_STAMPS -Iinclude -Iallreducetopk_amd/csrc scripts/seltest.hip -o scripts/seltest
 #include "../allreducetopk_amd/csrc/plan.hip"
 #include "../allreducetopk_amd/csrc/arctopk_kernels.hip"
+#include "../allreducetopk_amd/csrc/mselect.hip"
+#include "../allreducetopk_amd/csrc/vdraw.hip"
 #include <cstdio>
 #include <vector>
 #include <random>
@@ -32,8 +34,8 @@ int main() {
         float ms; (void)hipEventElapsedTime(&ms, e0, e1);
         unsigned long long st[64];
         (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_sel_stamps), sizeof(st));
-        printf("rep %d: %.2f us | energy %llu, hist %llu, gather %llu, rank %llu, radix-total %llu, count+scan %llu, write %llu (s_memtime ticks)\n", rep, ms * 1e3,
-               st[1] - st[0], st[5] - st[1], st[6] - st[5], st[7] - st[6], st[2] - st[1], st[3] - st[2], st[4] - st[3]);
+        printf("rep %d: %.2f us | load+energy %llu, or/and %llu, hist %llu, gather %llu, rank %llu, radix-total %llu, scan %llu, write %llu (s_memtime ticks)\n", rep, ms * 1e3,
+               st[8] - st[0], st[1] - st[8], st[5] - st[1], st[6] - st[5], st[7] - st[6], st[2] - st[1], st[3] - st[2], st[4] - st[3]);
     }
     return 0;
 }
