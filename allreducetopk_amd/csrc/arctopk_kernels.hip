@@ -1123,19 +1123,30 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     __shared__ uint32_t h[1 << W2];
     __shared__ uint32_t roff[kMMaxRanges], rcnt[kMMaxRanges];  // later: per-range (eq, gt) counts
     __shared__ uint32_t lds[NW], s_digit, s_acc;
-    const int tid = threadIdx.x;
+    constexpr int RB = 16;  // ranges per wave whose first candidates load up front
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const MItem it = b.it[t];
+    const uint32_t* src = ckey + it.cand_off;
+    // one round trip for everything independent: the state, the per-range counts, and the
+    // first 64 candidate slots of each range this wave copies (a range's region is fixed;
+    // its count only masks them)
     MState s = ws->st[t];
     const int nr = it.nranges;
     const uint32_t gt_above = tid < nr ? ws->cnt_gt[t][tid] : 0u;  // keys above the bin
     const uint32_t my_cnt = tid < nr ? ws->cnt_cand[t][tid] : 0u;
+    uint32_t v[RB];
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+        const int r = wave + q * NW;
+        const int64_t cap = r < nr ? min<int64_t>(64, it.n - (int64_t)r * it.range) : 0;  // region bound
+        v[q] = lane < cap ? src[(int64_t)r * it.range + lane] : 0u;
+    }
     uint32_t nc32;
     const uint32_t my_off = blk_exscan_u32<NW>(my_cnt, lds, &nc32);
     roff[tid] = my_off;
     rcnt[tid] = my_cnt;
     __syncthreads();
     const int64_t nc = nc32;
-    const uint32_t* src = ckey + it.cand_off;
     // global index of candidate p (p-th in range order): range = last r with roff[r] <= p
     auto gidx = [&](uint32_t p) -> int64_t {
         int lo = 0, hi = nr - 1;
@@ -1147,18 +1158,17 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
         return (int64_t)lo * it.range + (p - roff[lo]);
     };
     const bool staged = nc <= kRefineLdsCap;
-    const int lane = tid & 63, wave = tid >> 6;
     if (staged) {
-        // usual case, one round trip: wave w copies ranges w, w + NW, ..., lane j candidate j
-        // of each (a range's first 64 in one load, every range's load in flight before the
-        // stores; longer ranges loop), then everything is read from LDS
-        constexpr int RB = 16;
+        // usual case: wave w copies ranges w, w + NW, ..., lane j candidate j of each (the
+        // first RB ranges' first 64 candidates are already in registers; longer ranges and
+        // ranges past NW * RB load here), then everything is read from LDS
         for (int r0 = wave; r0 < nr; r0 += NW * RB) {
-            uint32_t v[RB];
+            if (r0 != wave) {
 #pragma unroll
-            for (int q = 0; q < RB; ++q) {
-                const int r = r0 + q * NW;
-                v[q] = (r < nr && (uint32_t)lane < rcnt[r]) ? src[(int64_t)r * it.range + lane] : 0u;
+                for (int q = 0; q < RB; ++q) {
+                    const int r = r0 + q * NW;
+                    v[q] = (r < nr && (uint32_t)lane < rcnt[r]) ? src[(int64_t)r * it.range + lane] : 0u;
+                }
             }
 #pragma unroll
             for (int q = 0; q < RB; ++q) {
@@ -1263,8 +1273,14 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(MBatch b, MWorksp
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-    if ((int)blockIdx.x < b.cnt)
+    if ((int)blockIdx.x < b.cnt) {
+#ifdef ARCTOPK_DIAG_REFINE_TWICE  // diagnostic builds only: the second pass runs warm
         arc_refine_item(b, (int)blockIdx.x, ws, ckey, dyn);
+        __syncthreads();
+        DIAG_STAMP(g_st_refine, 5);
+#endif
+        arc_refine_item(b, (int)blockIdx.x, ws, ckey, dyn);
+    }
     else
         select_small_seg<T, kRefineThreads>(segs, small_ids[blockIdx.x - b.cnt], sketch, R, sc, rowlist,
                                             slotmap, dyn);
@@ -1418,6 +1434,11 @@ __device__ __forceinline__ float4 pack4(const T* __restrict__ G, T* __restrict__
     return v;
 }
 
+#ifndef ARCTOPK_PACK_FULL_QUADS
+#define ARCTOPK_PACK_FULL_QUADS 1  // tuning switch (A/B builds): 0 = rewrite only quads with a selected row
+#endif
+constexpr bool kPackFullQuads = ARCTOPK_PACK_FULL_QUADS != 0;
+
 // Pack of a row range of an m in {1, 2} fp32 segment (Chunk mode 1): lane per 16-B quad of
 // the segment (4 / 2 rows), slot map read alongside; selected rows go to packed[slot * m],
 // and (EF14 / EF21) the quad of E is rewritten whole when it holds a selected row.
@@ -1485,7 +1506,9 @@ __device__ __forceinline__ void pack_stream_small(const SegDev& s, const Chunk& 
                 }
             }
             if constexpr (EF != ARCTOPK_EF_NONE) {
-                if (any) {
+                // every quad rewritten (unchanged values where no row is selected): whole
+                // lines leave L2 instead of masked partial writes (read-modify-write at HBM)
+                if (any || kPackFullQuads) {
                     if (el + 4 <= seg_end) {
                         *reinterpret_cast<float4*>(E + el) = make_float4(en[0], en[1], en[2], en[3]);
                     } else {
@@ -2095,7 +2118,14 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
             return env ? std::max<int64_t>(1, std::atoll(env)) : (int64_t)4096;
         }();
         const dim3 grid(p->n_small + job.n);
-        if (p->small_lds > big_rows * 4 + 16)
+        static_assert(((kSmallSelRows + 3) & ~3) * 4 + 16 <= kRefineLdsCap * 4, "small-select keys fit the LDS cap");
+        if (p->small_lds > 48 * 1024) {  // > 48 KiB of keys: the dynamic LDS attribute
+            static const hipError_t lds_ok = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&k_select_small<T, 1024>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, kRefineLdsCap * 4);
+            if (lds_ok != hipSuccess) return (int)lds_ok;
+        }
+        if (p->small_lds > big_rows * 4 + 16 || p->small_lds > 48 * 1024)
             hipLaunchKernelGGL((k_select_small<T, 1024>), grid, dim3(1024), (size_t)p->small_lds,
                                st, p->d_segs, p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap, job);
         else

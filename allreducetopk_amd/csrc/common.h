@@ -33,7 +33,14 @@ constexpr int kChunkElems = 8192;  // target elements per pack/decode work chunk
                                    // 16384 by 3 % on the headline, one 2048-row per wave)
 constexpr int kEncTargetBlocks = 2048;  // encode blocks a bucket's wave-per-row work aims at
                                         // (measured: 2048 beats 1024 on 256 CUs at 3 blocks/CU)
-constexpr int kSmallSelRows = 15360;  // rows up to this: keys in LDS (60 KiB + statics < 64 KiB)
+#ifndef ARCTOPK_SMALL_SEL_ROWS
+#define ARCTOPK_SMALL_SEL_ROWS 15360
+#endif
+// rows up to this: one block per segment, keys in LDS (at most 32752: the refine launch
+// that also runs these selects has 128 KiB of dynamic LDS; past 48 KiB the 1024-thread
+// select kernel gets the attribute).  Measured: a 32000-row segment takes 54 us in one
+// block vs 33 us multi-block, so the single block stops at 15360 rows.
+constexpr int kSmallSelRows = ARCTOPK_SMALL_SEL_ROWS;
 
 // 32-bit quotient by a runtime divisor: q = mulhi64(x, ceil(2^64/d)) is exact for
 // x, d < 2^32 (the fractional error x/2^64 < 1/d never crosses an integer).

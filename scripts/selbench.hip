@@ -149,6 +149,7 @@ int main(int argc, char** argv) {
                 for (size_t b = 0; b < 64; ++b) {
                     const unsigned long long* e = &st[2][b * 8];
                     if (!e[2] || e[2] < e[0]) break;
+                    if (e[5] > e[0] && e[5] < e[1]) printf("\n    item %2zu: first pass %.2f, second pass %.2f", b, (e[5] - e[0]) * 0.01, (e[1] - e[5]) * 0.01);
                     printf("\n    item %2zu: stage %.2f rounds %.2f count %.2f offsets %.2f (start %.2f)", b,
                            (e[2] - e[0]) * 0.01, (e[3] - e[2]) * 0.01, (e[4] - e[3]) * 0.01, (e[1] - e[4]) * 0.01,
                            (e[0] - t0) * 0.01);
