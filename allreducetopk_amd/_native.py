@@ -53,6 +53,9 @@ _SIGS = {
     "arctopk_select": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "arctopk_select_draw": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                       c_uint64, c_void_p, c_void_p]),
+    "arctopk_plan_bind": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "arctopk_step": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                               c_uint64, c_void_p, c_uint64, c_void_p]),
     "arctopk_row_energy": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                c_void_p]),

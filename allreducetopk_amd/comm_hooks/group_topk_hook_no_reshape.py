@@ -138,6 +138,10 @@ class BucketPlan:
         adv = N.c_uint64()
         N.check(L.arctopk_plan_philox_advance(handle, N.ctypes.byref(adv)), "arctopk_plan_philox_advance")
         self.philox_advance = int(adv.value)
+        # the buffers arctopk_step (one native call per world-size-1 step) works on
+        N.check(L.arctopk_plan_bind(handle, self.sketch.data_ptr(), self.rowlist.data_ptr(),
+                                    self.slotmap.data_ptr(), self.packed.data_ptr(),
+                                    self.V_ring[0].data_ptr()), "arctopk_plan_bind")
         bits = dtype_bits(dtype)
         # bits_sum of one call: sketch P + selected values per tensor (:32, :57, :70, :119)
         self.bits_sum = sum(((s.n if s.kind == N.SEG_RAW else s.n * r) + s.k_rows * s.m) * bits
@@ -328,8 +332,11 @@ class GroupTopKState(HookState):
         self.error_dict: Dict[int, torch.Tensor] = {}
         self.global_error_dict: Dict[int, torch.Tensor] = {}
         self.error_decay = error_decay
-        self.rng = torch.Generator()
-        self.rng.manual_seed(seed)
+        # the projection-seed generator (reference :165-166) -- see the `rng` property
+        self._rng = torch.Generator()
+        self._rng.manual_seed(seed)
+        self._rng_lag = 0          # seeds handed out but not yet drawn from _rng
+        self._rng_strict = False   # True once _rng was exposed: draw from it every call
         # MI355X codec state (not in the reference)
         self._plans: Dict[int, Tuple[tuple, BucketPlan]] = {}
         self._proj = ProjectionSource(r)
@@ -393,6 +400,48 @@ class GroupTopKState(HookState):
         self.predraw = os.environ.get("ARCTOPK_PREDRAW", "1") != "0"
         self.predraw_hits = 0
         self._order_pos: Dict[int, int] = {}
+
+    @property
+    def rng(self) -> torch.Generator:
+        """The projection-seed generator (reference :165-166, drawn once per compressed call
+        at :254).  The hook takes its seeds from a batched look-ahead clone and draws the
+        same values from this generator lazily: any access here first brings it to the exact
+        position, and from then on every call draws from it directly (the caller may keep
+        the reference and reseed it)."""
+        self._sync_rng()
+        self._rng_strict = True
+        return self._rng
+
+    @rng.setter
+    def rng(self, g: torch.Generator) -> None:
+        self._rng = g
+        self._rng_lag = 0
+        self._rng_strict = True
+        self._proj.reset()
+
+    def _sync_rng(self) -> None:
+        if self._rng_lag:  # one randint of n = n randints of 1, in order
+            torch.randint(0, 1_000_000_000, (self._rng_lag,), generator=self._rng)
+            self._rng_lag = 0
+
+    def _checkpoint_rng(self) -> torch.Generator:
+        """The generator at its exact position, for state_dict / load_state_dict (which
+        do not expose it to the caller)."""
+        self._sync_rng()
+        return self._rng
+
+    def _next_seed(self) -> int:
+        """This call's projection seed: the next value of rng's randint(0, 1e9) sequence."""
+        p = self._proj
+        if self._rng_strict:
+            return p.consume_seed(self._rng)
+        if p._lookahead is None:
+            self._sync_rng()
+            p._sync_lookahead(self._rng)
+        seed = p._peek_seeds(1)[0]
+        p._future_seeds.popleft()
+        self._rng_lag += 1
+        return seed
 
     def init_sketch_comm(self) -> None:
         """Create the sketch communicator now (a collective over every rank of the default
@@ -550,6 +599,35 @@ def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
         _prestage_next(state, bucket, dtype, dev)
         _ht("prestage_next")
     return vslot, V
+
+
+def _claim_projections(state, plan, seed: int, stream) -> bool:
+    """Device projections of this call: True when V must be drawn now, False when the
+    previous call's select launch already drew it for this seed (or there is no V).
+    Orders `stream` after V_ring[0]'s last user when that ran on another stream."""
+    if not plan.info.v_len:
+        return False
+    if plan.v_stream is not None and plan.v_stream != stream:
+        stream.wait_stream(plan.v_stream)  # V_ring[0]'s last writer / reader ran there
+    plan.v_stream = stream
+    pre, plan.v_drawn = plan.v_drawn, None
+    if pre == seed:
+        state.predraw_hits += 1
+        return False
+    return True
+
+
+def _predraw_target(state, b: int, dtype, dev, stream):
+    """(plan, seed) whose projections this call's select launch draws in advance: the
+    predicted next bucket's plan and the rng's next seed, or (None, 0)."""
+    if not state.predraw:
+        return None, 0
+    nplan = state._next_plan(b)
+    if (nplan is None or not nplan.info.v_len or nplan.dtype != dtype or nplan.device != dev
+            or (nplan.v_stream is not None and nplan.v_stream != stream)):
+        return None, 0
+    nseed = state._proj.peek_next_seed()
+    return (nplan, nseed) if nseed is not None else (None, 0)
 
 
 _RESEED_FAST = None
@@ -725,7 +803,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     # per-call projection seed, and the reference's global reseed side effect (:254-255)
     _ht()
     device_v = state.projections == "device"
-    seed = state._proj.consume_seed(state.rng)  # (:254), with a look-ahead of the sequence
+    seed = state._next_seed()  # (:254), from a batched look-ahead of the sequence
     plan = state._plan_for(bucket)
     dev = input_tensor.device
     _reseed_global(seed, dev.index or 0, plan.philox_advance)
@@ -765,17 +843,29 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                 e.record(s_)
             evs[name] = e
 
+    if device_v and world_size == 1 and evs is None and not state.host_staged:
+        # world size 1, no phase markers: the whole step in one native call (arctopk_step:
+        # [draw] -> encode -> select + the next call's projections -> pack -> decode)
+        draw = _claim_projections(state, plan, seed, stream)
+        nplan, nseed = _predraw_target(state, b, dtype, dev, stream)
+        N.check(N.lib().arctopk_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
+                                     int(err_in), int(draw), seed,
+                                     nplan.handle if nplan is not None else None, nseed, sid),
+                "arctopk_step")
+        if nplan is not None:
+            nplan.v_drawn, nplan.v_stream = nseed, stream
+        _ht("step")
+        state.maybe_increase_iter(bucket)
+        fut = torch.futures.Future()
+        fut.set_result(input_tensor)
+        _ht("tail")
+        return fut
+
     mark("start")
-    if device_v and plan.info.v_len:
-        if plan.v_stream is not None and plan.v_stream != stream:
-            stream.wait_stream(plan.v_stream)  # V_ring[0]'s last writer / reader ran there
-        plan.v_stream = stream
-        pre, plan.v_drawn = plan.v_drawn, None
-        if pre == seed:  # drawn by the previous call's select launch
-            state.predraw_hits += 1
-        else:  # V on this stream, right before the encode that reads it
-            N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid),
-                    "arctopk_draw_projections")
+    if device_v and _claim_projections(state, plan, seed, stream):
+        # V on this stream, right before the encode that reads it
+        N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid),
+                "arctopk_draw_projections")
         _ht("draw_v")
     mark("draw")
     _ht("events")
@@ -791,15 +881,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         sk_group = state._sketch_group(group) if overlap else group
         dist.all_reduce(plan.sketch_view, group=sk_group, async_op=False)
     mark("sketch_allreduce")
-    nplan = nseed = None
-    if device_v and state.predraw:
-        nplan = state._next_plan(b)
-        if (nplan is not None and nplan.info.v_len and nplan.dtype == dtype and nplan.device == dev
-                and (nplan.v_stream is None or nplan.v_stream == stream)):
-            nseed = state._proj.peek_next_seed()
-        if nseed is None:
-            nplan = None
-    plan.select(world_size, sid, nplan, nseed or 0)
+    nplan, nseed = _predraw_target(state, b, dtype, dev, stream) if device_v else (None, 0)
+    plan.select(world_size, sid, nplan, nseed)
     if nplan is not None:
         nplan.v_drawn, nplan.v_stream = nseed, stream
     mark("select")

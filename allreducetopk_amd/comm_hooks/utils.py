@@ -94,7 +94,7 @@ class HookState:
         ``torch.load(..., weights_only=True)``.
         """
         out = {k: getattr(self, k) for k in self._CKPT_SCALARS}
-        rng = getattr(self, "rng", None)
+        rng = self._checkpoint_rng() if hasattr(self, "_checkpoint_rng") else getattr(self, "rng", None)
         if rng is not None:
             out["rng_state"] = rng.get_state()
         for name in ("error_dict", "global_error_dict"):
@@ -109,9 +109,10 @@ class HookState:
             if k in sd:
                 setattr(self, k, sd[k])
         if "rng_state" in sd:
-            if getattr(self, "rng", None) is None:
+            rng = self._checkpoint_rng() if hasattr(self, "_checkpoint_rng") else getattr(self, "rng", None)
+            if rng is None:
                 raise KeyError("checkpoint holds an rng state but this hook state has no rng")
-            self.rng.set_state(sd["rng_state"])
+            rng.set_state(sd["rng_state"])
         for name in ("error_dict", "global_error_dict"):
             if name in sd:
                 setattr(self, name, {int(b): (t.to(device) if device is not None else t).clone()

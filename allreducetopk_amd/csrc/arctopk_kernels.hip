@@ -1259,7 +1259,7 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
 // overlap instead of running back to back.  Trailing blocks may draw the next call's
 // projections (VDrawJob).
 template <typename T>
-__global__ void __launch_bounds__(kRefineThreads) k_arc_refine(MBatch b, MWorkspace* ws,
+__global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __restrict__ bp, MWorkspace* ws,
                                                                const uint32_t* __restrict__ ckey,
                                                                const SegDev* __restrict__ segs,
                                                                const int32_t* __restrict__ small_ids,
@@ -1273,6 +1273,7 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(MBatch b, MWorksp
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    const MBatch& b = *bp;
     if ((int)blockIdx.x < b.cnt) {
 #ifdef ARCTOPK_DIAG_REFINE_TWICE  // diagnostic builds only: the second pass runs warm
         arc_refine_item(b, (int)blockIdx.x, ws, ckey, dyn);
@@ -2172,7 +2173,7 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
 #if ARCTOPK_DIAG_STOP == 1 || ARCTOPK_DIAG_KEYS >= 1  // diagnostic builds only
         continue;
 #endif
-        int e = ms_arc_compact(b, p->d_keys, p->d_mws, p->mws_cap, st);
+        int e = ms_arc_compact(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, st);
         if (e) return e;
         static const hipError_t lds_ok = hipFuncSetAttribute(
             reinterpret_cast<const void*>(&k_arc_refine<T>), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2183,12 +2184,12 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         if (bi != 0) bj.n = 0;
         uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
         hipLaunchKernelGGL(k_arc_refine<T>, dim3(b.cnt + nsm + bj.n), dim3(kRefineThreads),
-                           (size_t)kRefineLdsCap * 4, st, b, p->d_mws, ckey, p->d_segs,
+                           (size_t)kRefineLdsCap * 4, st, p->d_large_batches + bi, p->d_mws, ckey, p->d_segs,
                            p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap, bj);
         if (bi == 0) *drawn = true;
         e = (int)hipGetLastError();
         if (e) return e;
-        e = ms_arc_write(b, p->d_keys, p->d_mws, p->mws_cap, rowlist, slotmap, st);
+        e = ms_arc_write(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, rowlist, slotmap, st);
         if (e) return e;
     }
     return (int)hipGetLastError();

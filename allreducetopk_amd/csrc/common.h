@@ -301,7 +301,9 @@ struct arctopk_plan {
     int small_lds;                // bytes of LDS keys for the largest small segment
     int32_t* d_large;             // segments whose keys go through global memory
     int n_large;
-    arctopk::MBatch* h_large_batches;   // multi-block select items (host, by value at launch)
+    arctopk::MBatch* h_large_batches;   // multi-block select items (host)
+    arctopk::MBatch* d_large_batches;   // ... and their device copy (ARC kernels read it there:
+                                        // a 3 KiB by-value kernel argument costs ~2 us per launch)
     int n_large_batches;
     arctopk::MWorkspace* d_mws;         // multi-block select workspace
     int64_t mws_cap;                    // its candidate slots
@@ -311,4 +313,9 @@ struct arctopk_plan {
     uint64_t vdraw_advance;             // Philox offset after the bucket's draws
     arctopk::VChunk* d_vchunk;          // the draws cut into kVChunk-element blocks
     int n_vchunk;
+    void* b_sketch;                     // buffers bound by arctopk_plan_bind (arctopk_step)
+    int32_t* b_rowlist;
+    int32_t* b_slotmap;
+    void* b_packed;
+    void* b_V;
 };

@@ -203,9 +203,10 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
 // the single-block selects of the small segments share that launch), then ms_arc_write
 // (ascending row list and slot map).  ARC candidate regions: range r of item t owns
 // ckey[cand_off + r * range, + range) (cand_cap = n).
-int ms_arc_compact(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+// (b: the host copy for grid geometry; d_b: the same batch in device memory, read by the kernels)
+int ms_arc_compact(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
                    hipStream_t st);
-int ms_arc_write(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+int ms_arc_write(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
                  int32_t* out_idx, int32_t* out_slot, hipStream_t st);
 // candidate keys the ARC refine stages in LDS (more are read from their ranges' regions)
 constexpr int kRefineLdsCap = 32768;

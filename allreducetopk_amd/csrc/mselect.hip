@@ -248,8 +248,10 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
 // ARC: one block per range, no atomics: the keys above the first-pass bin are counted and
 // the bin's keys are copied (in index order) into the range's own candidate region;
 // cnt_gt / cnt_cand per range for the refine.
-__global__ void __launch_bounds__(256) k_arc_compact(MBatch b, const uint32_t* __restrict__ keys,
-                                                     MWorkspace* ws, uint32_t* __restrict__ ckey) {
+__global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ bp,
+                                                     const uint32_t* __restrict__ keys, MWorkspace* ws,
+                                                     uint32_t* __restrict__ ckey) {
+    const MBatch& b = *bp;
     __shared__ uint32_t lds[4], s_cnt[4];
     DIAG_STAMP(g_st_compact, 0);
     int t, r;
@@ -401,11 +403,32 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
 // ballot compaction in index order.  ARC: rows[out_off + slot] = i and the slot map for
 // every key; TopK: idx[out_off + slot] = i, vals[out_off + slot] = x[key_off + i].
 template <bool FROM_FLOAT, bool ARC>
+__device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
+                                              const float* __restrict__ x, MWorkspace* ws,
+                                              int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                              int32_t* __restrict__ out_slot);
+
+template <bool FROM_FLOAT, bool ARC>
 __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __restrict__ keys,
                                                   const float* __restrict__ x, MWorkspace* ws,
                                                   int32_t* __restrict__ out_idx,
                                                   float* __restrict__ out_val,
                                                   int32_t* __restrict__ out_slot) {
+    ms_write_body<FROM_FLOAT, ARC>(b, keys, x, ws, out_idx, out_val, out_slot);
+}
+
+// ARC: the batch from device memory (plan-resident)
+__global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp, const uint32_t* __restrict__ keys,
+                                                   MWorkspace* ws, int32_t* __restrict__ out_idx,
+                                                   int32_t* __restrict__ out_slot) {
+    ms_write_body<false, true>(*bp, keys, nullptr, ws, out_idx, nullptr, out_slot);
+}
+
+template <bool FROM_FLOAT, bool ARC>
+__device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
+                                              const float* __restrict__ x, MWorkspace* ws,
+                                              int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                              int32_t* __restrict__ out_slot) {
     __shared__ uint32_t s_eq[4], s_gt[4];
     DIAG_STAMP(g_st_write, 0);
     int t, r;
@@ -550,23 +573,22 @@ static int arc_batch_check(const MBatch& b, int64_t cap_total, int* gr) {
     return 0;
 }
 
-int ms_arc_compact(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+int ms_arc_compact(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
                    hipStream_t st) {
     if (b.cnt < 1) return 0;
     int gr;
     if (int e = arc_batch_check(b, cap_total, &gr)) return e;
     uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
-    hipLaunchKernelGGL(k_arc_compact, dim3(total_ranges(b)), dim3(256), 0, st, b, keys, ws, ckey);
+    hipLaunchKernelGGL(k_arc_compact, dim3(total_ranges(b)), dim3(256), 0, st, d_b, keys, ws, ckey);
     return (int)hipGetLastError();
 }
 
-int ms_arc_write(const MBatch& b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
+int ms_arc_write(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
                  int32_t* out_idx, int32_t* out_slot, hipStream_t st) {
     if (b.cnt < 1) return 0;
     int gr;
     if (int e = arc_batch_check(b, cap_total, &gr)) return e;
-    hipLaunchKernelGGL((k_ms_write<false, true>), dim3(total_ranges(b)), dim3(256), 0, st, b, keys, nullptr, ws,
-                       out_idx, nullptr, out_slot);
+    hipLaunchKernelGGL(k_arc_write, dim3(total_ranges(b)), dim3(256), 0, st, d_b, keys, ws, out_idx, out_slot);
     return (int)hipGetLastError();
 }
 

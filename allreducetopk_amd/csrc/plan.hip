@@ -295,6 +295,11 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             }
             p->mws_cap = std::max(p->mws_cap, cap);
         }
+        e = hipMalloc((void**)&p->d_large_batches, sizeof(MBatch) * (size_t)p->n_large_batches);
+        if (e == hipSuccess)
+            e = hipMemcpy(p->d_large_batches, p->h_large_batches, sizeof(MBatch) * (size_t)p->n_large_batches,
+                          hipMemcpyHostToDevice);
+        if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
         e = hipMalloc((void**)&p->d_mws, (size_t)ms_workspace_bytes(p->mws_cap));
         if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
         // arrival counters start at zero (each select kernel leaves them zero)
@@ -356,6 +361,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     delete[] p->h_segs;
     delete[] p->h_pack_begin;
     delete[] p->h_large_batches;
+    if (p->d_large_batches) (void)hipFree(p->d_large_batches);
     if (p->d_mws) (void)hipFree(p->d_mws);
     if (p->d_vdraw) (void)hipFree(p->d_vdraw);
     if (p->d_vchunk) (void)hipFree(p->d_vchunk);

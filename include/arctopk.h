@@ -141,6 +141,20 @@ int arctopk_select_draw(const arctopk_plan* plan, const void* sketch, int32_t wo
                         uint64_t next_seed, void* next_V, void* stream);
 
 /*
+ * One-call step at world size 1, where both all-reduces of the hook are identities
+ * (group_topk_hook_no_reshape.py:264, :280): [draw V for `seed` when draw != 0] -> encode
+ * -> select (+ the next call's projections: next / next_seed, as arctopk_select_draw) ->
+ * pack -> decode into `bucket`, on the buffers bound to the plan by arctopk_plan_bind (the
+ * sketch, row list, slot map, packed values and projection buffer the phase entry points
+ * take as arguments).  One foreign-function call per hook call instead of one per phase.
+ */
+int arctopk_plan_bind(arctopk_plan* plan, void* sketch, int32_t* rowlist, int32_t* slotmap,
+                      void* packed, void* V);
+int arctopk_step(const arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
+                 int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
+                 uint64_t next_seed, void* stream);
+
+/*
  * K2 variant for tests/bit-exact checks: the per-row energy keys only
  * (float bits of the energy the reference feeds torch.topk), keys[row_off + row].
  */

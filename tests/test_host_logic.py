@@ -304,3 +304,27 @@ def test_bf16_projection_draw_matches_reference_stream(seed):
         ms = [s.m for s in segs if s.kind == A.SKETCH]
         got = draw_host(seed, ms, 4, torch.bfloat16, pin=False)
         assert torch.equal(got[:ref.numel()], ref)
+
+
+def test_state_rng_is_lazy_but_exact():
+    """GroupTopKState hands out seeds from a batched look-ahead and draws them from
+    state.rng lazily: every observation of the generator (the attribute, state_dict) sees
+    exactly one draw per call, as the reference's randint at :254 leaves it, and a caller
+    who reseeds the exposed generator gets that sequence from the next call on."""
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import GroupTopKState
+    st = GroupTopKState(None, seed=5)
+    ref = torch.Generator().manual_seed(5)
+
+    def ref_seed():
+        return int(torch.randint(0, 1_000_000_000, (1,), generator=ref).item())
+    assert [st._next_seed() for _ in range(40)] == [ref_seed() for _ in range(40)]
+    assert torch.equal(st.state_dict()["rng_state"], ref.get_state())
+    assert not st._rng_strict  # checkpointing does not expose the generator
+    g = st.rng
+    assert torch.equal(g.get_state(), ref.get_state())
+    g.manual_seed(9)
+    ref.manual_seed(9)
+    assert [st._next_seed() for _ in range(5)] == [ref_seed() for _ in range(5)]
+    st2 = GroupTopKState(None, seed=1)
+    st2.load_state_dict(st.state_dict())
+    assert [st2._next_seed() for _ in range(3)] == [ref_seed() for _ in range(3)]
