@@ -484,8 +484,11 @@ class GroupTopKState(HookState):
         # prefetched projections were keyed on seeds of the old rng position
         self._proj.reset()
 
-    def _plan_for(self, bucket) -> BucketPlan:
-        buf = bucket.buffer()
+    def _plan_for(self, bucket, buf=None) -> BucketPlan:
+        if buf is None:
+            buf = bucket.buffer()
+        if _LIB[0] is None:
+            _LIB[0] = N.lib()
         if self._first_compressed_iter is None:
             self._first_compressed_iter = self.iter
         # fast path: the bucket's flat buffer is the one this plan was built for (DDP keeps a
@@ -601,15 +604,16 @@ def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
     return vslot, V
 
 
-def _claim_projections(state, plan, seed: int, stream) -> bool:
+def _claim_projections(state, plan, seed: int, sid: int, dev) -> bool:
     """Device projections of this call: True when V must be drawn now, False when the
     previous call's select launch already drew it for this seed (or there is no V).
-    Orders `stream` after V_ring[0]'s last user when that ran on another stream."""
+    Orders the caller's stream (raw handle `sid`) after V_ring[0]'s last user when that
+    ran on another stream."""
     if not plan.info.v_len:
         return False
-    if plan.v_stream is not None and plan.v_stream != stream:
-        stream.wait_stream(plan.v_stream)  # V_ring[0]'s last writer / reader ran there
-    plan.v_stream = stream
+    if plan.v_stream is not None and plan.v_stream != sid:  # V_ring[0]'s last user ran there
+        torch.cuda.current_stream(dev).wait_stream(torch.cuda.ExternalStream(plan.v_stream, device=dev))
+    plan.v_stream = sid
     pre, plan.v_drawn = plan.v_drawn, None
     if pre == seed:
         state.predraw_hits += 1
@@ -617,20 +621,26 @@ def _claim_projections(state, plan, seed: int, stream) -> bool:
     return True
 
 
-def _predraw_target(state, b: int, dtype, dev, stream):
+def _predraw_target(state, b: int, dtype, dev, sid: int):
     """(plan, seed) whose projections this call's select launch draws in advance: the
     predicted next bucket's plan and the rng's next seed, or (None, 0)."""
     if not state.predraw:
         return None, 0
     nplan = state._next_plan(b)
     if (nplan is None or not nplan.info.v_len or nplan.dtype != dtype or nplan.device != dev
-            or (nplan.v_stream is not None and nplan.v_stream != stream)):
+            or (nplan.v_stream is not None and nplan.v_stream != sid)):
         return None, 0
     nseed = state._proj.peek_next_seed()
     return (nplan, nseed) if nseed is not None else (None, 0)
 
 
 _RESEED_FAST = None
+_LIB = [None]
+
+
+def _current_raw_stream(device_index: int) -> int:
+    """The caller's current HIP stream on the device, as a raw handle (no Stream object)."""
+    return torch._C._cuda_getCurrentRawStream(device_index)
 
 # optional host-time breakdown of the hook (diagnostics; ARCTOPK_HOST_TIMING=1)
 # Priority of the projection copy stream.  HIP maps a process's streams onto a few HW
@@ -804,18 +814,38 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     _ht()
     device_v = state.projections == "device"
     seed = state._next_seed()  # (:254), from a batched look-ahead of the sequence
-    plan = state._plan_for(bucket)
+    plan = state._plan_for(bucket, input_tensor)
     dev = input_tensor.device
-    _reseed_global(seed, dev.index or 0, plan.philox_advance)
+    dix = dev.index or 0
+    _reseed_global(seed, dix, plan.philox_advance)
     _ht("seed+plan")
 
-    stream = torch.cuda.current_stream(dev)
-    sid = stream.cuda_stream
+    sid = _current_raw_stream(dix)
+    dtype = input_tensor.dtype
     pend = state._pending.pop(b, None)
     if pend is not None:  # this bucket's previous decode (side stream) must be done
-        stream.wait_event(pend)
-    dtype = input_tensor.dtype
+        torch.cuda.current_stream(dev).wait_event(pend)
     _ht("plan+pending")
+    if device_v and world_size == 1 and not state.host_staged and not (
+            state.phase_events is not None or state.hook_events is not None):
+        # world size 1, no phase markers: the whole step in one native call (arctopk_step:
+        # [draw] -> encode -> select + the next call's projections -> pack -> decode)
+        draw = _claim_projections(state, plan, seed, sid, dev)
+        nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
+        N.check(_LIB[0].arctopk_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
+                                     int(err_in), int(draw), seed,
+                                     nplan.handle if nplan is not None else None, nseed, sid),
+                "arctopk_step")
+        if nplan is not None:
+            nplan.v_drawn, nplan.v_stream = nseed, sid
+        _ht("step")
+        state.maybe_increase_iter(bucket)
+        fut = torch.futures.Future()
+        fut.set_result(input_tensor)
+        _ht("tail")
+        return fut
+
+    stream = torch.cuda.current_stream(dev)
     vslot, V = -1, plan.V_ring[0]
     if not device_v:
         vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, stream)
@@ -843,26 +873,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                 e.record(s_)
             evs[name] = e
 
-    if device_v and world_size == 1 and evs is None and not state.host_staged:
-        # world size 1, no phase markers: the whole step in one native call (arctopk_step:
-        # [draw] -> encode -> select + the next call's projections -> pack -> decode)
-        draw = _claim_projections(state, plan, seed, stream)
-        nplan, nseed = _predraw_target(state, b, dtype, dev, stream)
-        N.check(N.lib().arctopk_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
-                                     int(err_in), int(draw), seed,
-                                     nplan.handle if nplan is not None else None, nseed, sid),
-                "arctopk_step")
-        if nplan is not None:
-            nplan.v_drawn, nplan.v_stream = nseed, stream
-        _ht("step")
-        state.maybe_increase_iter(bucket)
-        fut = torch.futures.Future()
-        fut.set_result(input_tensor)
-        _ht("tail")
-        return fut
-
     mark("start")
-    if device_v and _claim_projections(state, plan, seed, stream):
+    if device_v and _claim_projections(state, plan, seed, sid, dev):
         # V on this stream, right before the encode that reads it
         N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid),
                 "arctopk_draw_projections")
@@ -881,10 +893,10 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         sk_group = state._sketch_group(group) if overlap else group
         dist.all_reduce(plan.sketch_view, group=sk_group, async_op=False)
     mark("sketch_allreduce")
-    nplan, nseed = _predraw_target(state, b, dtype, dev, stream) if device_v else (None, 0)
+    nplan, nseed = _predraw_target(state, b, dtype, dev, sid) if device_v else (None, 0)
     plan.select(world_size, sid, nplan, nseed)
     if nplan is not None:
-        nplan.v_drawn, nplan.v_stream = nseed, stream
+        nplan.v_drawn, nplan.v_stream = nseed, sid
     mark("select")
     _ht("select")
     state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum

@@ -318,4 +318,6 @@ struct arctopk_plan {
     int32_t* b_slotmap;
     void* b_packed;
     void* b_V;
+    void* step_cache;                   // arctopk_step's instantiated graphs (arctopk_kernels.hip)
 };
+namespace arctopk { void step_cache_free(void* cache); }

@@ -360,6 +360,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_part) (void)hipFree(p->d_part);
     delete[] p->h_segs;
     delete[] p->h_pack_begin;
+    if (p->step_cache) arctopk::step_cache_free(p->step_cache);
     delete[] p->h_large_batches;
     if (p->d_large_batches) (void)hipFree(p->d_large_batches);
     if (p->d_mws) (void)hipFree(p->d_mws);

@@ -20,18 +20,4 @@ extern "C" int arctopk_plan_bind(arctopk_plan* p, void* sketch, int32_t* rowlist
     return 0;
 }
 
-extern "C" int arctopk_step(const arctopk_plan* p, void* bucket, void* err, void* gerr, int32_t ef,
-                            int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
-                            uint64_t next_seed, void* stream) {
-    if (!p || !bucket || !p->b_sketch) return ARCTOPK_EINVAL;  // unbound plan
-    if (next && !next->b_sketch) return ARCTOPK_EINVAL;
-    int e = 0;
-    if (draw && p->info.v_len > 0) e = arctopk_draw_projections(p, seed, p->b_V, stream);
-    if (!e) e = arctopk_encode(p, bucket, err, ef, err_in, p->b_V, p->b_sketch, stream);
-    if (!e)
-        e = arctopk_select_draw(p, p->b_sketch, 1, p->b_rowlist, p->b_slotmap, next, next_seed,
-                                next ? next->b_V : nullptr, stream);
-    if (!e) e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
-    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, 1, ef, gerr, bucket, stream);
-    return e;
-}
+// arctopk_step (the cached-graph step) lives with the kernels it launches (arctopk_kernels.hip).
