@@ -68,17 +68,17 @@ _SIGS = {
     "arctopk_sparse_workspace_bytes": (c_int64, [c_int32, POINTER(c_int64)]),
     "arctopk_topk_select": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
                                       POINTER(c_int64), POINTER(c_int64), c_void_p, c_void_p, c_void_p,
-                                      c_void_p]),
+                                      c_int32, c_void_p]),
     "arctopk_randk_indices": (c_int32, [c_int32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64),
                                         c_uint64, c_void_p, c_void_p]),
     "arctopk_sparse_gather": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
-                                        POINTER(c_int64), c_void_p, c_void_p, c_void_p]),
+                                        POINTER(c_int64), c_void_p, c_void_p, c_int32, c_void_p]),
     "arctopk_sparse_residual": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
-                                          POINTER(c_int64), c_void_p, c_void_p, c_int32, c_void_p]),
+                                          POINTER(c_int64), c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "arctopk_sparse_decode": (c_int32, [c_void_p, c_int64, c_int32, POINTER(c_int64), POINTER(c_int64),
                                         POINTER(c_int64), c_int64, c_void_p, c_void_p, c_int32, c_int32,
-                                        c_int32, c_void_p, c_void_p]),
-    "arctopk_ef_apply": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
+                                        c_int32, c_void_p, c_int32, c_void_p]),
+    "arctopk_ef_apply": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p]),
     "arctopk_draw_bf16_normal": (c_int32, [c_uint64, c_int64, c_void_p]),
     "arctopk_draw_normal": (c_int32, [c_uint64, c_int32, c_int32, POINTER(c_int64), c_void_p]),
     "arctopk_draw_pool_create": (c_int32, [c_int32, POINTER(c_void_p)]),

@@ -123,8 +123,8 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
     if state.sparse_type != "tensor":  # the reference crashes for row/column (:96)
         raise ValueError(f"not enough values to unpack (sparse_type={state.sparse_type!r}: only "
                          "'tensor' is functional in the reference)")
-    if not input_tensor.is_cuda or input_tensor.dtype != torch.float32:
-        raise RuntimeError("sparse HIP codec needs a float32 bucket on a GPU")
+    if not input_tensor.is_cuda or input_tensor.dtype not in N.DTYPE_CODE:
+        raise RuntimeError("sparse HIP codec needs a float32 or bfloat16 bucket on a GPU")
     L = N.lib()
     device = input_tensor.device
     dtype = input_tensor.dtype
@@ -132,6 +132,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
     total = input_tensor.shape[0]
     stream = torch.cuda.current_stream(device).cuda_stream
     ef = N.EF_CODE[state.use_error_feedback]
+    dt = N.DTYPE_CODE[dtype]
 
     if ef == N.EF14:
         err_in = b in state.error_dict
@@ -140,13 +141,13 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
             state.error_dict[b] = torch.zeros(total, device=device, dtype=dtype)
         err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
         N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), err.data_ptr(), total,
-                                   N.EF14, int(err_in), stream), "arctopk_ef_apply")
+                                   N.EF14, int(err_in), dt, stream), "arctopk_ef_apply")
     elif ef == N.EF21:
         if b in state.error_dict:
             err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
             _residual_on(state.global_error_dict, b, input_tensor, "global_error_dict")
             N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), err.data_ptr(),
-                                       total, N.EF21, 1, stream), "arctopk_ef_apply")
+                                       total, N.EF21, 1, dt, stream), "arctopk_ef_apply")
         else:  # (:213-226)
             logger.info("A tensor of length %s that represents local/global error is created.", total)
             state.error_dict[b] = torch.clone(input_tensor).detach()
@@ -193,12 +194,12 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
             N.check(L.arctopk_randk_indices(nt, a_n, a_k, a_ko, int(seed), indices.data_ptr(),
                                             stream), "arctopk_randk_indices")
         N.check(L.arctopk_sparse_gather(x, nt, a_off, a_k, a_ko, indices.data_ptr(),
-                                        values.data_ptr(), stream), "arctopk_sparse_gather")
+                                        values.data_ptr(), dt, stream), "arctopk_sparse_gather")
         bits_sum = sum_k * dtype_bits(dtype)
     else:
         ws_buf = _workspace(state, device, numels)
         N.check(L.arctopk_topk_select(x, nt, a_off, a_n, a_k, a_ko, indices.data_ptr(),
-                                      values.data_ptr(), ws_buf.data_ptr(), stream),
+                                      values.data_ptr(), ws_buf.data_ptr(), dt, stream),
                 "arctopk_topk_select")
         bits_sum = sum_k * (dtype_bits(dtype) + 32)
 
@@ -207,7 +208,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
     state.last_indices, state.last_k = indices, ks
     if ef != N.EF_NONE:  # residual persistence (:257-267)
         N.check(L.arctopk_sparse_residual(state.error_dict[b].data_ptr(), nt, a_off, a_k, a_ko,
-                                          indices.data_ptr(), values.data_ptr(), ef, stream),
+                                          indices.data_ptr(), values.data_ptr(), ef, dt, stream),
                 "arctopk_sparse_residual")
     gerr = state.global_error_dict[b].data_ptr() if ef == N.EF21 else None
 
@@ -216,7 +217,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
         if world_size > 1:
             dist.all_reduce(values, group=group, async_op=False)
         N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, indices.data_ptr(),
-                                        values.data_ptr(), 1, world_size, 0, gerr, stream),
+                                        values.data_ptr(), 1, world_size, 0, gerr, dt, stream),
                 "arctopk_sparse_decode")
     else:
         state.comm_bits_this_round += (world_size - 1) * world_size * bits_sum
@@ -229,7 +230,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
             all_vals, all_idx = values, indices
         N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, all_idx.data_ptr(),
                                         all_vals.data_ptr(), world_size, world_size, 1, gerr,
-                                        stream), "arctopk_sparse_decode")
+                                        dt, stream), "arctopk_sparse_decode")
 
     state.maybe_increase_iter(bucket)
     fut = torch.futures.Future()

@@ -2045,6 +2045,17 @@ __global__ void __launch_bounds__(256) k_ef_apply(float* __restrict__ x, float* 
     }
 }
 
+// bf16 buckets (TopK / RandK): element-wise, x = rnd(x +- E) as the reference's bf16 add_
+template <int EF, bool ERR_IN>
+__global__ void __launch_bounds__(256) k_ef_apply_bf16(bf16_t* __restrict__ x, bf16_t* __restrict__ E,
+                                                       int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float v = ef_apply1<bf16_t, EF, ERR_IN>(x, E, i);
+        if constexpr (EF == ARCTOPK_EF14) st1<bf16_t>(E + i, v);
+        if constexpr (EF != ARCTOPK_EF14 || ERR_IN) st1<bf16_t>(x + i, v);
+    }
+}
+
 // sketch of column-split tensors: the parts' fp32 partial sketches summed in part order,
 // then rounded to T once (the reference's mm accumulates in fp32 and rounds its output)
 template <typename T>
@@ -2376,11 +2387,29 @@ extern "C" int arctopk_decode(const arctopk_plan* p, const void* packed, const i
     return arctopk_decode_segments(p, 0, p->nseg, packed, slotmap, ws, ef, gerr, out, stream);
 }
 
-extern "C" int arctopk_ef_apply(float* x, float* E, int64_t n, int32_t ef, int32_t err_in,
-                                void* stream) {
-    if (!x || n < 0) return ARCTOPK_EINVAL;
+extern "C" int arctopk_ef_apply(void* x_, void* E_, int64_t n, int32_t ef, int32_t err_in,
+                                int32_t dtype, void* stream) {
+    if (!x_ || n < 0) return ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF_NONE || n == 0) return 0;
-    if (!E) return ARCTOPK_EINVAL;
+    if (!E_) return ARCTOPK_EINVAL;
+    if (dtype == ARCTOPK_BF16) {
+        bf16_t* x = static_cast<bf16_t*>(x_);
+        bf16_t* E = static_cast<bf16_t*>(E_);
+        const dim3 g((unsigned)std::min<int64_t>(8192, (n + 255) / 256));
+        hipStream_t st = (hipStream_t)stream;
+        if (ef == ARCTOPK_EF14 && err_in)
+            hipLaunchKernelGGL((k_ef_apply_bf16<ARCTOPK_EF14, true>), g, dim3(256), 0, st, x, E, n);
+        else if (ef == ARCTOPK_EF14)
+            hipLaunchKernelGGL((k_ef_apply_bf16<ARCTOPK_EF14, false>), g, dim3(256), 0, st, x, E, n);
+        else if (ef == ARCTOPK_EF21)
+            hipLaunchKernelGGL((k_ef_apply_bf16<ARCTOPK_EF21, true>), g, dim3(256), 0, st, x, E, n);
+        else
+            return ARCTOPK_EINVAL;
+        return (int)hipGetLastError();
+    }
+    float* x = static_cast<float*>(x_);
+    float* E = static_cast<float*>(E_);
     // float4 path needs 16-B aligned x and E (torch allocations are)
     if (((uintptr_t)x | (uintptr_t)E) & 15) return ARCTOPK_EINVAL;
     const int grid = (int)std::min<int64_t>(8192, (n / 4 + 255) / 256 + 1);

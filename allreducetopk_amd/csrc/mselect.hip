@@ -18,18 +18,28 @@ constexpr int kW2 = 10;  // refinement digit width (12 + 10 + 10 >= 32 key bits)
 constexpr int kPerLane = kMTile / 256;  // keys per lane of a tile (16)
 constexpr int kCandPerBlock = 2048;     // candidates per block of a refinement pass
 
-template <bool FROM_FLOAT>
+// key sources: 0 = uint32 keys (ARC energies), 1 = |x| of fp32 x, 2 = |x| of bf16 x (the bf16
+// bits widened to the fp32 bit pattern of the same value: exact, so the order is bf16's)
+template <int SRC>
 __device__ __forceinline__ uint32_t load_bits(const uint32_t* __restrict__ keys,
-                                              const float* __restrict__ x, int64_t i) {
-    if constexpr (FROM_FLOAT) return __float_as_uint(x[i]);
+                                              const void* __restrict__ x, int64_t i) {
+    if constexpr (SRC == 1) return __float_as_uint(static_cast<const float*>(x)[i]);
+    else if constexpr (SRC == 2) return (uint32_t)static_cast<const uint16_t*>(x)[i] << 16;
     else return keys[i];
 }
 
 // |x| for TopK keys: NaN sorts above inf
-template <bool FROM_FLOAT>
+template <int SRC>
 __device__ __forceinline__ uint32_t key_of(uint32_t bits) {
-    if constexpr (FROM_FLOAT) return bits & 0x7FFFFFFFu;
+    if constexpr (SRC != 0) return bits & 0x7FFFFFFFu;
     else return bits;
+}
+
+// the selected value of x (TopK outputs), in x's own type
+template <int SRC>
+__device__ __forceinline__ void store_val(void* __restrict__ out, int64_t j, uint32_t bits) {
+    if constexpr (SRC == 1) static_cast<float*>(out)[j] = __uint_as_float(bits);
+    else if constexpr (SRC == 2) static_cast<uint16_t*>(out)[j] = (uint16_t)(bits >> 16);
 }
 
 __device__ __forceinline__ uint32_t popc64(uint64_t v) { return (uint32_t)__popcll(v); }
@@ -95,9 +105,9 @@ __global__ void __launch_bounds__(256) k_ms_init(MBatch b, MWorkspace* ws) {
 // has them.  LDS histogram, merged with one global atomic per non-empty bin; the last
 // block then reads (and clears) the global histogram and fixes the digit holding the
 // kk-th largest key.  PASS 0 also fixes the candidate bin and mode.
-template <bool FROM_FLOAT, int PASS>
+template <int SRC, int PASS>
 __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __restrict__ keys,
-                                                 const float* __restrict__ x, MWorkspace* ws,
+                                                 const void* __restrict__ x, MWorkspace* ws,
                                                  const uint32_t* __restrict__ ckey) {
     constexpr int W = PASS == 0 ? kW1 : kW2;
     constexpr int PER = (1 << W) / 256;
@@ -127,14 +137,14 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             k4[u] = from_cand ? src[i + u * stride]
-                              : key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i + u * stride));
+                              : key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + i + u * stride));
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if ((k4[u] & s.mask) == s.prefix) atomicAdd(&h[(k4[u] >> shift) & dmask], 1u);
     }
     for (; i < n; i += stride) {
         const uint32_t key = from_cand ? src[i]
-                                       : key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
+                                       : key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + i));
         if ((key & s.mask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
     }
     __syncthreads();
@@ -182,9 +192,9 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
 // One block per range: count of keys above the first-pass bin, and (candidate mode)
 // append the bin's keys + local indices to the item's candidate list, one counter
 // atomic per block tile (a tile's candidates stay contiguous).
-template <bool FROM_FLOAT>
+template <int SRC>
 __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __restrict__ keys,
-                                                    const float* __restrict__ x, MWorkspace* ws,
+                                                    const void* __restrict__ x, MWorkspace* ws,
                                                     uint32_t* __restrict__ ckey,
                                                     uint32_t* __restrict__ cidx) {
     __shared__ uint32_t lds[4], s_cnt[4], s_base;
@@ -203,7 +213,7 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
         uint32_t kv[kPerLane];
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j)
-            kv[j] = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)));
+            kv[j] = key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)));
         uint32_t nin = 0;
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
@@ -308,9 +318,9 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
 // compact pass's counts: from the candidates or, in full mode, by rescanning each
 // range.  The last block then turns them into per-range T-equal allowances (lowest
 // ranges first) and output offsets.
-template <bool FROM_FLOAT>
+template <int SRC>
 __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __restrict__ keys,
-                                                  const float* __restrict__ x, MWorkspace* ws,
+                                                  const void* __restrict__ x, MWorkspace* ws,
                                                   const uint32_t* __restrict__ ckey,
                                                   const uint32_t* __restrict__ cidx) {
     __shared__ uint32_t lds[4];
@@ -349,7 +359,7 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
             const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
             uint32_t gt = 0, eq = 0;
             for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
-                const uint32_t key = key_of<FROM_FLOAT>(load_bits<FROM_FLOAT>(keys, x, it.key_off + i));
+                const uint32_t key = key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + i));
                 const bool in = (key & s.m1) == s.p1;
                 gt += (in && key > T) ? 1u : 0u;
                 eq += key == T ? 1u : 0u;
@@ -402,32 +412,32 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
 // One block per range, 4096-key tiles (each wave a contiguous 1024 keys, 16 per lane):
 // ballot compaction in index order.  ARC: rows[out_off + slot] = i and the slot map for
 // every key; TopK: idx[out_off + slot] = i, vals[out_off + slot] = x[key_off + i].
-template <bool FROM_FLOAT, bool ARC>
+template <int SRC, bool ARC>
 __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
-                                              const float* __restrict__ x, MWorkspace* ws,
-                                              int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                              const void* __restrict__ x, MWorkspace* ws,
+                                              int32_t* __restrict__ out_idx, void* __restrict__ out_val,
                                               int32_t* __restrict__ out_slot);
 
-template <bool FROM_FLOAT, bool ARC>
+template <int SRC, bool ARC>
 __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __restrict__ keys,
-                                                  const float* __restrict__ x, MWorkspace* ws,
+                                                  const void* __restrict__ x, MWorkspace* ws,
                                                   int32_t* __restrict__ out_idx,
-                                                  float* __restrict__ out_val,
+                                                  void* __restrict__ out_val,
                                                   int32_t* __restrict__ out_slot) {
-    ms_write_body<FROM_FLOAT, ARC>(b, keys, x, ws, out_idx, out_val, out_slot);
+    ms_write_body<SRC, ARC>(b, keys, x, ws, out_idx, out_val, out_slot);
 }
 
 // ARC: the batch from device memory (plan-resident)
 __global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp, const uint32_t* __restrict__ keys,
                                                    MWorkspace* ws, int32_t* __restrict__ out_idx,
                                                    int32_t* __restrict__ out_slot) {
-    ms_write_body<false, true>(*bp, keys, nullptr, ws, out_idx, nullptr, out_slot);
+    ms_write_body<0, true>(*bp, keys, nullptr, ws, out_idx, nullptr, out_slot);
 }
 
-template <bool FROM_FLOAT, bool ARC>
+template <int SRC, bool ARC>
 __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
-                                              const float* __restrict__ x, MWorkspace* ws,
-                                              int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                              const void* __restrict__ x, MWorkspace* ws,
+                                              int32_t* __restrict__ out_idx, void* __restrict__ out_val,
                                               int32_t* __restrict__ out_slot) {
     __shared__ uint32_t s_eq[4], s_gt[4];
     DIAG_STAMP(g_st_write, 0);
@@ -446,12 +456,12 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* _
         uint32_t bits[kPerLane];
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j)
-            bits[j] = load_bits<FROM_FLOAT>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1));
+            bits[j] = load_bits<SRC>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1));
         uint32_t weq = 0, wgt = 0;
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
             const bool valid = wb + j * 64 + lane < r1;
-            const uint32_t key = key_of<FROM_FLOAT>(bits[j]);
+            const uint32_t key = key_of<SRC>(bits[j]);
             weq += popc64(__ballot(valid && key == T));
             wgt += popc64(__ballot(valid && key > T));
         }
@@ -475,7 +485,7 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* _
         for (int j = 0; j < kPerLane; ++j) {
             const int64_t i = wb + j * 64 + lane;
             const bool valid = i < r1;
-            const uint32_t key = key_of<FROM_FLOAT>(bits[j]);
+            const uint32_t key = key_of<SRC>(bits[j]);
             const bool eq = valid && key == T;
             const bool gt = valid && key > T;
             const uint64_t beq = __ballot(eq);
@@ -484,7 +494,7 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* _
             const int64_t my = run_sel + popc64(bsel & lt);
             if (sel && my < it.k) {  // bound: never store past the item's k outputs
                 out_idx[it.out_off + my] = (int32_t)i;
-                if constexpr (!ARC) out_val[it.out_off + my] = __uint_as_float(bits[j]);
+                if constexpr (!ARC) store_val<SRC>(out_val, it.out_off + my, bits[j]);
             }
             if constexpr (ARC) {
                 if (valid) out_slot[it.slot_off + i] = sel ? (int32_t)my : -1;
@@ -525,8 +535,8 @@ int64_t ms_workspace_bytes(int64_t cap_total) {
     return (int64_t)sizeof(MWorkspace) + 8 * cap_total;
 }
 
-int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* x, bool arc,
-              MWorkspace* ws, int64_t cap_total, int32_t* out_idx, float* out_val,
+int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
+              MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
               int32_t* out_slot, hipStream_t st) {
     const int cnt = b.cnt;
     if (cnt < 1) return 0;
@@ -554,9 +564,11 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const float* 
                            out_val, out_slot);                                                         \
     } while (0)
     if (arc)
-        MS_LAUNCH(false, true);
+        MS_LAUNCH(0, true);
+    else if (x_bf16)
+        MS_LAUNCH(2, false);
     else
-        MS_LAUNCH(true, false);
+        MS_LAUNCH(1, false);
 #undef MS_LAUNCH
     return (int)hipGetLastError();
 }

@@ -6,7 +6,9 @@
 // blocks, and per-block ballot compaction -- so the selected indices come out
 // ascending and ties at the threshold resolve to the lowest indices.
 // All tensors of a bucket (up to ARCTOPK_SPARSE_MAX_BATCH per launch) go into the
-// same launches via blockIdx.y.
+// same launches via blockIdx.y.  fp32 and bf16 buckets: values, residuals and the decoded
+// bucket stay in the bucket dtype, every add / divide rounded to it as the reference's
+// torch ops on a bf16 tensor do (sparse_hook.py:16-34, :103-141, :257-297).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -68,56 +70,62 @@ __global__ void __launch_bounds__(256) k_randk(SparseBatch b, uint64_t seed, int
     }
 }
 
-__global__ void __launch_bounds__(256) k_gather(SparseBatch b, const float* __restrict__ x,
+template <typename T>
+__global__ void __launch_bounds__(256) k_gather(SparseBatch b, const T* __restrict__ x,
                                                 const int32_t* __restrict__ idx,
-                                                float* __restrict__ vals) {
+                                                T* __restrict__ vals) {
     const int t = blockIdx.y;
     const int64_t k = b.k[t];
-    const float* xs = x + b.off[t];
+    const T* xs = x + b.off[t];
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256)
         vals[b.koff[t] + j] = xs[idx[b.koff[t] + j]];
 }
 
-template <int EF>
-__global__ void __launch_bounds__(256) k_residual(SparseBatch b, float* __restrict__ E,
+template <typename T, int EF>
+__global__ void __launch_bounds__(256) k_residual(SparseBatch b, T* __restrict__ E,
                                                   const int32_t* __restrict__ idx,
-                                                  const float* __restrict__ vals) {
+                                                  const T* __restrict__ vals) {
     const int t = blockIdx.y;
     const int64_t k = b.k[t];
-    float* es = E + b.off[t];
+    T* es = E + b.off[t];
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
         const int32_t i = idx[b.koff[t] + j];
-        if constexpr (EF == ARCTOPK_EF14) es[i] = 0.f;
-        else es[i] = es[i] + vals[b.koff[t] + j];
+        if constexpr (EF == ARCTOPK_EF14) es[i] = arctopk::from_f<T>(0.f);
+        else es[i] = arctopk::from_f<T>(arctopk::to_f(es[i]) + arctopk::to_f(vals[b.koff[t] + j]));
     }
 }
 
 // rank-ordered decode: one launch per rank keeps the sum order of the reference
-template <bool ACC>
-__global__ void __launch_bounds__(256) k_scatter(SparseBatch b, float* __restrict__ out,
+template <typename T, bool ACC>
+__global__ void __launch_bounds__(256) k_scatter(SparseBatch b, T* __restrict__ out,
                                                  const int32_t* __restrict__ idx,
-                                                 const float* __restrict__ vals, float wsf) {
+                                                 const T* __restrict__ vals, float wsf) {
+    using arctopk::from_f;
+    using arctopk::to_f;
     const int t = blockIdx.y;
     const int64_t k = b.k[t];
-    float* os = out + b.off[t];
+    T* os = out + b.off[t];
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
         const int32_t i = idx[b.koff[t] + j];
-        const float v = vals[b.koff[t] + j];
-        if constexpr (ACC) os[i] = os[i] + v;          // indices unique within one payload
-        else os[i] = __fdiv_rn(v, wsf);
+        const float v = to_f(vals[b.koff[t] + j]);
+        if constexpr (ACC) os[i] = from_f<T>(to_f(os[i]) + v);  // indices unique within one payload
+        else os[i] = from_f<T>(__fdiv_rn(v, wsf));
     }
 }
 
-__global__ void __launch_bounds__(256) k_div_gE(float* __restrict__ out, float* __restrict__ gE,
+template <typename T>
+__global__ void __launch_bounds__(256) k_div_gE(T* __restrict__ out, T* __restrict__ gE,
                                                 int64_t n, float wsf, int do_div) {
+    using arctopk::from_f;
+    using arctopk::to_f;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        float v = out[i];
-        if (do_div) v = __fdiv_rn(v, wsf);
+        float v = to_f(out[i]);
+        if (do_div) v = to_f(from_f<T>(__fdiv_rn(v, wsf)));
         if (gE) {
-            v = gE[i] + v;
-            gE[i] = v;
+            v = to_f(from_f<T>(to_f(gE[i]) + v));
+            gE[i] = from_f<T>(v);
         }
-        out[i] = v;
+        out[i] = from_f<T>(v);
     }
 }
 
@@ -168,11 +176,12 @@ extern "C" int64_t arctopk_sparse_workspace_bytes(int32_t nt, const int64_t* num
     return arctopk::ms_workspace_bytes(topk_cap_total(nt, numels));
 }
 
-extern "C" int arctopk_topk_select(const float* x, int32_t nt, const int64_t* offsets,
+extern "C" int arctopk_topk_select(const void* x, int32_t nt, const int64_t* offsets,
                                    const int64_t* numels, const int64_t* ks, const int64_t* k_off,
-                                   int32_t* idx, float* vals, void* workspace, void* stream) {
+                                   int32_t* idx, void* vals, void* workspace, int32_t dtype, void* stream) {
     if (!x || !offsets || !numels || !ks || !k_off || !idx || !vals || !workspace || nt < 1)
         return ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
     for (int32_t j = 0; j < nt; ++j)
         if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j])
             return ARCTOPK_EINVAL;
@@ -196,7 +205,8 @@ extern "C" int arctopk_topk_select(const float* x, int32_t nt, const int64_t* of
             cap += it.cand_cap;
             maxn = std::max(maxn, numels[j]);
         }
-        int e = arctopk::ms_select(b, maxn, nullptr, x, false, ws, cap_total, idx, vals, nullptr, st);
+        int e = arctopk::ms_select(b, maxn, nullptr, x, dtype == ARCTOPK_BF16, false, ws, cap_total, idx, vals,
+                                   nullptr, st);
         if (e) return e;
     }
     return 0;
@@ -219,27 +229,34 @@ extern "C" int arctopk_randk_indices(int32_t nt, const int64_t* numels, const in
     return 0;
 }
 
-extern "C" int arctopk_sparse_gather(const float* x, int32_t nt, const int64_t* offsets,
+extern "C" int arctopk_sparse_gather(const void* x, int32_t nt, const int64_t* offsets,
                                      const int64_t* ks, const int64_t* k_off, const int32_t* idx,
-                                     float* vals, void* stream) {
+                                     void* vals, int32_t dtype, void* stream) {
     if (!x || !offsets || !ks || !k_off || !idx || !vals || nt < 1) return ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
     for (int32_t first = 0; first < nt; first += kB) {
         SparseBatch b;
         int64_t maxn, maxk;
         const int cnt = std::min<int32_t>(kB, nt - first);
         int e = fill_batch(b, first, cnt, offsets, nullptr, ks, k_off, maxn, maxk);
         if (e) return e;
-        hipLaunchKernelGGL(k_gather, dim3(grid_for(maxk, 2048), cnt), dim3(256), 0,
-                           (hipStream_t)stream, b, x, idx, vals);
+        if (dtype == ARCTOPK_BF16)
+            hipLaunchKernelGGL(k_gather<arctopk::bf16_t>, dim3(grid_for(maxk, 2048), cnt), dim3(256), 0,
+                               (hipStream_t)stream, b, static_cast<const arctopk::bf16_t*>(x), idx,
+                               static_cast<arctopk::bf16_t*>(vals));
+        else
+            hipLaunchKernelGGL(k_gather<float>, dim3(grid_for(maxk, 2048), cnt), dim3(256), 0,
+                               (hipStream_t)stream, b, static_cast<const float*>(x), idx, static_cast<float*>(vals));
         e = (int)hipGetLastError();
         if (e) return e;
     }
     return 0;
 }
 
-extern "C" int arctopk_sparse_residual(float* E, int32_t nt, const int64_t* offsets,
+extern "C" int arctopk_sparse_residual(void* E, int32_t nt, const int64_t* offsets,
                                        const int64_t* ks, const int64_t* k_off, const int32_t* idx,
-                                       const float* vals, int32_t ef, void* stream) {
+                                       const void* vals, int32_t ef, int32_t dtype, void* stream) {
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF_NONE) return 0;
     if (!E || !offsets || !ks || !k_off || !idx || nt < 1) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF21 && !vals) return ARCTOPK_EINVAL;
@@ -250,28 +267,39 @@ extern "C" int arctopk_sparse_residual(float* E, int32_t nt, const int64_t* offs
         int e = fill_batch(b, first, cnt, offsets, nullptr, ks, k_off, maxn, maxk);
         if (e) return e;
         dim3 grid(grid_for(maxk, 2048), cnt);
-        if (ef == ARCTOPK_EF14)
-            hipLaunchKernelGGL(k_residual<ARCTOPK_EF14>, grid, dim3(256), 0, (hipStream_t)stream, b, E, idx, vals);
-        else if (ef == ARCTOPK_EF21)
-            hipLaunchKernelGGL(k_residual<ARCTOPK_EF21>, grid, dim3(256), 0, (hipStream_t)stream, b, E, idx, vals);
-        else
-            return ARCTOPK_EINVAL;
+        hipStream_t st = (hipStream_t)stream;
+        using arctopk::bf16_t;
+        if (dtype == ARCTOPK_BF16) {
+            bf16_t* Eb = static_cast<bf16_t*>(E);
+            const bf16_t* vb = static_cast<const bf16_t*>(vals);
+            if (ef == ARCTOPK_EF14)
+                hipLaunchKernelGGL((k_residual<bf16_t, ARCTOPK_EF14>), grid, dim3(256), 0, st, b, Eb, idx, vb);
+            else if (ef == ARCTOPK_EF21)
+                hipLaunchKernelGGL((k_residual<bf16_t, ARCTOPK_EF21>), grid, dim3(256), 0, st, b, Eb, idx, vb);
+            else
+                return ARCTOPK_EINVAL;
+        } else {
+            float* Ef = static_cast<float*>(E);
+            const float* vf = static_cast<const float*>(vals);
+            if (ef == ARCTOPK_EF14)
+                hipLaunchKernelGGL((k_residual<float, ARCTOPK_EF14>), grid, dim3(256), 0, st, b, Ef, idx, vf);
+            else if (ef == ARCTOPK_EF21)
+                hipLaunchKernelGGL((k_residual<float, ARCTOPK_EF21>), grid, dim3(256), 0, st, b, Ef, idx, vf);
+            else
+                return ARCTOPK_EINVAL;
+        }
         e = (int)hipGetLastError();
         if (e) return e;
     }
     return 0;
 }
 
-extern "C" int arctopk_sparse_decode(float* out, int64_t numel, int32_t nt, const int64_t* offsets,
-                                     const int64_t* ks, const int64_t* k_off, int64_t packed_len,
-                                     const int32_t* idx, const float* vals, int32_t nranks,
-                                     int32_t world_size, int32_t accumulate, float* gerr,
-                                     void* stream) {
-    if (!out || !offsets || !ks || !k_off || !idx || !vals || nt < 1 || nranks < 1 ||
-        world_size < 1 || numel < 0)
-        return ARCTOPK_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    hipError_t he = hipMemsetAsync(out, 0, (size_t)numel * sizeof(float), st);
+namespace {
+template <typename T>
+int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, const int64_t* ks,
+                    const int64_t* k_off, int64_t packed_len, const int32_t* idx, const T* vals,
+                    int32_t nranks, int32_t world_size, int32_t accumulate, T* gerr, hipStream_t st) {
+    hipError_t he = hipMemsetAsync(out, 0, (size_t)numel * sizeof(T), st);
     if (he != hipSuccess) return (int)he;
     const float wsf = (float)world_size;
     const int nr = accumulate ? nranks : 1;
@@ -284,16 +312,37 @@ extern "C" int arctopk_sparse_decode(float* out, int64_t numel, int32_t nt, cons
             if (e) return e;
             dim3 grid(grid_for(maxk, 2048), cnt);
             const int32_t* iq = idx + (int64_t)q * packed_len;
-            const float* vq = vals + (int64_t)q * packed_len;
+            const T* vq = vals + (int64_t)q * packed_len;
             if (accumulate)
-                hipLaunchKernelGGL(k_scatter<true>, grid, dim3(256), 0, st, b, out, iq, vq, wsf);
+                hipLaunchKernelGGL((k_scatter<T, true>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
             else
-                hipLaunchKernelGGL(k_scatter<false>, grid, dim3(256), 0, st, b, out, iq, vq, wsf);
+                hipLaunchKernelGGL((k_scatter<T, false>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
         }
     }
     if (accumulate || gerr) {
-        hipLaunchKernelGGL(k_div_gE, dim3(grid_for(numel, 8192)), dim3(256), 0, st, out, gerr,
+        hipLaunchKernelGGL(k_div_gE<T>, dim3(grid_for(numel, 8192)), dim3(256), 0, st, out, gerr,
                            numel, wsf, accumulate);
     }
     return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int arctopk_sparse_decode(void* out, int64_t numel, int32_t nt, const int64_t* offsets,
+                                     const int64_t* ks, const int64_t* k_off, int64_t packed_len,
+                                     const int32_t* idx, const void* vals, int32_t nranks,
+                                     int32_t world_size, int32_t accumulate, void* gerr,
+                                     int32_t dtype, void* stream) {
+    if (!out || !offsets || !ks || !k_off || !idx || !vals || nt < 1 || nranks < 1 ||
+        world_size < 1 || numel < 0)
+        return ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    using arctopk::bf16_t;
+    if (dtype == ARCTOPK_BF16)
+        return sparse_decode_t<bf16_t>(static_cast<bf16_t*>(out), numel, nt, offsets, ks, k_off, packed_len, idx,
+                                       static_cast<const bf16_t*>(vals), nranks, world_size, accumulate,
+                                       static_cast<bf16_t*>(gerr), st);
+    return sparse_decode_t<float>(static_cast<float*>(out), numel, nt, offsets, ks, k_off, packed_len, idx,
+                                  static_cast<const float*>(vals), nranks, world_size, accumulate,
+                                  static_cast<float*>(gerr), st);
 }

@@ -202,7 +202,9 @@ int arctopk_decode_segments(const arctopk_plan* plan, int32_t seg_begin, int32_t
 
 /* ---- TopK / RandK baselines (comm_hooks/sparse_hook.py, sparse_hook_c4.py) ---------- */
 /*
- * Tensors of a bucket are described by host arrays of `ntensors` entries:
+ * Bucket-typed buffers (x, vals, E, out, gerr) are of element type `dtype` (ARCTOPK_F32 or
+ * ARCTOPK_BF16); bf16 arithmetic rounds after every add / divide, as the reference's torch
+ * ops on bf16 tensors do.  Tensors of a bucket are described by host arrays of `ntensors` entries:
  * offsets[i] (element offset in the bucket), numels[i], ks[i] (= max(1, int(numel*ratio)),
  * sparse_hook.py:77-78) and k_off[i] (offset of tensor i's k entries in the packed
  * idx/vals buffers).  Up to ARCTOPK_SPARSE_MAX_BATCH tensors go into one launch; more
@@ -224,9 +226,9 @@ int64_t arctopk_sparse_workspace_bytes(int32_t ntensors, const int64_t* numels);
  * Replaces: torch.topk(tensor.abs(), k, sorted=False), .to(int32), tensor[indices]
  * (sparse_hook.py:26-28, :97-98).
  */
-int arctopk_topk_select(const float* x, int32_t ntensors, const int64_t* offsets,
+int arctopk_topk_select(const void* x, int32_t ntensors, const int64_t* offsets,
                         const int64_t* numels, const int64_t* ks, const int64_t* k_off,
-                        int32_t* idx, float* vals, void* workspace, void* stream);
+                        int32_t* idx, void* vals, void* workspace, int32_t dtype, void* stream);
 
 /*
  * RandK index source, device-side: idx[k_off[i] + j] = pi_i(j) for j < k, where pi_i is
@@ -238,18 +240,18 @@ int arctopk_randk_indices(int32_t ntensors, const int64_t* numels, const int64_t
                           const int64_t* k_off, uint64_t seed, int32_t* idx, void* stream);
 
 /* Gather vals[k_off[i] + j] = x[offsets[i] + idx[k_off[i] + j]]  (sparse_hook.py:22). */
-int arctopk_sparse_gather(const float* x, int32_t ntensors, const int64_t* offsets,
+int arctopk_sparse_gather(const void* x, int32_t ntensors, const int64_t* offsets,
                           const int64_t* ks, const int64_t* k_off, const int32_t* idx,
-                          float* vals, void* stream);
+                          void* vals, int32_t dtype, void* stream);
 
 /*
  * Residual persistence at the selected entries (sparse_hook.py:103-109, :257-267):
  *   EF14 : E[off + idx] = 0        (E already holds x = G + E_prev, see arctopk_ef_apply)
  *   EF21 : E[off + idx] += vals    (E_new = E + C(G - E); C(.) is zero elsewhere)
  */
-int arctopk_sparse_residual(float* E, int32_t ntensors, const int64_t* offsets,
+int arctopk_sparse_residual(void* E, int32_t ntensors, const int64_t* offsets,
                             const int64_t* ks, const int64_t* k_off, const int32_t* idx,
-                            const float* vals, int32_t ef, void* stream);
+                            const void* vals, int32_t ef, int32_t dtype, void* stream);
 
 /*
  * Decode into `out` (every element written):
@@ -259,10 +261,11 @@ int arctopk_sparse_residual(float* E, int32_t ntensors, const int64_t* offsets,
  * `vals`/`idx` hold nranks consecutive payloads of packed_len entries each.
  * EF21 (gerr != NULL): gE += out; out = gE (:295-297).
  */
-int arctopk_sparse_decode(float* out, int64_t numel, int32_t ntensors, const int64_t* offsets,
+int arctopk_sparse_decode(void* out, int64_t numel, int32_t ntensors, const int64_t* offsets,
                           const int64_t* ks, const int64_t* k_off, int64_t packed_len,
-                          const int32_t* idx, const float* vals, int32_t nranks,
-                          int32_t world_size, int32_t accumulate, float* gerr, void* stream);
+                          const int32_t* idx, const void* vals, int32_t nranks,
+                          int32_t world_size, int32_t accumulate, void* gerr, int32_t dtype,
+                          void* stream);
 
 /*
  * EF pre-apply on a whole bucket, one pass (ARC-TopK fuses this into arctopk_encode):
@@ -271,7 +274,8 @@ int arctopk_sparse_decode(float* out, int64_t numel, int32_t ntensors, const int
  * Replaces: input_tensor.add_(error_dict[b], alpha=+-1) (sparse_hook.py:205, :212) and the
  * full-bucket E.copy_(input_tensor) of EF14 (:258).
  */
-int arctopk_ef_apply(float* x, float* E, int64_t numel, int32_t ef, int32_t err_in, void* stream);
+int arctopk_ef_apply(void* x, void* E, int64_t numel, int32_t ef, int32_t err_in, int32_t dtype,
+                     void* stream);
 
 /*
  * Device projections of one bucket call: for every SKETCH segment in bucket order,

@@ -111,7 +111,7 @@ def test_compute_entry_points_reject_null_without_touching_device(lib):
     assert lib.arctopk_select(None, 0, 1, 0, 0, None) == 1001
     assert lib.arctopk_pack(None, 0, 0, 0, 0, 0, 0, None) == 1001
     assert lib.arctopk_decode(None, 0, 0, 1, 0, 0, 0, None) == 1001
-    assert lib.arctopk_ef_apply(None, None, 10, 1, 1, None) == 1001
+    assert lib.arctopk_ef_apply(None, None, 10, 1, 1, 0, None) == 1001
     assert lib.arctopk_sparse_workspace_bytes(2, N.i64_array([10, 4_000_000])) > 500_000 * 8
     assert lib.arctopk_sparse_workspace_bytes(0, None) == -1001
     assert lib.arctopk_sparse_workspace_bytes(1, N.i64_array([0])) == -1001
