@@ -24,7 +24,7 @@ namespace arctopk {
 constexpr int kMaxR = 8;           // sketch rank supported by the kernels
 constexpr int kTileRows = 256;     // row granule of a small-m encode tile (thread per row)
 #ifndef ARCTOPK_SMALL_TILE_BYTES
-#define ARCTOPK_SMALL_TILE_BYTES 32768
+#define ARCTOPK_SMALL_TILE_BYTES 16384  // 16 KiB: ResNet-18 DDP buckets 228 -> 234 GB/s, large buckets unchanged
 #endif
 constexpr int kSmallTileBytes = ARCTOPK_SMALL_TILE_BYTES;  // tensor bytes per small-m encode tile
 constexpr int kSmallM = 64;        // m below this: thread-per-row tiles; else wave-per-row

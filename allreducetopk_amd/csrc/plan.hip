@@ -120,8 +120,14 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     if (const char* env = std::getenv("ARCTOPK_ENC_TARGET_BLOCKS")) target = std::max(1, std::atoi(env));  // tuning
     const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(8192, row_work / target));
     int64_t pack_elems = kChunkElems, dec_elems = kChunkElems;  // tuning switches (A/B)
+    // short rows (m < 256) and the m <= 2 streams: smaller chunks, more blocks in flight
+    // (ResNet-50 1x1 mix, 2048-element stream pack chunks: 346 -> 356 GB/s; 4096-element
+    // decode chunks: +3 %; rows of >= 256 elements keep kChunkElems)
+    int64_t stream_pack_elems = 2048, short_dec_elems = 4096;
     if (const char* env = std::getenv("ARCTOPK_PACK_CHUNK")) pack_elems = std::max(64, std::atoi(env));
     if (const char* env = std::getenv("ARCTOPK_DEC_CHUNK")) dec_elems = std::max(64, std::atoi(env));
+    if (const char* env = std::getenv("ARCTOPK_STREAM_PACK_CHUNK")) stream_pack_elems = std::max(64, std::atoi(env));
+    if (const char* env = std::getenv("ARCTOPK_SHORT_DEC_CHUNK")) short_dec_elems = std::max(64, std::atoi(env));
     bool interleave = true;  // tuning switch (A/B): interleaved row tiles vs contiguous ranges
     if (const char* env = std::getenv("ARCTOPK_ENC_INTERLEAVE")) interleave = std::atoi(env) != 0;
     int64_t part_len = 0, split_rows_max = 0;
@@ -203,7 +209,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         // their 4- and 8-B rows are too short for per-row gathers
         const bool stream_small = (s.m == 1 || s.m == 2) && s.offset % 4 == 0 && dtype == ARCTOPK_F32;
         if (stream_small) {
-            const int64_t per = pack_elems / s.m;  // a multiple of 4 rows: quads never straddle chunks
+            const int64_t per = (stream_pack_elems / s.m + 3) / 4 * 4;  // quads never straddle chunks
             for (int64_t row = 0; row < s.n; row += per)
                 pack.push_back(Chunk{(int32_t)i, 1, row, std::min(per, s.n - row)});
         } else {
@@ -214,7 +220,8 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         }
         // ---- decode chunks: all rows
         {
-            int64_t per = std::max<int64_t>(min_rows, dec_elems / s.m);
+            int64_t per = std::max<int64_t>(min_rows, (s.m < 256 ? short_dec_elems : dec_elems) / s.m);
+            if (stream_small) per = (per + 3) / 4 * 4;  // mode 1: whole quads per chunk
             if (small_tile)  // the chunk tile lives in LDS: <= 64 KiB
                 per = std::min<int64_t>(std::min<int64_t>(per, kSmallTileRows), 16000 / s.m);
             for (int64_t row = 0; row < s.n; row += per)
