@@ -594,3 +594,39 @@ def test_device_projection_draw_matches_torch_randn_on_device(dtype):
             adv = ctypes.c_uint64()
             N.check(N.lib().arctopk_plan_philox_advance(plan.handle, ctypes.byref(adv)), "advance")
             assert adv.value == off, f"set {si}: philox advance {adv.value} vs torch {off}"
+
+
+@pytest.mark.parametrize("ef", ["ef14", "ef21"])
+def test_torch_op_layer_matches_direct_calls(ef):
+    """torch.ops.arctopk.* (allreducetopk_amd/ops.py) run the same kernels as the C entry
+    points: one call through the ops and one through the BucketPlan methods on identical
+    inputs give bit-identical sketch, rows, slots, packed values, residuals and output."""
+    import allreducetopk_amd.ops  # noqa: F401
+    shapes = [tuple(s) for s in MIX]
+    code = N.EF_CODE[ef]
+    outs = []
+    for use_ops in (False, True):
+        plan = BucketPlan(shapes, 4, 0.2, torch.float32, DEV)
+        h = plan.handle.value
+        G = _rand_bucket(MIX, 77).to(DEV)
+        E = _rand_bucket(MIX, 78).to(DEV) * 0.1
+        gE = _rand_bucket(MIX, 79).to(DEV)
+        V = plan.V_ring[0]
+        s = torch.cuda.current_stream().cuda_stream
+        if use_ops:
+            torch.ops.arctopk.draw_projections(h, 12345, V)
+            torch.ops.arctopk.encode(h, G, E, code, True, V, plan.sketch)
+            torch.ops.arctopk.select(h, plan.sketch, 1, plan.rowlist, plan.slotmap)
+            torch.ops.arctopk.pack(h, G, E, code, plan.rowlist, plan.slotmap, plan.packed)
+            torch.ops.arctopk.decode(h, plan.packed, plan.slotmap, 1, code,
+                                     gE if ef == "ef21" else None, G)
+        else:
+            N.check(N.lib().arctopk_draw_projections(plan.handle, 12345, V.data_ptr(), s), "draw")
+            plan.encode(G, E, code, True, V, s)
+            plan.select(1, s)
+            plan.pack(G, E, code, s)
+            plan.decode(1, code, gE if ef == "ef21" else None, G, s)
+        torch.cuda.synchronize()
+        outs.append([t.clone().cpu() for t in (plan.sketch, plan.rowlist, plan.slotmap, plan.packed, E, gE, G)])
+    for a, b_, what in zip(outs[0], outs[1], ("sketch", "rowlist", "slotmap", "packed", "E", "gE", "out")):
+        assert_bitwise(b_, a, f"ops vs direct: {what}")

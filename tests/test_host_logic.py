@@ -328,3 +328,20 @@ def test_state_rng_is_lazy_but_exact():
     st2 = GroupTopKState(None, seed=1)
     st2.load_state_dict(st.state_dict())
     assert [st2._next_seed() for _ in range(3)] == [ref_seed() for _ in range(3)]
+
+
+def test_torch_op_layer_registered():
+    """torch.ops.arctopk.* exist with schemas that declare what each op mutates (so the
+    dispatcher, torch.compile and graph capture see the codec phases as ops)."""
+    import allreducetopk_amd.ops  # noqa: F401
+    sch = {name: str(getattr(torch.ops.arctopk, name).default._schema)
+           for name in ("draw_projections", "encode", "select", "pack", "decode")}
+    import re
+
+    def mutated(s):
+        return set(re.findall(r"Tensor\(a\d+!\)\?? (\w+)", s))
+    assert mutated(sch["draw_projections"]) == {"V"}
+    assert mutated(sch["encode"]) == {"err", "sketch"}
+    assert mutated(sch["select"]) == {"rowlist", "slotmap"}
+    assert mutated(sch["pack"]) == {"err", "packed"}
+    assert mutated(sch["decode"]) == {"gerr", "out"}
