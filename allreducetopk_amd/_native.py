@@ -68,7 +68,8 @@ _SIGS = {
     "arctopk_sparse_workspace_bytes": (c_int64, [c_int32, POINTER(c_int64)]),
     "arctopk_topk_select": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
                                       POINTER(c_int64), POINTER(c_int64), c_void_p, c_void_p, c_void_p,
-                                      c_int32, c_void_p]),
+                                      c_int32, c_int32, c_void_p]),
+    "arctopk_ef14_fold": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p]),
     "arctopk_randk_indices": (c_int32, [c_int32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64),
                                         c_uint64, c_void_p, c_void_p]),
     "arctopk_sparse_gather": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),

@@ -140,8 +140,10 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
             logger.info("A zero tensor of length %s that represents local error is created.", total)
             state.error_dict[b] = torch.zeros(total, device=device, dtype=dtype)
         err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
-        N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), err.data_ptr(), total,
-                                   N.EF14, int(err_in), dt, stream), "arctopk_ef_apply")
+        # E := G + E (:205, :258); selection and gathers then read the pre-compression bucket
+        # from E, and the decode writes the bucket once
+        N.check(L.arctopk_ef14_fold(input_tensor.data_ptr(), err.data_ptr(), total, int(err_in),
+                                    dt, stream), "arctopk_ef14_fold")
     elif ef == N.EF21:
         if b in state.error_dict:
             err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
@@ -181,11 +183,13 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
         acc += k
     sum_k = acc
     nt = len(tensors)
+    fold14 = ef == N.EF14  # the pre-compression bucket lives in E (arctopk_ef14_fold)
     a_off, a_n, a_k, a_ko = (N.i64_array(offsets), N.i64_array(numels), N.i64_array(ks),
                              N.i64_array(k_off))
     values = torch.empty(sum_k, dtype=dtype, device=device)
     indices = torch.empty(sum_k, dtype=torch.int32, device=device)
     x = input_tensor.data_ptr()
+    xsrc = state.error_dict[b].data_ptr() if fold14 else x
     if state.random:
         if state.index_source == "torch":  # the reference's own draw (:20), per tensor in order
             for t, k, ko in zip(tensors, ks, k_off):
@@ -193,20 +197,21 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
         else:
             N.check(L.arctopk_randk_indices(nt, a_n, a_k, a_ko, int(seed), indices.data_ptr(),
                                             stream), "arctopk_randk_indices")
-        N.check(L.arctopk_sparse_gather(x, nt, a_off, a_k, a_ko, indices.data_ptr(),
+        N.check(L.arctopk_sparse_gather(xsrc, nt, a_off, a_k, a_ko, indices.data_ptr(),
                                         values.data_ptr(), dt, stream), "arctopk_sparse_gather")
         bits_sum = sum_k * dtype_bits(dtype)
     else:
         ws_buf = _workspace(state, device, numels)
-        N.check(L.arctopk_topk_select(x, nt, a_off, a_n, a_k, a_ko, indices.data_ptr(),
-                                      values.data_ptr(), ws_buf.data_ptr(), dt, stream),
+        # EF14: the residual's `E[indices] = 0` (:104) happens in the select's last pass
+        N.check(L.arctopk_topk_select(xsrc, nt, a_off, a_n, a_k, a_ko, indices.data_ptr(),
+                                      values.data_ptr(), ws_buf.data_ptr(), dt, int(fold14), stream),
                 "arctopk_topk_select")
         bits_sum = sum_k * (dtype_bits(dtype) + 32)
 
     # the call's selection, for inspection and tests (int32 indices per tensor, concatenated
     # in bucket order at the k offsets; TopK: ascending within a tensor)
     state.last_indices, state.last_k = indices, ks
-    if ef != N.EF_NONE:  # residual persistence (:257-267)
+    if ef != N.EF_NONE and not (fold14 and not state.random):  # residual persistence (:257-267)
         N.check(L.arctopk_sparse_residual(state.error_dict[b].data_ptr(), nt, a_off, a_k, a_ko,
                                           indices.data_ptr(), values.data_ptr(), ef, dt, stream),
                 "arctopk_sparse_residual")

@@ -2026,7 +2026,9 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
     }
 }
 
-template <int EF, bool ERR_IN>
+// WRITE_X = false (EF14 fold): E := x + E only; the caller reads the pre-compression
+// bucket from E afterwards (TopK / RandK), so x is not written twice
+template <int EF, bool ERR_IN, bool WRITE_X = true>
 __global__ void __launch_bounds__(256) k_ef_apply(float* __restrict__ x, float* __restrict__ E,
                                                   int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * 256;
@@ -2036,23 +2038,23 @@ __global__ void __launch_bounds__(256) k_ef_apply(float* __restrict__ x, float* 
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
         const float4 v = ef_apply4<EF, ERR_IN>(x4, e4, i);
         if constexpr (EF == ARCTOPK_EF14) e4[i] = v;
-        if constexpr (EF != ARCTOPK_EF14 || ERR_IN) x4[i] = v;
+        if constexpr ((EF != ARCTOPK_EF14 || ERR_IN) && WRITE_X) x4[i] = v;
     }
     for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         const float v = ef_apply1<float, EF, ERR_IN>(x, E, i);
         if constexpr (EF == ARCTOPK_EF14) E[i] = v;
-        if constexpr (EF != ARCTOPK_EF14 || ERR_IN) x[i] = v;
+        if constexpr ((EF != ARCTOPK_EF14 || ERR_IN) && WRITE_X) x[i] = v;
     }
 }
 
 // bf16 buckets (TopK / RandK): element-wise, x = rnd(x +- E) as the reference's bf16 add_
-template <int EF, bool ERR_IN>
+template <int EF, bool ERR_IN, bool WRITE_X = true>
 __global__ void __launch_bounds__(256) k_ef_apply_bf16(bf16_t* __restrict__ x, bf16_t* __restrict__ E,
                                                        int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const float v = ef_apply1<bf16_t, EF, ERR_IN>(x, E, i);
         if constexpr (EF == ARCTOPK_EF14) st1<bf16_t>(E + i, v);
-        if constexpr (EF != ARCTOPK_EF14 || ERR_IN) st1<bf16_t>(x + i, v);
+        if constexpr ((EF != ARCTOPK_EF14 || ERR_IN) && WRITE_X) st1<bf16_t>(x + i, v);
     }
 }
 
@@ -2422,6 +2424,37 @@ extern "C" int arctopk_ef_apply(void* x_, void* E_, int64_t n, int32_t ef, int32
         hipLaunchKernelGGL((k_ef_apply<ARCTOPK_EF21, true>), dim3(grid), dim3(256), 0, st, x, E, n);
     else
         return ARCTOPK_EINVAL;
+    return (int)hipGetLastError();
+}
+
+// EF14 fold for the sparse hooks: E := x + E (err_in) or E := x (first call), x untouched.
+// Replaces input_tensor.add_(E) (sparse_hook.py:205) and E.copy_(input_tensor) (:258): the
+// caller then selects / gathers from E and decodes into x, so x is written once, by the
+// decode, instead of twice.
+extern "C" int arctopk_ef14_fold(const void* x_, void* E_, int64_t n, int32_t err_in, int32_t dtype,
+                                 void* stream) {
+    if (!x_ || !E_ || n < 0) return ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == ARCTOPK_BF16) {
+        bf16_t* x = static_cast<bf16_t*>(const_cast<void*>(x_));
+        bf16_t* E = static_cast<bf16_t*>(E_);
+        const dim3 g((unsigned)std::min<int64_t>(8192, (n + 255) / 256));
+        if (err_in)
+            hipLaunchKernelGGL((k_ef_apply_bf16<ARCTOPK_EF14, true, false>), g, dim3(256), 0, st, x, E, n);
+        else
+            hipLaunchKernelGGL((k_ef_apply_bf16<ARCTOPK_EF14, false, false>), g, dim3(256), 0, st, x, E, n);
+        return (int)hipGetLastError();
+    }
+    float* x = static_cast<float*>(const_cast<void*>(x_));
+    float* E = static_cast<float*>(E_);
+    if (((uintptr_t)x | (uintptr_t)E) & 15) return ARCTOPK_EINVAL;
+    const int grid = (int)std::min<int64_t>(8192, (n / 4 + 255) / 256 + 1);
+    if (err_in)
+        hipLaunchKernelGGL((k_ef_apply<ARCTOPK_EF14, true, false>), dim3(grid), dim3(256), 0, st, x, E, n);
+    else
+        hipLaunchKernelGGL((k_ef_apply<ARCTOPK_EF14, false, false>), dim3(grid), dim3(256), 0, st, x, E, n);
     return (int)hipGetLastError();
 }
 

@@ -191,9 +191,10 @@ int64_t ms_workspace_bytes(int64_t cap_total);
 // ascending indices + gathered values.  cap_total: candidate slots in the workspace
 // (the items' cand_off + cand_cap must fit).  The workspace's `done` counters must be
 // zero before the first use (hipMemset once; every kernel leaves them zero).
+// zero_x (TopK only, = x or null): write x back with the selected elements zeroed
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
-              int32_t* out_slot, hipStream_t st);
+              int32_t* out_slot, void* zero_x, hipStream_t st);
 
 // ARC selection after the fused key kernel (keys + first-pass histogram + digit, every
 // item in candidate mode), in three launches per batch: ms_arc_compact (per range: the

@@ -416,29 +416,32 @@ template <int SRC, bool ARC>
 __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
                                               const void* __restrict__ x, MWorkspace* ws,
                                               int32_t* __restrict__ out_idx, void* __restrict__ out_val,
-                                              int32_t* __restrict__ out_slot);
+                                              int32_t* __restrict__ out_slot, void* zero_x);
 
 template <int SRC, bool ARC>
 __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __restrict__ keys,
                                                   const void* __restrict__ x, MWorkspace* ws,
                                                   int32_t* __restrict__ out_idx,
                                                   void* __restrict__ out_val,
-                                                  int32_t* __restrict__ out_slot) {
-    ms_write_body<SRC, ARC>(b, keys, x, ws, out_idx, out_val, out_slot);
+                                                  int32_t* __restrict__ out_slot, void* zero_x) {
+    ms_write_body<SRC, ARC>(b, keys, x, ws, out_idx, out_val, out_slot, zero_x);
 }
 
 // ARC: the batch from device memory (plan-resident)
 __global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp, const uint32_t* __restrict__ keys,
                                                    MWorkspace* ws, int32_t* __restrict__ out_idx,
                                                    int32_t* __restrict__ out_slot) {
-    ms_write_body<0, true>(*bp, keys, nullptr, ws, out_idx, nullptr, out_slot);
+    ms_write_body<0, true>(*bp, keys, nullptr, ws, out_idx, nullptr, out_slot, nullptr);
 }
 
+// TopK (!ARC) with zero_x (= x): the tile is rewritten with its selected elements zeroed,
+// whole tiles, so no line is left partially dirty -- EF14's `tensor.view(-1)[indices] = 0`
+// (sparse_hook.py:104) fused into the pass that already reads every element
 template <int SRC, bool ARC>
 __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
                                               const void* __restrict__ x, MWorkspace* ws,
                                               int32_t* __restrict__ out_idx, void* __restrict__ out_val,
-                                              int32_t* __restrict__ out_slot) {
+                                              int32_t* __restrict__ out_slot, void* zero_x) {
     __shared__ uint32_t s_eq[4], s_gt[4];
     DIAG_STAMP(g_st_write, 0);
     int t, r;
@@ -498,6 +501,11 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* _
             }
             if constexpr (ARC) {
                 if (valid) out_slot[it.slot_off + i] = sel ? (int32_t)my : -1;
+            } else {
+                if (zero_x && valid) {
+                    if constexpr (SRC == 1) static_cast<float*>(zero_x)[it.key_off + i] = sel ? 0.f : __uint_as_float(bits[j]);
+                    else if constexpr (SRC == 2) static_cast<uint16_t*>(zero_x)[it.key_off + i] = sel ? (uint16_t)0 : (uint16_t)(bits[j] >> 16);
+                }
             }
             run_eq += popc64(beq);
             run_sel += popc64(bsel);
@@ -537,7 +545,7 @@ int64_t ms_workspace_bytes(int64_t cap_total) {
 
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
-              int32_t* out_slot, hipStream_t st) {
+              int32_t* out_slot, void* zero_x, hipStream_t st) {
     const int cnt = b.cnt;
     if (cnt < 1) return 0;
     int gr = 1;
@@ -561,7 +569,7 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
         hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
         hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);          \
         hipLaunchKernelGGL((k_ms_write<FF, AR>), gflat, dim3(256), 0, st, b, keys, x, ws, out_idx,     \
-                           out_val, out_slot);                                                         \
+                           out_val, out_slot, zero_x);                                                 \
     } while (0)
     if (arc)
         MS_LAUNCH(0, true);

@@ -96,7 +96,9 @@ __global__ void __launch_bounds__(256) k_residual(SparseBatch b, T* __restrict__
 }
 
 // rank-ordered decode: one launch per rank keeps the sum order of the reference
-template <typename T, bool ACC>
+// MODE 0: out[i] = v / ws (RandK); 1: out[i] += v (TopK, ranks after the first);
+// 2: out[i] = 0 + v (TopK's first rank into the zeroed bucket: no read, -0 still becomes +0)
+template <typename T, int MODE>
 __global__ void __launch_bounds__(256) k_scatter(SparseBatch b, T* __restrict__ out,
                                                  const int32_t* __restrict__ idx,
                                                  const T* __restrict__ vals, float wsf) {
@@ -108,7 +110,8 @@ __global__ void __launch_bounds__(256) k_scatter(SparseBatch b, T* __restrict__ 
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
         const int32_t i = idx[b.koff[t] + j];
         const float v = to_f(vals[b.koff[t] + j]);
-        if constexpr (ACC) os[i] = from_f<T>(to_f(os[i]) + v);  // indices unique within one payload
+        if constexpr (MODE == 1) os[i] = from_f<T>(to_f(os[i]) + v);  // indices unique within one payload
+        else if constexpr (MODE == 2) os[i] = from_f<T>(0.f + v);
         else os[i] = from_f<T>(__fdiv_rn(v, wsf));
     }
 }
@@ -178,7 +181,8 @@ extern "C" int64_t arctopk_sparse_workspace_bytes(int32_t nt, const int64_t* num
 
 extern "C" int arctopk_topk_select(const void* x, int32_t nt, const int64_t* offsets,
                                    const int64_t* numels, const int64_t* ks, const int64_t* k_off,
-                                   int32_t* idx, void* vals, void* workspace, int32_t dtype, void* stream) {
+                                   int32_t* idx, void* vals, void* workspace, int32_t dtype,
+                                   int32_t zero_selected, void* stream) {
     if (!x || !offsets || !numels || !ks || !k_off || !idx || !vals || !workspace || nt < 1)
         return ARCTOPK_EINVAL;
     if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
@@ -206,7 +210,7 @@ extern "C" int arctopk_topk_select(const void* x, int32_t nt, const int64_t* off
             maxn = std::max(maxn, numels[j]);
         }
         int e = arctopk::ms_select(b, maxn, nullptr, x, dtype == ARCTOPK_BF16, false, ws, cap_total, idx, vals,
-                                   nullptr, st);
+                                   nullptr, zero_selected ? const_cast<void*>(x) : nullptr, st);
         if (e) return e;
     }
     return 0;
@@ -313,15 +317,19 @@ int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, c
             dim3 grid(grid_for(maxk, 2048), cnt);
             const int32_t* iq = idx + (int64_t)q * packed_len;
             const T* vq = vals + (int64_t)q * packed_len;
-            if (accumulate)
-                hipLaunchKernelGGL((k_scatter<T, true>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
+            if (accumulate && q > 0)
+                hipLaunchKernelGGL((k_scatter<T, 1>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
+            else if (accumulate)
+                hipLaunchKernelGGL((k_scatter<T, 2>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
             else
-                hipLaunchKernelGGL((k_scatter<T, false>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
+                hipLaunchKernelGGL((k_scatter<T, 0>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
         }
     }
-    if (accumulate || gerr) {
+    // TopK's out /= ws (sparse_hook.py:293) is the identity at ws = 1 (x / 1 == x for every x)
+    const bool div = accumulate && world_size > 1;
+    if (div || gerr) {
         hipLaunchKernelGGL(k_div_gE<T>, dim3(grid_for(numel, 8192)), dim3(256), 0, st, out, gerr,
-                           numel, wsf, accumulate);
+                           numel, wsf, div ? 1 : 0);
     }
     return (int)hipGetLastError();
 }

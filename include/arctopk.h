@@ -224,11 +224,14 @@ int64_t arctopk_sparse_workspace_bytes(int32_t ntensors, const int64_t* numels);
  * k-th |x|: lowest index first.  Writes each tensor's k indices ascending as int32
  * (idx[k_off[i] ..]) and the values x[idx] (vals[k_off[i] ..]).
  * Replaces: torch.topk(tensor.abs(), k, sorted=False), .to(int32), tensor[indices]
- * (sparse_hook.py:26-28, :97-98).
+ * (sparse_hook.py:26-28, :97-98).  zero_selected = 1: x (non-const here) is also written
+ * back with its selected elements zeroed, in the same pass (EF14's `tensor[indices] = 0`,
+ * :104, when x is the residual E after arctopk_ef14_fold).
  */
 int arctopk_topk_select(const void* x, int32_t ntensors, const int64_t* offsets,
                         const int64_t* numels, const int64_t* ks, const int64_t* k_off,
-                        int32_t* idx, void* vals, void* workspace, int32_t dtype, void* stream);
+                        int32_t* idx, void* vals, void* workspace, int32_t dtype,
+                        int32_t zero_selected, void* stream);
 
 /*
  * RandK index source, device-side: idx[k_off[i] + j] = pi_i(j) for j < k, where pi_i is
@@ -276,6 +279,16 @@ int arctopk_sparse_decode(void* out, int64_t numel, int32_t ntensors, const int6
  */
 int arctopk_ef_apply(void* x, void* E, int64_t numel, int32_t ef, int32_t err_in, int32_t dtype,
                      void* stream);
+
+/*
+ * EF14 fold for the sparse hooks: E := x + E (err_in = 1) or E := x (first call); x is not
+ * written.  The caller then selects / gathers from E (which holds the pre-compression
+ * bucket) and decodes into x.  Replaces input_tensor.add_(E) (sparse_hook.py:205) and the
+ * full-bucket E.copy_(input_tensor) (:258).  With arctopk_topk_select(..., zero_selected=1)
+ * on E, the EF14 residual `E[indices] = 0` (:104) is done in the select's last pass.
+ */
+int arctopk_ef14_fold(const void* x, void* E, int64_t numel, int32_t err_in, int32_t dtype,
+                      void* stream);
 
 /*
  * Device projections of one bucket call: for every SKETCH segment in bucket order,

@@ -65,7 +65,7 @@ sk_val = torch.empty(sum(ks), device=dev)
 wsb = torch.empty(int(L.arctopk_sparse_workspace_bytes(len(ks), N.i64_array(numel_t))), dtype=torch.uint8, device=dev)
 KS = sum(ks)
 variants["sparse ef_apply ef14"] = (lambda: L.arctopk_ef_apply(a.data_ptr(), b.data_ptr(), n, N.EF14, 1, 0, s), 12 * n)
-variants["topk_select (16 tensors)"] = (lambda: L.arctopk_topk_select(G.data_ptr(), nt, A_off, A_n, A_k, A_ko, sk_idx.data_ptr(), sk_val.data_ptr(), wsb.data_ptr(), 0, s), 4 * 5 * n + 8 * KS)
+variants["topk_select (16 tensors)"] = (lambda: L.arctopk_topk_select(G.data_ptr(), nt, A_off, A_n, A_k, A_ko, sk_idx.data_ptr(), sk_val.data_ptr(), wsb.data_ptr(), 0, 0, s), 4 * 5 * n + 8 * KS)
 variants["randk_indices hash"] = (lambda: L.arctopk_randk_indices(nt, A_n, A_k, A_ko, 7, sk_idx.data_ptr(), s), 4 * KS)
 variants["sparse_gather"] = (lambda: L.arctopk_sparse_gather(G.data_ptr(), nt, A_off, A_k, A_ko, sk_idx.data_ptr(), sk_val.data_ptr(), 0, s), 12 * KS)
 variants["sparse_residual ef14"] = (lambda: L.arctopk_sparse_residual(b.data_ptr(), nt, A_off, A_k, A_ko, sk_idx.data_ptr(), sk_val.data_ptr(), N.EF14, 0, s), 8 * KS)

@@ -28,7 +28,7 @@ for label, numel_t, gen in [("topk 16x4M randn", [4 << 20] * 16, lambda n: torch
     wsb = torch.zeros(nb, dtype=torch.uint8, device=dev)
     N.check(L.arctopk_topk_select(X.data_ptr(), len(ks), N.i64_array(offs), N.i64_array(numel_t),
                                   N.i64_array(ks), N.i64_array(kof), idx.data_ptr(), val.data_ptr(),
-                                  wsb.data_ptr(), 0, s), "topk_select")
+                                  wsb.data_ptr(), 0, 0, s), "topk_select")
     torch.cuda.synchronize()
     w = wsb.cpu().numpy().tobytes()
     print("==", label, "workspace", nb)

@@ -37,6 +37,6 @@ wsb = torch.empty(int(L.arctopk_sparse_workspace_bytes(len(ks), N.i64_array(nume
 for _ in range(REPS):
     N.check(L.arctopk_topk_select(X.data_ptr(), len(ks), N.i64_array(offs), N.i64_array(numel_t),
                                   N.i64_array(ks), N.i64_array(kof), idx.data_ptr(), val.data_ptr(),
-                                  wsb.data_ptr(), 0, s), "topk_select")
+                                  wsb.data_ptr(), 0, 0, s), "topk_select")
 torch.cuda.synchronize()
 print("done")

@@ -72,7 +72,7 @@ def test_topk_select_kernel_ties_and_order():
     st = torch.cuda.current_stream().cuda_stream
     N.check(L.arctopk_topk_select(xd.data_ptr(), 1, N.i64_array([0]), N.i64_array([n]),
                                   N.i64_array([k]), N.i64_array([0]), idx.data_ptr(),
-                                  vals.data_ptr(), ws.data_ptr(), 0, st), "topk_select")
+                                  vals.data_ptr(), ws.data_ptr(), 0, 0, st), "topk_select")
     torch.cuda.synchronize()
     i = idx.cpu().long()
     assert torch.all(i[1:] > i[:-1])
@@ -84,7 +84,7 @@ def test_topk_select_kernel_ties_and_order():
     vals2 = torch.empty(k2, device=DEV)
     N.check(L.arctopk_topk_select(xd.data_ptr(), 1, N.i64_array([0]), N.i64_array([n]),
                                   N.i64_array([k2]), N.i64_array([0]), idx2.data_ptr(),
-                                  vals2.data_ptr(), ws.data_ptr(), 0, st), "topk_select")
+                                  vals2.data_ptr(), ws.data_ptr(), 0, 0, st), "topk_select")
     torch.cuda.synchronize()
     assert check_rows_tie_aware(idx2.cpu(), x.abs(), k2, band=0.0) == 0
 
@@ -115,7 +115,7 @@ def test_topk_select_degenerate_large(case):
     st = torch.cuda.current_stream().cuda_stream
     N.check(L.arctopk_topk_select(xd.data_ptr(), 2, N.i64_array([0, n]), N.i64_array(numels),
                                   N.i64_array(ks), N.i64_array([0, k]), idx.data_ptr(),
-                                  vals.data_ptr(), ws.data_ptr(), 0, st), "topk_select")
+                                  vals.data_ptr(), ws.data_ptr(), 0, 0, st), "topk_select")
     torch.cuda.synchronize()
     i = idx.cpu().long()
     xa = xd.cpu()
