@@ -2035,7 +2035,30 @@ __global__ void __launch_bounds__(256) k_ef_apply(float* __restrict__ x, float* 
     const int64_t n4 = n >> 2;
     float4* x4 = reinterpret_cast<float4*>(x);
     float4* e4 = reinterpret_cast<float4*>(E);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+    constexpr bool kReadE = EF == ARCTOPK_EF21 || (EF == ARCTOPK_EF14 && ERR_IN);
+    // U quads per lane in flight, nontemporal streams (the bucket is touched once here)
+    constexpr int U = 4;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        float4 g[U], e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            g[u] = ld_stream(x4 + i + u * stride);
+            if constexpr (kReadE) e[u] = ld_stream(e4 + i + u * stride);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float4 v = g[u];
+            if constexpr (EF == ARCTOPK_EF14 && ERR_IN) {
+                v.x += e[u].x; v.y += e[u].y; v.z += e[u].z; v.w += e[u].w;
+            } else if constexpr (EF == ARCTOPK_EF21) {
+                v.x -= e[u].x; v.y -= e[u].y; v.z -= e[u].z; v.w -= e[u].w;
+            }
+            if constexpr (EF == ARCTOPK_EF14) st_stream(e4 + i + u * stride, v);
+            if constexpr ((EF != ARCTOPK_EF14 || ERR_IN) && WRITE_X) st_stream(x4 + i + u * stride, v);
+        }
+    }
+    for (; i < n4; i += stride) {
         const float4 v = ef_apply4<EF, ERR_IN>(x4, e4, i);
         if constexpr (EF == ARCTOPK_EF14) e4[i] = v;
         if constexpr ((EF != ARCTOPK_EF14 || ERR_IN) && WRITE_X) x4[i] = v;

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "common.h"
 #include "mselect.h"
@@ -114,6 +115,61 @@ __global__ void __launch_bounds__(256) k_scatter(SparseBatch b, T* __restrict__ 
         else if constexpr (MODE == 2) os[i] = from_f<T>(0.f + v);
         else os[i] = from_f<T>(__fdiv_rn(v, wsf));
     }
+}
+
+// TopK's first payload (rank 0) into the bucket, zero fill included: each block composes a
+// 4096-element chunk of one tensor in LDS (zeros, then 0 + v at the payload's indices that
+// fall in the chunk) and writes it whole.  The payload's indices are ascending per tensor
+// (arctopk_topk_select), so the chunk's slice of them is found by two 64-way searches.
+// Replaces the bucket memset + a scattered read-modify-write pass.
+constexpr int kDecChunk = 4096;
+
+// first position in a[lo, hi) with a[p] >= target (a ascending), one wave
+__device__ __forceinline__ int64_t wave_lower_bound(const int32_t* __restrict__ a, int64_t lo, int64_t hi,
+                                                    int32_t target) {
+    const int lane = threadIdx.x & 63;
+    while (hi - lo > 64) {
+        const int64_t step = (hi - lo + 63) / 64;
+        const int64_t p = lo + (int64_t)lane * step;
+        const bool pred = p < hi && a[p] < target;
+        const int c = __popcll(__ballot(pred));
+        if (c == 0) return lo;
+        const int64_t nlo = lo + (int64_t)(c - 1) * step + 1;
+        const int64_t phi = lo + (int64_t)c * step;
+        hi = phi < hi ? phi : hi;
+        lo = nlo;
+    }
+    const int64_t p = lo + lane;
+    return lo + __popcll(__ballot(p < hi && a[p] < target));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_scatter_first(SparseBatch b, T* __restrict__ out,
+                                                       const int32_t* __restrict__ idx,
+                                                       const T* __restrict__ vals) {
+    using arctopk::from_f;
+    using arctopk::to_f;
+    __shared__ T chunk[kDecChunk];
+    __shared__ int64_t s_lb[2];
+    const int t = blockIdx.y;
+    const int64_t n = b.n[t];
+    const int64_t c0 = (int64_t)blockIdx.x * kDecChunk;
+    if (c0 >= n) return;
+    const int64_t c1 = min<int64_t>(n, c0 + kDecChunk);
+    const int32_t* it = idx + b.koff[t];
+    const T* vt = vals + b.koff[t];
+    const int wave = threadIdx.x >> 6;
+    if (wave < 2) {
+        const int64_t lb = wave_lower_bound(it, 0, b.k[t], (int32_t)(wave == 0 ? c0 : c1));
+        if ((threadIdx.x & 63) == 0) s_lb[wave] = lb;
+    }
+    for (int e = threadIdx.x; e < kDecChunk; e += 256) chunk[e] = from_f<T>(0.f);
+    __syncthreads();
+    for (int64_t j = s_lb[0] + threadIdx.x; j < s_lb[1]; j += 256)
+        chunk[it[j] - c0] = from_f<T>(0.f + to_f(vt[j]));
+    __syncthreads();
+    T* o = out + b.off[t] + c0;
+    for (int64_t e = threadIdx.x; e < c1 - c0; e += 256) o[e] = chunk[e];
 }
 
 template <typename T>
@@ -303,11 +359,33 @@ template <typename T>
 int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, const int64_t* ks,
                     const int64_t* k_off, int64_t packed_len, const int32_t* idx, const T* vals,
                     int32_t nranks, int32_t world_size, int32_t accumulate, T* gerr, hipStream_t st) {
-    hipError_t he = hipMemsetAsync(out, 0, (size_t)numel * sizeof(T), st);
-    if (he != hipSuccess) return (int)he;
+    // TopK (accumulate, ascending indices per tensor): rank 0's payload writes the whole
+    // bucket, zeros included (k_scatter_first); the tensors tile the bucket in order
+    bool tiled = accumulate != 0;
+    for (int32_t i = 0; tiled && i < nt; ++i) {
+        const int64_t end = i + 1 < nt ? offsets[i + 1] : numel;
+        if (offsets[i] < 0 || end <= offsets[i] || end - offsets[i] >= (1ll << 31) || (i == 0 && offsets[0] != 0))
+            tiled = false;
+    }
+    if (!tiled) {
+        hipError_t he = hipMemsetAsync(out, 0, (size_t)numel * sizeof(T), st);
+        if (he != hipSuccess) return (int)he;
+    } else {
+        std::vector<int64_t> numels(nt);
+        for (int32_t i = 0; i < nt; ++i) numels[i] = (i + 1 < nt ? offsets[i + 1] : numel) - offsets[i];
+        for (int32_t first = 0; first < nt; first += kB) {
+            SparseBatch b;
+            int64_t maxn, maxk;
+            const int cnt = std::min<int32_t>(kB, nt - first);
+            int e = fill_batch(b, first, cnt, offsets, numels.data(), ks, k_off, maxn, maxk);
+            if (e) return e;
+            const dim3 grid((unsigned)((maxn + kDecChunk - 1) / kDecChunk), cnt);
+            hipLaunchKernelGGL(k_scatter_first<T>, grid, dim3(256), 0, st, b, out, idx, vals);
+        }
+    }
     const float wsf = (float)world_size;
     const int nr = accumulate ? nranks : 1;
-    for (int q = 0; q < nr; ++q) {
+    for (int q = tiled ? 1 : 0; q < nr; ++q) {
         for (int32_t first = 0; first < nt; first += kB) {
             SparseBatch b;
             int64_t maxn, maxk;
