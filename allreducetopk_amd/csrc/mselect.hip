@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "mselect.h"
 
@@ -558,7 +559,14 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
     }
     uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
     uint32_t* cidx = ckey + cap_total;
-    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(kMHistBlocks, (maxn + 8191) / 8192));
+    // histogram blocks per item: every block merges its LDS histogram with memory-side
+    // atomics on the same hot words, so the batch's total is capped (tuning switch)
+    static const int64_t hist_total = [] {
+        const char* env = std::getenv("ARCTOPK_TOPK_HIST_BLOCKS");
+        return env ? std::max(1, std::atoi(env)) : 1024;  // headline TopK: 387 -> 404 GB/s (512: 399, 2048: 387)
+    }();
+    const int hb = (int)std::max<int64_t>(
+        1, std::min<int64_t>(std::min<int64_t>(kMHistBlocks, (maxn + 8191) / 8192), hist_total / cnt));
     const dim3 gh(hb, cnt), gt(gr, cnt), gflat(total_ranges(b));
 #define MS_LAUNCH(FF, AR)                                                                              \
     do {                                                                                               \
