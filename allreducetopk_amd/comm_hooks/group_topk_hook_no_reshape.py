@@ -570,9 +570,10 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
     nplan.prestaged = (seed, i)
 
 
-# light samples alternate between the whole hook (start .. decode end) and the encode
-# kernel alone (after the V draw .. after encode): two markers per sampled call
-_LIGHT_MARKS = (frozenset(("start", "decode")), frozenset(("draw", "encode")))
+# light samples alternate between a marker after the decode (the device timeline between
+# two of them, several calls apart, gives the hook's device time per call) and the encode
+# kernel alone (after the V draw .. after encode)
+_LIGHT_MARKS = (frozenset(("decode",)), frozenset(("draw", "encode")))
 
 
 def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
@@ -859,7 +860,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             evs = {}
             state.phase_events.append(evs)
         elif state.hook_events is not None and state.hook_event_every and c % state.hook_event_every == 0:
-            evs, light = {}, _LIGHT_MARKS[(c // state.hook_event_every) % 2]
+            evs, light = {"_call": c}, _LIGHT_MARKS[(c // state.hook_event_every) % 2]
             state.hook_events.append(evs)
 
     def mark(name, on=None):
