@@ -49,10 +49,12 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4):
     """
     from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import _geometry
     n_el = bucket_numel(shapes)
-    k_el = sk = vbytes = 0
+    k_el = sk = vbytes = rows = k_rows = 0
     for s_ in shapes:
         kind, n, m = _geometry(s_)
         k_el += max(1, int(n * ratio)) * m
+        rows += n
+        k_rows += max(1, int(n * ratio))
         sk += eb * n * (1 if m == 1 and len(s_) == 1 else r)
         vbytes += 0 if len(s_) == 1 else m * r * eb
     if ef == "noef":
@@ -70,7 +72,9 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4):
         pack = 4 * eb * k_el  # read G, E rows; write packed, E rows
         dec = eb * (2 * k_el + 2 * n_el)  # packed, gE, out, gE rows
         read = 2 * eb * n_el + vbytes + sk + 2 * eb * k_el + eb * (k_el + n_el)
-    sel = 2 * sk
+    # select: read the sketch once; write the slot map (int32 per row) and the row list
+    # (int32 per selected row)
+    sel = sk + 4 * rows + 4 * k_rows
     return dict(encode=enc, select=sel, pack=pack, decode=dec, total=enc + sel + pack + dec,
                 read=read)
 
