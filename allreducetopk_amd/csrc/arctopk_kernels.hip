@@ -1159,6 +1159,10 @@ __device__ __forceinline__ uint32_t blk_exscan_u32(uint32_t v, uint32_t* lds, ui
 // (compact pass) these become per-range T-equal allowances (lowest ranges first) and
 // output offsets for ms_arc_write.  No atomics outside LDS histograms.
 constexpr int kRefineThreads = 1024;
+#ifndef ARCTOPK_REFINE_PRE
+#define ARCTOPK_REFINE_PRE 64  // tuning switch (A/B builds): candidates per range loaded up front, 64 or 128
+#endif
+constexpr int kRefinePre = ARCTOPK_REFINE_PRE;
 static_assert(kRefineThreads == kMMaxRanges, "one range per thread in the offset scan");
 __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspace* ws,
                                                 const uint32_t* __restrict__ ckey,
@@ -1174,17 +1178,27 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     // one round trip for everything independent: the state, the per-range counts, and the
     // first 64 candidate slots of each range this wave copies (a range's region is fixed;
     // its count only masks them)
-    MState s = ws->st[t];
+    MState s = ws->st[t];  // the first-pass bin (compact launch / key pass)
     const int nr = it.nranges;
-    const uint32_t gt_above = tid < nr ? ws->cnt_gt[t][tid] : 0u;  // keys above the bin
-    const uint32_t my_cnt = tid < nr ? ws->cnt_cand[t][tid] : 0u;
-    uint32_t v[RB];
+    // loaded for every thread (NT == kMMaxRanges: in bounds) so that they need not wait for
+    // `it`; entries past nr are masked below
+    const uint32_t gt_raw = ws->cnt_gt[t][tid], cnt_raw = ws->cnt_cand[t][tid];
+    uint32_t v[RB];  // candidate slots lane and lane + 64 of each range
+    [[maybe_unused]] uint32_t v2[RB];
 #pragma unroll
     for (int q = 0; q < RB; ++q) {
         const int r = wave + q * NW;
-        const int64_t cap = r < nr ? min<int64_t>(64, it.n - (int64_t)r * it.range) : 0;  // region bound
+        const int64_t cap = r < nr ? min<int64_t>(kRefinePre, it.n - (int64_t)r * it.range) : 0;  // region bound
         v[q] = lane < cap ? src[(int64_t)r * it.range + lane] : 0u;
+        if constexpr (kRefinePre > 64) v2[q] = lane + 64 < cap ? src[(int64_t)r * it.range + 64 + lane] : 0u;
     }
+    if constexpr (kArcLocalDigit) {
+        // every reader of the key pass's histogram (the compact launch) is done: zero it for
+        // the next key pass
+        for (int i = tid; i < kMBins; i += NT) ws->hist[t][i] = 0u;
+    }
+    const uint32_t gt_above = tid < nr ? gt_raw : 0u;  // keys above the bin
+    const uint32_t my_cnt = tid < nr ? cnt_raw : 0u;
     uint32_t nc32;
     const uint32_t my_off = blk_exscan_u32<NW>(my_cnt, lds, &nc32);
     roff[tid] = my_off;
@@ -1203,15 +1217,17 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     };
     const bool staged = nc <= kRefineLdsCap;
     if (staged) {
-        // usual case: wave w copies ranges w, w + NW, ..., lane j candidate j of each (the
-        // first RB ranges' first 64 candidates are already in registers; longer ranges and
-        // ranges past NW * RB load here), then everything is read from LDS
+        // usual case: wave w copies ranges w, w + NW, ..., lane j candidates j and j + 64 of
+        // each (the first RB ranges' first 128 candidates are already in registers; longer
+        // ranges and ranges past NW * RB load here), then everything is read from LDS
         for (int r0 = wave; r0 < nr; r0 += NW * RB) {
             if (r0 != wave) {
 #pragma unroll
                 for (int q = 0; q < RB; ++q) {
                     const int r = r0 + q * NW;
-                    v[q] = (r < nr && (uint32_t)lane < rcnt[r]) ? src[(int64_t)r * it.range + lane] : 0u;
+                    const uint32_t c = r < nr ? rcnt[r] : 0u;
+                    v[q] = (uint32_t)lane < c ? src[(int64_t)r * it.range + lane] : 0u;
+                    if constexpr (kRefinePre > 64) v2[q] = (uint32_t)lane + 64 < c ? src[(int64_t)r * it.range + 64 + lane] : 0u;
                 }
             }
 #pragma unroll
@@ -1220,7 +1236,8 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
                 if (r < nr) {
                     const uint32_t c = rcnt[r], o = roff[r];
                     if ((uint32_t)lane < c) stage[o + lane] = v[q];
-                    for (uint32_t j = 64 + lane; j < c; j += 64) stage[o + j] = src[(int64_t)r * it.range + j];
+                    if constexpr (kRefinePre > 64) if ((uint32_t)lane + 64 < c) stage[o + 64 + lane] = v2[q];
+                    for (uint32_t j = kRefinePre + lane; j < c; j += 64) stage[o + j] = src[(int64_t)r * it.range + j];
                 }
             }
         }
@@ -1339,8 +1356,10 @@ struct KeysGrid {
 
 // Larger segments: energy keys into global memory, fused with the first radix pass of
 // the multi-block select (mselect.h): each block histograms its keys' top 12 bits in LDS
-// and merges the non-empty bins into the segment's global histogram; the last block to
-// finish picks the bin holding the k-th largest key (ms_arc_first_digit).
+// and merges the non-empty bins into the segment's global histogram.  The bin holding the
+// k-th largest key is then derived from that histogram by each block of the next launches
+// (ms_arc_digit_local; with ARCTOPK_ARC_LOCAL_DIGIT=0, by this kernel's last block:
+// ms_arc_first_digit).
 template <typename T, int KT>
 __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs,
                                                   const int32_t* __restrict__ ids, int first,
@@ -1441,11 +1460,15 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
             if (h[i]) atomicAdd(&ws->hist[t][hist_slot(i)], h[i]);
     }
     DIAG_STAMP(g_st_keys, 2);
+    if constexpr (kArcLocalDigit) {  // the compact and refine blocks derive the digit themselves
+        DIAG_STAMP(g_st_keys, 3);
+        return;
+    }
     if (!ms_arrive_last(&ws->done[t].v, nblk)) {
         DIAG_STAMP(g_st_keys, 3);
         return;
     }
-    ms_arc_first_digit<KT>(ws, t, s.k_rows);
+    ms_arc_first_digit<KT>(ws, t, s.k_rows, h);
     DIAG_STAMP(g_st_keys, 3);
 }
 

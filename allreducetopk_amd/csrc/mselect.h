@@ -104,6 +104,20 @@ __device__ inline uint32_t ms_take(uint32_t* p) {  // read-and-clear at the memo
     return __hip_atomic_exchange(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Read-and-clear bins [0, nb) of item t's global histogram into lds_h[bin] (nb a power of
+// two <= kMBins; all threads of the block; the caller syncs before reading lds_h).  The
+// atomics walk the histogram in slot order, so a wave instruction covers whole 128-B lines
+// (bin order puts every lane on a line of its own: memory-side atomics then run ~17x
+// slower, which made this read-back the longest step of the last block).
+__device__ inline void ms_take_hist(MWorkspace* ws, int t, int nb, uint32_t* lds_h) {
+    const int g = nb >= 128 ? nb >> 7 : 1;  // bins per 128-B line
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) {
+        const int line = j / g, q = j - line * g;
+        const int bin = nb >= 128 ? q * 128 + line : j;
+        lds_h[bin] = ms_take(&ws->hist[t][(line << 5) | q]);
+    }
+}
+
 // Start state of item t (all threads of one block): histogram cleared, the keys' common
 // leading bits decided (kor / kand = OR / AND of all keys; TopK: |x| keys, kor = ~0).
 __device__ inline void ms_init_item(MWorkspace* ws, int t, int64_t k, uint32_t kor, uint32_t kand) {
@@ -133,15 +147,16 @@ __device__ inline void ms_init_item(MWorkspace* ws, int t, int64_t k, uint32_t k
 // (cand_cap = n for ARC items: every key of the bin fits).
 constexpr int kArcShift = 31 - 12;
 template <int NT>
-__device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k) {
+__device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k, uint32_t* lds_h /* kMBins */) {
     __shared__ uint32_t s_w[NT / 64], s_d, s_acc;
     constexpr int PER = kMBins / NT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    ms_take_hist(ws, t, kMBins, lds_h);
+    __syncthreads();
     uint32_t c[PER], sum = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-        const int bin = kMBins - 1 - (tid * PER + q);  // descending
-        c[q] = ms_take(&ws->hist[t][hist_slot(bin)]);
+        c[q] = lds_h[kMBins - 1 - (tid * PER + q)];  // descending
         sum += c[q];
     }
     uint32_t incl = sum;
@@ -179,6 +194,79 @@ __device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k) {
         ws->ncand[t].v = 0;
     }
 }
+
+// The same first-pass digit derived by every ARC compact block from the merged histogram
+// that an EARLIER launch (the key pass) finished, with plain loads: this takes the
+// last-block hand-off (arrival counter + read-back, ~4.5 us of serial tail) out of the key
+// pass.  Two levels over the slot layout (slot L*32 + g holds bin g*128 + L): with NT a
+// multiple of 32, thread tid's PER slots all belong to bin group g = tid & 31, so group
+// totals need no transposition; wave 0 picks the group holding the k-th largest key, then
+// the bin inside it from that group's 128 counts.  lds: NT + 128 words.  Returns the bin d
+// and the keys above it (acc); all NT threads.
+template <int NT>
+__device__ inline void ms_arc_digit_local(const uint32_t* __restrict__ hist_t, int64_t k, uint32_t* lds,
+                                          uint32_t* d_out, uint32_t* acc_out) {
+    static_assert(NT % 64 == 0 && kMBins % NT == 0 && kMBins == 32 * 128, "slot layout");
+    constexpr int PER = kMBins / NT;  // slots per thread
+    constexpr int SUB = NT / 32;      // threads per bin group
+    __shared__ uint32_t s_g, s_acc, s_d, s_acc2;
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        c[q] = hist_t[q * NT + tid];  // coalesced: slot q * NT + tid
+        sum += c[q];
+    }
+    lds[tid] = sum;
+    __syncthreads();
+    if (tid < 64) {  // lane j < 32: group 31 - j (descending bins)
+        uint32_t tot = 0;
+        if (lane < 32)
+            for (int j = 0; j < SUB; ++j) tot += lds[(31 - lane) + 32 * j];
+        uint32_t incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const uint64_t excl = incl - tot;
+        if (lane < 32 && excl < (uint64_t)k && excl + tot >= (uint64_t)k) {
+            s_g = (uint32_t)(31 - lane);
+            s_acc = (uint32_t)excl;
+        }
+    }
+    __syncthreads();
+    const uint32_t g = s_g;
+    if ((uint32_t)(tid & 31) == g) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) lds[NT + q * SUB + (tid >> 5)] = c[q];  // lds[NT + L]
+    }
+    __syncthreads();
+    if (tid < 64) {  // lane j: L = 127 - 2j, 126 - 2j
+        const uint32_t a0 = lds[NT + 127 - 2 * lane], a1 = lds[NT + 126 - 2 * lane];
+        const uint32_t two = a0 + a1;
+        uint32_t incl = two;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const uint64_t excl = (uint64_t)s_acc + incl - two;
+        if (excl < (uint64_t)k && excl + two >= (uint64_t)k) {
+            const bool first = excl + a0 >= (uint64_t)k;
+            s_d = g * 128u + (uint32_t)(first ? 127 - 2 * lane : 126 - 2 * lane);
+            s_acc2 = (uint32_t)(first ? excl : excl + a0);
+        }
+    }
+    __syncthreads();
+    *d_out = s_d;
+    *acc_out = s_acc2;
+}
+
+#ifndef ARCTOPK_ARC_LOCAL_DIGIT
+#define ARCTOPK_ARC_LOCAL_DIGIT 1  // tuning switch (A/B builds): 0 = the key pass's last block picks the digit
+#endif
+constexpr bool kArcLocalDigit = ARCTOPK_ARC_LOCAL_DIGIT != 0;
 
 // host-side geometry of one item: fills range / nranges / cand_cap (cand_off by caller)
 void ms_item_geometry(MItem& it);

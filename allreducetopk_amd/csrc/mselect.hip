@@ -156,12 +156,14 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
     // ---- last block: digit of the kk-th largest key (bins scanned from the top)
     const int nb = 1 << w;
     const int per = (nb + 255) / 256;
+    ms_take_hist(ws, t, nb, h);  // h is free: the merge above read it before the arrival's barrier
+    __syncthreads();
     uint32_t c[PER];
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int bin = nb - 1 - ((int)threadIdx.x * per + q);
-        c[q] = (q < per && bin >= 0) ? ms_take(&ws->hist[t][hist_slot(bin)]) : 0u;
+        c[q] = (q < per && bin >= 0) ? h[bin] : 0u;
         sum += c[q];
     }
     uint32_t total;
@@ -268,7 +270,28 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
     int t, r;
     if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
-    const MState s = ws->st[t];
+    MState s;
+    if constexpr (kArcLocalDigit) {
+        __shared__ uint32_t lds_d[256 + 128];
+        uint32_t d, acc;
+        ms_arc_digit_local<256>(ws->hist[t], it.k, lds_d, &d, &acc);
+        s.p1 = d << kArcShift;
+        s.m1 = ~((1u << kArcShift) - 1u);
+        if (r == 0 && threadIdx.x == 0) {  // the item's state for the refine (next launch)
+            MState g;
+            g.prefix = s.p1;
+            g.mask = s.m1;
+            g.bit = kArcShift;
+            g.cand = 1;
+            g.kk = it.k - (int64_t)acc;
+            g.p1 = s.p1;
+            g.m1 = s.m1;
+            g.ncand = 0;
+            ws->st[t] = g;
+        }
+    } else {
+        s = ws->st[t];
+    }
     const uint32_t hi = s.p1 | ~s.m1;  // largest key of the bin
     const int64_t r0 = (int64_t)r * it.range;
     const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
@@ -378,12 +401,19 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
 
     // ---- last block: offsets over the item's ranges (4 consecutive ranges per thread)
     const int nr = it.nranges;
+    // read-and-clear in range order (contiguous lines per wave instruction), then regroup
+    __shared__ uint32_t s_eq[kMMaxRanges], s_gt[kMMaxRanges];
+    for (int r = threadIdx.x; r < nr; r += 256) {
+        s_eq[r] = ms_take(&ws->cnt_eq[t][r]);
+        s_gt[r] = ms_take(&ws->cnt_gt[t][r]);
+    }
+    __syncthreads();
     uint32_t eq[4], gt[4], se = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int r = threadIdx.x * 4 + q;
-        eq[q] = r < nr ? ms_take(&ws->cnt_eq[t][r]) : 0u;
-        gt[q] = r < nr ? ms_take(&ws->cnt_gt[t][r]) : 0u;
+        eq[q] = r < nr ? s_eq[r] : 0u;
+        gt[q] = r < nr ? s_gt[r] : 0u;
         se += eq[q];
     }
     uint32_t tot;
