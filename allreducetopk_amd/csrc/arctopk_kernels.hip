@@ -1150,6 +1150,115 @@ __device__ __forceinline__ uint32_t blk_exscan_u32(uint32_t v, uint32_t* lds, ui
     return before + x - v;
 }
 
+// LDS histogram add, all lanes of the wave (contrib: the lane adds to `bin`).  The lanes
+// sharing the first contributing lane's bin add once for all: candidates of a degenerate bin
+// (e.g. tied all-zero rows) all hit one word, and one-lane-at-a-time LDS atomics on it
+// serialised the radix rounds (~90 us for a Llama embedding with 90 % zero rows).
+__device__ __forceinline__ void hist_add_wave(uint32_t* h, uint32_t bin, bool contrib) {
+    const uint64_t bm = __ballot(contrib);
+    if (!bm) return;
+    const int leader = __ffsll((long long)bm) - 1;
+    const uint32_t lb = __shfl(bin, leader, 64);
+    const uint64_t same = __ballot(contrib && bin == lb);
+    if ((int)(threadIdx.x & 63) == leader) atomicAdd(&h[lb], (uint32_t)__popcll(same));
+    if (contrib && bin != lb) atomicAdd(&h[bin], 1u);
+}
+
+// Decide at once the undecided bits that every candidate shares (kor / kand: OR / AND of the
+// candidates, which all match s's prefix): a bin of tied keys (all-zero rows) then needs no
+// radix round at all, and s.bit == 0 means every candidate equals the threshold.
+__device__ __forceinline__ void decide_common_bits(MState& s, uint32_t kor, uint32_t kand) {
+    const uint32_t diff = kor ^ kand;
+    const int hb = diff ? 32 - __clz(diff) : 0;
+    if (hb < s.bit) {
+        const uint32_t above = s.bit >= 32 ? ~0u : ((1u << s.bit) - 1u);
+        const uint32_t bits = above & ~((1u << hb) - 1u);  // [hb, s.bit)
+        s.prefix |= kand & bits;
+        s.mask |= bits;
+        s.bit = hb;
+    }
+}
+
+// two exclusive block scans plus a block-wide OR / AND (kor, kand in place), one pair of
+// barriers (lds: 4 * NW words)
+template <int NW>
+__device__ __forceinline__ void blk_exscan2_or_and(uint32_t a, uint32_t b, uint32_t& kor, uint32_t& kand,
+                                                   uint32_t* lds, uint32_t* ea, uint32_t* eb, uint32_t* ta,
+                                                   uint32_t* tb) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = a, y = b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t xo = __shfl_up(x, o, 64), yo = __shfl_up(y, o, 64);
+        if (lane >= o) {
+            x += xo;
+            y += yo;
+        }
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 63) {
+        lds[wave] = x;
+        lds[NW + wave] = y;
+        lds[2 * NW + wave] = kor;
+        lds[3 * NW + wave] = kand;
+    }
+    __syncthreads();
+    uint32_t bx = 0, by = 0, sx = 0, sy = 0, o_ = 0u, a_ = ~0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint32_t vx = lds[w], vy = lds[NW + w];
+        bx += w < wave ? vx : 0u;
+        by += w < wave ? vy : 0u;
+        sx += vx;
+        sy += vy;
+        o_ |= lds[2 * NW + w];
+        a_ &= lds[3 * NW + w];
+    }
+    __syncthreads();
+    *ea = bx + x - a;
+    *eb = by + y - b;
+    *ta = sx;
+    *tb = sy;
+    kor = o_;
+    kand = a_;
+}
+
+// two exclusive block scans with one pair of barriers (lds: 2 * NW words)
+template <int NW>
+__device__ __forceinline__ void blk_exscan_u32x2(uint32_t a, uint32_t b, uint32_t* lds, uint32_t* ea,
+                                                 uint32_t* eb, uint32_t* ta, uint32_t* tb) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = a, y = b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t xo = __shfl_up(x, o, 64), yo = __shfl_up(y, o, 64);
+        if (lane >= o) {
+            x += xo;
+            y += yo;
+        }
+    }
+    if (lane == 63) {
+        lds[wave] = x;
+        lds[NW + wave] = y;
+    }
+    __syncthreads();
+    uint32_t bx = 0, by = 0, sx = 0, sy = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const uint32_t vx = lds[w], vy = lds[NW + w];
+        bx += w < wave ? vx : 0u;
+        by += w < wave ? vy : 0u;
+        sx += vx;
+        sy += vy;
+    }
+    __syncthreads();
+    *ea = bx + x - a;
+    *eb = by + y - b;
+    *ta = sx;
+    *tb = sy;
+}
+
 // ARC refine of one large segment (after ms_arc_compact), one 1024-thread block.  Range r's
 // candidates (every key of the first-pass bin in that range, in index order) sit in its
 // own region of the candidate list; a block scan of the per-range counts lays them out
@@ -1170,7 +1279,8 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     constexpr int NT = kRefineThreads, NW = NT / 64, U = 8, W2 = 10;
     __shared__ uint32_t h[1 << W2];
     __shared__ uint32_t roff[kMMaxRanges], rcnt[kMMaxRanges];  // later: per-range (eq, gt) counts
-    __shared__ uint32_t lds[NW], s_digit, s_acc;
+    __shared__ uint32_t toff[kMMaxRanges];  // tail offsets while staging; later: per-range eq counts
+    __shared__ uint32_t lds[NW], lds2[4 * NW], s_digit, s_acc;
     constexpr int RB = 16;  // ranges per wave whose first candidates load up front
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const MItem it = b.it[t];
@@ -1183,6 +1293,7 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     // loaded for every thread (NT == kMMaxRanges: in bounds) so that they need not wait for
     // `it`; entries past nr are masked below
     const uint32_t gt_raw = ws->cnt_gt[t][tid], cnt_raw = ws->cnt_cand[t][tid];
+    const uint32_t or_raw = ws->cand_or[t][tid], and_raw = ws->cand_and[t][tid];
     uint32_t v[RB];  // candidate slots lane and lane + 64 of each range
     [[maybe_unused]] uint32_t v2[RB];
 #pragma unroll
@@ -1199,27 +1310,40 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     }
     const uint32_t gt_above = tid < nr ? gt_raw : 0u;  // keys above the bin
     const uint32_t my_cnt = tid < nr ? cnt_raw : 0u;
-    uint32_t nc32;
-    const uint32_t my_off = blk_exscan_u32<NW>(my_cnt, lds, &nc32);
+    const uint32_t my_tail = my_cnt > (uint32_t)kRefinePre ? my_cnt - (uint32_t)kRefinePre : 0u;
+    uint32_t nc32, ntail, my_off, my_toff;
+    uint32_t kor = tid < nr ? or_raw : 0u, kand = tid < nr ? and_raw : ~0u;
+    blk_exscan2_or_and<NW>(my_cnt, my_tail, kor, kand, lds2, &my_off, &my_toff, &nc32, &ntail);
     roff[tid] = my_off;
     rcnt[tid] = my_cnt;
+    toff[tid] = my_toff;
     __syncthreads();
+    decide_common_bits(s, kor, kand);
+    const bool all_eq = s.bit == 0;  // every candidate equals the threshold
     const int64_t nc = nc32;
-    // global index of candidate p (p-th in range order): range = last r with roff[r] <= p
-    auto gidx = [&](uint32_t p) -> int64_t {
+    // last r in [0, nr) with a[r] <= p: the range holding the p-th entry of an exclusive scan
+    // (ranges with nothing share their successor's offset; the last of equals holds p)
+    auto range_of = [&](const uint32_t* a, uint32_t p) -> int {
         int lo = 0, hi = nr - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (roff[mid] <= p) lo = mid;
+            if (a[mid] <= p) lo = mid;
             else hi = mid - 1;
         }
+        return lo;
+    };
+    // global index of candidate p (p-th in range order)
+    auto gidx = [&](uint32_t p) -> int64_t {
+        const int lo = range_of(roff, p);
         return (int64_t)lo * it.range + (p - roff[lo]);
     };
-    const bool staged = nc <= kRefineLdsCap;
+    const bool staged = !all_eq && nc <= kRefineLdsCap;
     if (staged) {
-        // usual case: wave w copies ranges w, w + NW, ..., lane j candidates j and j + 64 of
-        // each (the first RB ranges' first 128 candidates are already in registers; longer
-        // ranges and ranges past NW * RB load here), then everything is read from LDS
+        // usual case: wave w copies ranges w, w + NW, ..., lane j candidate j (and j + 64)
+        // of each (the first RB ranges' first kRefinePre candidates are already in
+        // registers; ranges past NW * RB load here); the tails past kRefinePre follow as one
+        // flat list with UT loads in flight per thread (a per-range loop would chain one
+        // round trip per range); then everything is read from LDS
         for (int r0 = wave; r0 < nr; r0 += NW * RB) {
             if (r0 != wave) {
 #pragma unroll
@@ -1237,9 +1361,25 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
                     const uint32_t c = rcnt[r], o = roff[r];
                     if ((uint32_t)lane < c) stage[o + lane] = v[q];
                     if constexpr (kRefinePre > 64) if ((uint32_t)lane + 64 < c) stage[o + 64 + lane] = v2[q];
-                    for (uint32_t j = kRefinePre + lane; j < c; j += 64) stage[o + j] = src[(int64_t)r * it.range + j];
                 }
             }
+        }
+        constexpr int UT = 4;
+        for (uint32_t p0 = 0; p0 < ntail; p0 += (uint32_t)NT * UT) {
+            uint32_t kv[UT], dst[UT];
+#pragma unroll
+            for (int u = 0; u < UT; ++u) {
+                const uint32_t p = p0 + (uint32_t)(u * NT + tid);
+                if (p < ntail) {
+                    const int r = range_of(toff, p);
+                    const uint32_t j = (uint32_t)kRefinePre + (p - toff[r]);
+                    kv[u] = src[(int64_t)r * it.range + j];
+                    dst[u] = roff[r] + j;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UT; ++u)
+                if (p0 + (uint32_t)(u * NT + tid) < ntail) stage[dst[u]] = kv[u];
         }
         __syncthreads();
     }
@@ -1261,7 +1401,7 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t i = base + u * NT + tid;
-                if (i < nc && (kv[u] & s.mask) == s.prefix) atomicAdd(&h[(kv[u] >> shift) & dmask], 1u);
+                hist_add_wave(h, (kv[u] >> shift) & dmask, i < nc && (kv[u] & s.mask) == s.prefix);
             }
         }
         __syncthreads();
@@ -1282,27 +1422,67 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     }
     DIAG_STAMP(g_st_refine, 3);
     const uint32_t T = s.prefix;
-    // wave per range: its candidates above / equal to T by ballots; the counts replace the
-    // range's (count, offset) entries (read first, by the same wave)
-    for (int r = wave; r < nr; r += NW) {
-        const uint32_t c = rcnt[r], o = roff[r];
-        uint32_t g = 0, e = 0;
-        for (uint32_t j0 = 0; j0 < c; j0 += 64) {
-            const uint32_t j = j0 + (uint32_t)lane;
-            const uint32_t k = j < c ? (staged ? stage[o + j] : src[(int64_t)r * it.range + j]) : 0u;
-            g += (uint32_t)__popcll(__ballot(j < c && k > T));
-            e += (uint32_t)__popcll(__ballot(j < c && k == T));
+    const uint32_t* cgt;  // per-range candidates above / equal to T
+    const uint32_t* ceq;
+    if (all_eq) {
+        h[tid] = 0u;
+        cgt = h;
+        ceq = rcnt;
+    } else if (staged) {
+        // thread per contiguous run of the staged list (an odd run length keeps the lanes'
+        // LDS reads on distinct banks); counts go to LDS per range when the run crosses into
+        // the next range (h: gt, toff: eq -- both free now)
+        h[tid] = 0u;
+        toff[tid] = 0u;
+        __syncthreads();
+        const uint32_t per = ((nc32 + NT - 1) / NT) | 1u;
+        const uint32_t p0 = (uint32_t)tid * per, p1 = min(nc32, p0 + per);
+        if (p0 < p1) {
+            int r = range_of(roff, p0);
+            uint32_t rend = r + 1 < nr ? roff[r + 1] : nc32;
+            uint32_t g = 0, e = 0;
+            for (uint32_t p = p0; p < p1; ++p) {
+                while (p >= rend) {
+                    if (g) atomicAdd(&h[r], g);
+                    if (e) atomicAdd(&toff[r], e);
+                    g = e = 0;
+                    ++r;
+                    rend = r + 1 < nr ? roff[r + 1] : nc32;
+                }
+                const uint32_t k = stage[p];
+                g += k > T ? 1u : 0u;
+                e += k == T ? 1u : 0u;
+            }
+            if (g) atomicAdd(&h[r], g);
+            if (e) atomicAdd(&toff[r], e);
         }
-        if (lane == 0) {
-            rcnt[r] = g;
-            roff[r] = e;
+        cgt = h;
+        ceq = toff;
+    } else {
+        // wave per range: its candidates above / equal to T by ballots; the counts replace
+        // the range's (count, offset) entries (read first, by the same wave)
+        for (int r = wave; r < nr; r += NW) {
+            const uint32_t c = rcnt[r];
+            uint32_t g = 0, e = 0;
+            for (uint32_t j0 = 0; j0 < c; j0 += 64) {
+                const uint32_t j = j0 + (uint32_t)lane;
+                const uint32_t k = j < c ? src[(int64_t)r * it.range + j] : 0u;
+                g += (uint32_t)__popcll(__ballot(j < c && k > T));
+                e += (uint32_t)__popcll(__ballot(j < c && k == T));
+            }
+            if (lane == 0) {
+                rcnt[r] = g;
+                roff[r] = e;
+            }
         }
+        cgt = rcnt;
+        ceq = roff;
     }
     __syncthreads();
     DIAG_STAMP(g_st_refine, 4);
     const int r = tid;
-    const uint32_t gt = (tid < nr ? rcnt[tid] : 0u) + gt_above;
-    const uint32_t eq = tid < nr ? roff[tid] : 0u;
+    const uint32_t gt = (tid < nr ? cgt[tid] : 0u) + gt_above;
+    const uint32_t eq = tid < nr ? ceq[tid] : 0u;
     uint32_t tot;
     const uint32_t eq_before = blk_exscan_u32<NW>(eq, lds, &tot);
     int64_t take = s.kk - (int64_t)eq_before;
@@ -1347,6 +1527,279 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __r
         select_small_seg<T, kRefineThreads>(segs, small_ids[blockIdx.x - b.cnt], sketch, R, sc, rowlist,
                                             slotmap, dyn);
     DIAG_STAMP(g_st_refine, 1);
+}
+
+// ---- the refine folded into the write pass (items of up to kFuseMaxRows rows) ----
+// k_arc_refine is one block per item: a chain of cold round trips (~11 us on ResNet-18's
+// 131 K-row items) between the compact and write launches.  For items whose candidate lists
+// are a few thousand keys, every write block (one per range, as k_arc_write) re-derives the
+// threshold itself instead: it stages the item's candidates in LDS, runs the same two 10-bit
+// rounds, counts the candidates of the ranges before its own, and writes its range.  The
+// selection is the same exact top-k (same T, same lowest-range-first T-equal allowances).
+constexpr int kFuseCap = 8192;              // staged candidates per block (32 KiB of LDS)
+constexpr int64_t kFuseMaxRows = 262144;    // host rule: largest item of a fused batch
+constexpr int kFuseNT = 256;
+
+__device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int r, const uint32_t* __restrict__ keys,
+                                                      MWorkspace* ws, const uint32_t* __restrict__ ckey,
+                                                      int32_t* __restrict__ out_idx, int32_t* __restrict__ out_slot,
+                                                      uint32_t* __restrict__ stage /* LDS, kFuseCap */) {
+    constexpr int NT = kFuseNT, NW = NT / 64, PR = kMMaxRanges / NT, W2 = 10, NB = 1 << W2, PB = NB / NT;
+    constexpr int kPer = kMTile / 256;  // keys per lane of a write tile
+    __shared__ uint32_t h[NB];
+    __shared__ uint32_t roff[kMMaxRanges];
+    __shared__ uint32_t lds[4 * NW], s_digit, s_acc, s_eq[NW], s_gt[NW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int nr = it.nranges;
+    const uint32_t* src = ckey + it.cand_off;
+    const int64_t r0 = (int64_t)r * it.range;
+    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+    DIAG_STAMP(g_st_refine, 0);
+    // one round trip: the first-pass state, the per-range counts and this range's first tile
+    MState s = ws->st[t];
+    uint32_t cc[PR], cg[PR], kor = 0u, kand = ~0u;
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        const int rr = tid * PR + q;
+        cc[q] = rr < nr ? ws->cnt_cand[t][rr] : 0u;
+        cg[q] = rr < r ? ws->cnt_gt[t][rr] : 0u;  // keys above the bin, ranges before r
+        kor |= rr < nr ? ws->cand_or[t][rr] : 0u;
+        kand &= rr < nr ? ws->cand_and[t][rr] : ~0u;
+    }
+    const int64_t wb0 = r0 + (int64_t)wave * (kMTile / 4);
+    uint32_t kv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) kv[j] = keys[it.key_off + min<int64_t>(wb0 + j * 64 + lane, r1 - 1)];
+    if (r == 0)  // the compact launch was the last reader of the key pass's histogram
+        for (int i = tid; i < kMBins; i += NT) ws->hist[t][i] = 0u;
+    uint32_t csum = 0, gsum = 0;
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        csum += cc[q];
+        gsum += cg[q];
+    }
+    uint32_t cbase, gdummy, nc32, gabove;
+    blk_exscan2_or_and<NW>(csum, gsum, kor, kand, lds, &cbase, &gdummy, &nc32, &gabove);
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        roff[tid * PR + q] = cbase;
+        cbase += cc[q];
+    }
+    __syncthreads();
+    decide_common_bits(s, kor, kand);
+    const bool all_eq = s.bit == 0;  // every candidate equals the threshold
+    const bool staged = !all_eq && nc32 <= (uint32_t)kFuseCap;
+    if (staged) {
+        constexpr int UT = 8;
+        int rr = 0;  // range of the lane's current candidate: positions only grow
+        for (uint32_t p0 = 0; p0 < nc32; p0 += (uint32_t)NT * UT) {
+            uint32_t v[UT];
+#pragma unroll
+            for (int u = 0; u < UT; ++u) {
+                const uint32_t p = p0 + (uint32_t)(u * NT + tid);
+                if (p < nc32) {
+                    while (rr + 1 < nr && roff[rr + 1] <= p) ++rr;
+                    v[u] = src[(int64_t)rr * it.range + (p - roff[rr])];
+                } else {
+                    v[u] = 0u;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UT; ++u) {
+                const uint32_t p = p0 + (uint32_t)(u * NT + tid);
+                if (p < nc32) stage[p] = v[u];
+            }
+        }
+        __syncthreads();
+    }
+    // f(p, key) for candidates p < lim: from LDS, or (more than kFuseCap candidates, e.g. a
+    // bin of tied zero rows) from their regions with UG loads in flight per thread
+    auto sweep = [&](uint32_t lim, auto&& f) {
+        if (staged) {
+            for (uint32_t p0 = 0; p0 < lim; p0 += (uint32_t)NT * 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t p = p0 + (uint32_t)(u * NT + tid);
+                    v[u] = p < lim ? stage[p] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t p = p0 + (uint32_t)(u * NT + tid);
+                    f(p, v[u], p < lim);  // every lane (f may use wave operations)
+                }
+            }
+        } else {
+            constexpr int UG = 32;
+            int rr = 0;  // range of the lane's current candidate: positions only grow
+            for (uint32_t p0 = 0; p0 < lim; p0 += (uint32_t)NT * UG) {
+                uint32_t v[UG];
+#pragma unroll
+                for (int u = 0; u < UG; ++u) {
+                    const uint32_t p = p0 + (uint32_t)(u * NT + tid);
+                    if (p < lim) {
+                        while (rr + 1 < nr && roff[rr + 1] <= p) ++rr;
+                        v[u] = src[(int64_t)rr * it.range + (p - roff[rr])];
+                    } else {
+                        v[u] = 0u;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UG; ++u) {
+                    const uint32_t p = p0 + (uint32_t)(u * NT + tid);
+                    f(p, v[u], p < lim);
+                }
+            }
+        }
+    };
+    DIAG_STAMP(g_st_refine, 2);
+    while (s.bit > 0) {
+        const int w = s.bit < W2 ? s.bit : W2;
+        const int shift = s.bit - w;
+        const uint32_t dmask = (1u << w) - 1u;
+#pragma unroll
+        for (int q = 0; q < PB; ++q) h[q * NT + tid] = 0u;
+        __syncthreads();
+        const uint32_t pm = s.mask, pp = s.prefix;
+        sweep(nc32, [&](uint32_t, uint32_t k, bool ok) {
+            hist_add_wave(h, (k >> shift) & dmask, ok && (k & pm) == pp);
+        });
+        __syncthreads();
+        const int nb = 1 << w;
+        const int per = (nb + NT - 1) / NT;  // bins per thread, consecutive from the top
+        uint32_t c[PB], sum = 0;
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+            const int bin = nb - 1 - (tid * per + q);
+            c[q] = (q < per && bin >= 0) ? h[bin] : 0u;
+            sum += c[q];
+        }
+        uint32_t total;
+        const uint32_t excl = blk_exscan_u32<NW>(sum, lds, &total);
+        if ((uint64_t)excl < (uint64_t)s.kk && (uint64_t)excl + sum >= (uint64_t)s.kk) {
+            uint32_t acc = excl;
+            int q = 0;
+            for (; q < per - 1; ++q) {
+                if ((uint64_t)acc + c[q] >= (uint64_t)s.kk) break;
+                acc += c[q];
+            }
+            s_digit = (uint32_t)(nb - 1 - (tid * per + q));
+            s_acc = acc;
+        }
+        __syncthreads();
+        s.prefix |= s_digit << shift;
+        s.mask |= dmask << shift;
+        s.kk -= (int64_t)s_acc;
+        s.bit = shift;
+        __syncthreads();  // s_digit / s_acc / h are rewritten by the next round
+    }
+    DIAG_STAMP(g_st_refine, 3);
+    const uint32_t T = s.prefix;
+    // candidates before this range (> T, == T) and this range's == T
+    const uint32_t cb = roff[r], ce = r + 1 < nr ? roff[r + 1] : nc32;
+    uint32_t gb = 0, eb = 0, eo = 0;
+    if (all_eq) {  // no candidate above T; every one ties with it
+        if (tid == 0) {
+            eb = cb;
+            eo = ce - cb;
+        }
+    } else sweep(ce, [&](uint32_t p, uint32_t k, bool ok) {
+        if (!ok) return;
+        if (p < cb) {
+            gb += k > T ? 1u : 0u;
+            eb += k == T ? 1u : 0u;
+        } else {
+            eo += k == T ? 1u : 0u;
+        }
+    });
+    uint32_t x0, x1, tgb, teb;
+    blk_exscan_u32x2<NW>(gb, eb, lds, &x0, &x1, &tgb, &teb);
+    uint32_t teo;
+    (void)blk_exscan_u32<NW>(eo, lds, &teo);
+    const int64_t kk = s.kk;
+    int64_t take = kk - (int64_t)teb;
+    take = take < 0 ? 0 : (take > (int64_t)teo ? (int64_t)teo : take);
+    uint32_t take_left = (uint32_t)take;
+    int64_t run = (int64_t)gabove + tgb + min<int64_t>(kk, (int64_t)teb);
+    DIAG_STAMP(g_st_refine, 4);
+    // the write of this range (k_arc_write's body): ballot compaction in index order
+    for (int64_t tile = r0; tile < r1; tile += kMTile) {
+        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
+        if (tile != r0) {
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) kv[j] = keys[it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)];
+        }
+        uint32_t weq = 0, wgt = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const bool valid = wb + j * 64 + lane < r1;
+            weq += (uint32_t)__popcll(__ballot(valid && kv[j] == T));
+            wgt += (uint32_t)__popcll(__ballot(valid && kv[j] > T));
+        }
+        if (lane == 0) {
+            s_eq[wave] = weq;
+            s_gt[wave] = wgt;
+        }
+        __syncthreads();
+        uint32_t eqb = 0, gtb = 0, teq = 0, tgt = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            eqb += w < wave ? s_eq[w] : 0u;
+            gtb += w < wave ? s_gt[w] : 0u;
+            teq += s_eq[w];
+            tgt += s_gt[w];
+        }
+        __syncthreads();
+        uint32_t run_eq = eqb;
+        int64_t run_sel = run + gtb + min(eqb, take_left);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int64_t i = wb + j * 64 + lane;
+            const bool valid = i < r1;
+            const bool eq = valid && kv[j] == T;
+            const bool gt = valid && kv[j] > T;
+            const uint64_t beq = __ballot(eq);
+            const bool sel = gt || (eq && run_eq + (uint32_t)__popcll(beq & lt) < take_left);
+            const uint64_t bsel = __ballot(sel);
+            const int64_t my = run_sel + (int64_t)__popcll(bsel & lt);
+            if (sel && my < it.k) out_idx[it.out_off + my] = (int32_t)i;  // bound: never past k
+            if (valid) out_slot[it.slot_off + i] = sel ? (int32_t)my : -1;
+            run_eq += (uint32_t)__popcll(beq);
+            run_sel += (int64_t)__popcll(bsel);
+        }
+        const uint32_t te = min(teq, take_left);
+        run += tgt + te;
+        take_left -= te;
+    }
+#ifdef ARCTOPK_STAMPS
+    __syncthreads();
+#endif
+    DIAG_STAMP(g_st_refine, 1);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, int nflat,
+                                                             const uint32_t* __restrict__ keys, MWorkspace* ws,
+                                                             const uint32_t* __restrict__ ckey,
+                                                             const SegDev* __restrict__ segs,
+                                                             const int32_t* __restrict__ small_ids,
+                                                             const T* __restrict__ sketch, int R, Scale sc,
+                                                             int32_t* __restrict__ rowlist,
+                                                             int32_t* __restrict__ slotmap, VDrawJob job) {
+    if (maybe_draw_v<T>(job, kFuseNT)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    if ((int)blockIdx.x >= nflat) {  // the small segments' single-block selects
+        select_small_seg<T, kFuseNT>(segs, small_ids[blockIdx.x - nflat], sketch, R, sc, rowlist, slotmap, dyn);
+        return;
+    }
+    const MBatch& b = *bp;
+    int t = 0, r = (int)blockIdx.x;  // flat grid: the ranges of the batch's items back to back
+    while (t + 1 < b.cnt && r >= b.it[t].nranges) {
+        r -= b.it[t].nranges;
+        ++t;
+    }
+    arc_write_fused_range(b.it[t], t, r, keys, ws, ckey, rowlist, slotmap, dyn);
 }
 
 struct KeysGrid {
@@ -2280,14 +2733,39 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
 #endif
         int e = ms_arc_compact(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, st);
         if (e) return e;
-        static const hipError_t lds_ok = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&k_arc_refine<T>), hipFuncAttributeMaxDynamicSharedMemorySize,
-            kRefineLdsCap * 4);
-        if (lds_ok != hipSuccess) return (int)lds_ok;
         const int nsm = (bi == 0 && !ARCTOPK_DIAG_NOSMALL) ? p->n_small : 0;
         VDrawJob bj = job;
         if (bi != 0) bj.n = 0;
         uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
+        // items of at most kFuseMaxRows rows: the refine runs inside the write blocks (one
+        // launch fewer); the small selects sharing the launch must fit 256-thread blocks
+        static const bool fuse_ok = [] {  // tuning switch (A/B): ARCTOPK_FUSED_WRITE=0 disables
+            const char* env = std::getenv("ARCTOPK_FUSED_WRITE");
+            return !(env && std::atoi(env) == 0);
+        }();
+        if (fuse_ok && maxn <= kFuseMaxRows && (nsm == 0 || p->small_lds <= 4096 * 4 + 16)) {
+            int nflat = 0;
+            for (int i = 0; i < b.cnt; ++i) nflat += b.it[i].nranges;
+            const size_t shm = std::max<size_t>((size_t)kFuseCap * 4, nsm ? (size_t)p->small_lds : 0);
+            if (bi == 0)
+                launch_job_kernel(&k_arc_write_fused<T>, dim3(nflat + nsm + bj.n), dim3(kFuseNT), shm, st,
+                                  (const MBatch*)(p->d_large_batches + bi), nflat, (const uint32_t*)p->d_keys,
+                                  p->d_mws, (const uint32_t*)ckey, (const SegDev*)p->d_segs,
+                                  (const int32_t*)p->d_small, sketch, (int)p->r, make_scale(ws), rowlist, slotmap,
+                                  bj);
+            else
+                hipLaunchKernelGGL(k_arc_write_fused<T>, dim3(nflat + nsm + bj.n), dim3(kFuseNT), shm, st,
+                                   p->d_large_batches + bi, nflat, p->d_keys, p->d_mws, ckey, p->d_segs, p->d_small,
+                                   sketch, p->r, make_scale(ws), rowlist, slotmap, bj);
+            if (bi == 0) *drawn = true;
+            e = (int)hipGetLastError();
+            if (e) return e;
+            continue;
+        }
+        static const hipError_t lds_ok = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&k_arc_refine<T>), hipFuncAttributeMaxDynamicSharedMemorySize,
+            kRefineLdsCap * 4);
+        if (lds_ok != hipSuccess) return (int)lds_ok;
         if (bi == 0)
             launch_job_kernel(&k_arc_refine<T>, dim3(b.cnt + nsm + bj.n), dim3(kRefineThreads),
                               (size_t)kRefineLdsCap * 4, st, (const MBatch*)(p->d_large_batches + bi), p->d_mws,

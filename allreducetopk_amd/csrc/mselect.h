@@ -74,6 +74,8 @@ struct MWorkspace {
     uint32_t take_eq[kMB][kMMaxRanges];
     uint32_t sel_before[kMB][kMMaxRanges];
     uint32_t cnt_cand[kMB][kMMaxRanges];   // ARC: candidates of each range (k_arc_compact)
+    uint32_t cand_or[kMB][kMMaxRanges];    // ARC: OR / AND of each range's candidates (the bits
+    uint32_t cand_and[kMB][kMMaxRanges];   // all candidates share are decided without a round)
     // followed by the candidate lists: uint32 key[cap_total], uint32 index[cap_total]
 };
 

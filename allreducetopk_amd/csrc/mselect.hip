@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
                                                      const uint32_t* __restrict__ keys, MWorkspace* ws,
                                                      uint32_t* __restrict__ ckey) {
     const MBatch& b = *bp;
-    __shared__ uint32_t lds[4], s_cnt[4];
+    __shared__ uint32_t lds[4], s_cnt[4], s_and[4];
     DIAG_STAMP(g_st_compact, 0);
     int t, r;
     if (!ms_locate(b, &t, &r)) return;
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     uint32_t* dst = ckey + it.cand_off + r0;
-    uint32_t gt = 0, run = 0;
+    uint32_t gt = 0, run = 0, kor = 0u, kand = ~0u;
     for (int64_t tile = r0; tile < r1; tile += kMTile) {
         const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
         uint32_t kv[kPerLane];
@@ -323,17 +323,34 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
         }
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
-            if ((bm[j] >> lane) & 1ull) dst[base + popc64(bm[j] & lt)] = kv[j];
+            if ((bm[j] >> lane) & 1ull) {
+                dst[base + popc64(bm[j] & lt)] = kv[j];
+                kor |= kv[j];
+                kand &= kv[j];
+            }
             base += popc64(bm[j]);
         }
         run += tot;
         __syncthreads();  // s_cnt is rewritten by the next tile
     }
-    uint32_t total;
-    (void)block_exscan_u32<4>(gt, lds, &total);
+    // block totals: keys above the bin, OR / AND of the bin's keys (one barrier)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        gt += __shfl_xor(gt, o, 64);
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 0) {
+        lds[wave] = gt;
+        s_cnt[wave] = kor;
+        s_and[wave] = kand;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        ws->cnt_gt[t][r] = total;
+        ws->cnt_gt[t][r] = lds[0] + lds[1] + lds[2] + lds[3];
         ws->cnt_cand[t][r] = run;
+        ws->cand_or[t][r] = s_cnt[0] | s_cnt[1] | s_cnt[2] | s_cnt[3];
+        ws->cand_and[t][r] = s_and[0] & s_and[1] & s_and[2] & s_and[3];
     }
     DIAG_STAMP(g_st_compact, 1);
 }

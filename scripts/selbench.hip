@@ -65,6 +65,11 @@ int main(int argc, char** argv) {
     std::normal_distribution<float> n01;
     std::vector<float> hG(info.numel), hV(info.v_len);
     for (auto& x : hG) x = n01(rng);
+    if (const char* zr = getenv("ZERO_ROWS")) {  // ZERO_ROWS=m: 9 of every 10 rows of m values all zero
+        const int64_t m = atoll(zr);
+        for (int64_t i = 0; i < (int64_t)hG.size(); ++i)
+            if ((i / m) % 10 != 0) hG[i] = 0.f;
+    }
     for (auto& x : hV) x = n01(rng);
     float *G, *V, *sk;
     int32_t *rl, *sm;

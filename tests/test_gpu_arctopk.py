@@ -398,6 +398,37 @@ def test_select_degenerate_energies(fill):
         assert torch.all(r_[1:] > r_[:-1])
 
 
+@pytest.mark.parametrize("fill", ["band", "zero_rows"])
+def test_select_crowded_first_bin(fill):
+    """The k-th energy's 12-bit first-pass bin holding far more candidates than a write block
+    stages (the fused refine-in-write path's global-memory rounds): "band" = every energy
+    distinct inside one bin, so both 10-bit rounds run; "zero_rows" = 90 % all-zero rows
+    around ragged non-zero ones (the Llama embedding case), resolved by the shared-bit
+    decision.  Exact top-k under the tie rule, ascending rows."""
+    shapes = [(200000, 8), (70000, 8), (300, 4)]
+    segs = A.segments(shapes, 0.2)
+    plan = BucketPlan(shapes, 4, 0.2, torch.float32, DEV)
+    stream = torch.cuda.current_stream().cuda_stream
+    gen = torch.Generator().manual_seed(5)
+    Ps = []
+    for s in segs:
+        P = torch.zeros(s.n, 4)
+        if fill == "band":  # energies in [1, 1 + 1/17): one 12-bit bin of the key bits
+            P[:, 0] = torch.sqrt(1.0 + torch.rand(s.n, generator=gen) / 17.0)
+        else:
+            nz = torch.arange(s.n) % 10 == 3
+            P[nz] = torch.randn(int(nz.sum()), 4, generator=gen)
+        Ps.append(P)
+    ref = torch.cat([p.flatten() for p in Ps])
+    plan.sketch[:ref.numel()].copy_(ref.to(DEV))
+    plan.select(1, stream)
+    torch.cuda.synchronize()
+    norms, _ = A.select(Ps, 1, segs)
+    for r_, nrm, s in zip(_gpu_rows(plan), norms, plan.segments):
+        assert check_rows_tie_aware(r_, nrm, int(s.k_rows), band=0.0) == 0
+        assert torch.all(r_[1:] > r_[:-1])
+
+
 @pytest.mark.parametrize("name", [n for n in case_names("arc_") if "bf16" in n and n.endswith("ws1")])
 def test_bf16_golden_on_gpu(name):
     """bf16 buckets against reference-generated golden vectors.
