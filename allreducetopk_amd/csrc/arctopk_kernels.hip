@@ -1539,6 +1539,7 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __r
 constexpr int kFuseCap = 8192;              // staged candidates per block (32 KiB of LDS)
 constexpr int64_t kFuseMaxRows = 262144;    // host rule: largest item of a fused batch
 constexpr int kFuseNT = 256;
+constexpr int kFuseMaxBlocks = 512;         // host rule: two blocks per CU (LDS allows three)
 
 __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int r, const uint32_t* __restrict__ keys,
                                                       MWorkspace* ws, const uint32_t* __restrict__ ckey,
@@ -2738,14 +2739,21 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         if (bi != 0) bj.n = 0;
         uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
         // items of at most kFuseMaxRows rows: the refine runs inside the write blocks (one
-        // launch fewer); the small selects sharing the launch must fit 256-thread blocks
+        // launch fewer)
         static const bool fuse_ok = [] {  // tuning switch (A/B): ARCTOPK_FUSED_WRITE=0 disables
             const char* env = std::getenv("ARCTOPK_FUSED_WRITE");
             return !(env && std::atoi(env) == 0);
         }();
-        if (fuse_ok && maxn <= kFuseMaxRows && (nsm == 0 || p->small_lds <= 4096 * 4 + 16)) {
-            int nflat = 0;
-            for (int i = 0; i < b.cnt; ++i) nflat += b.it[i].nranges;
+        int nflat = 0;
+        for (int i = 0; i < b.cnt; ++i) nflat += b.it[i].nranges;
+        // ... and only while every write block is resident at once: each one now carries a
+        // refine, so a second round of blocks costs more than the refine launch it saves
+        // (28 x [512, 512, 3, 3]: 896 blocks, select 63 -> 74 us)
+        // The small selects sharing the launch run as 256-thread blocks: only when none has
+        // more than 4,096 rows (1,024-thread blocks select 8 K-row segments faster than these
+        // write blocks finish: ResNet-18's third DDP bucket measured 250 -> 241 GB/s fused)
+        if (fuse_ok && maxn <= kFuseMaxRows && nflat + nsm + bj.n <= kFuseMaxBlocks &&
+            (nsm == 0 || p->small_lds <= 4096 * 4 + 16)) {
             const size_t shm = std::max<size_t>((size_t)kFuseCap * 4, nsm ? (size_t)p->small_lds : 0);
             if (bi == 0)
                 launch_job_kernel(&k_arc_write_fused<T>, dim3(nflat + nsm + bj.n), dim3(kFuseNT), shm, st,
