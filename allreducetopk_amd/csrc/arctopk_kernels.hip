@@ -424,6 +424,10 @@ __device__ __forceinline__ void wave_sum_r(float (&a)[R], int lane) {
 #define ARCTOPK_ENC_ROW_WPE 4
 #endif
 constexpr int kEncRowUnits = ARCTOPK_ENC_ROW_UNITS;
+#ifndef ARCTOPK_ENC_ROW_UNITS_BF16
+#define ARCTOPK_ENC_ROW_UNITS_BF16 4  // tuning switch (A/B builds): a bf16 unit is 8 elements
+#endif
+constexpr int kEncRowUnitsBf16 = ARCTOPK_ENC_ROW_UNITS_BF16;
 template <typename T, int R, int EF, bool ERR_IN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ARCTOPK_ENC_ROW_WPE)))
 k_encode_rows(const SegDev* __restrict__ segs, const EncTile* __restrict__ tiles,
@@ -436,7 +440,7 @@ k_encode_rows(const SegDev* __restrict__ segs, const EncTile* __restrict__ tiles
     constexpr bool WRITE_E = (EF == ARCTOPK_EF14);
     constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
     constexpr int PQ = kQuadsPer16<T>;
-    constexpr int U = kEncRowUnits;
+    constexpr int U = sizeof(T) == 2 ? kEncRowUnitsBf16 : kEncRowUnits;
     const int m = (int)s.m;
     const int c0 = t.c0, cl = t.clen;
     const T* __restrict__ Vs = V + s.v_off;
@@ -459,6 +463,90 @@ k_encode_rows(const SegDev* __restrict__ segs, const EncTile* __restrict__ tiles
     const int m4 = cl >> 2;
     const int mu = m4 / PQ;
     const float4* vt4 = reinterpret_cast<const float4*>(lds);
+    // the row's R sums, reduced over the wave, to the sketch (or a column part's partials)
+    auto put_row = [&](int64_t row, float (&acc)[R]) {
+        wave_sum_r<R>(acc, lane);
+        if constexpr (R == 4) {
+            if ((lane & 15) == 0) {
+                const int j = ((lane >> 5) << 1) | ((lane >> 4) & 1);
+                if (pt_out) pt_out[row * R + j] = acc[0];
+                else st1<T>(sk_out + row * R + j, acc[0]);
+            }
+        } else {
+            if (lane < R) {
+                float v = acc[0];
+#pragma unroll
+                for (int j = 1; j < R; ++j)
+                    if (lane == j) v = acc[j];
+                if (pt_out) pt_out[row * R + lane] = v;
+                else st1<T>(sk_out + row * R + lane, v);
+            }
+        }
+    };
+    const int upr = (mu + 63) >> 6;  // 64-unit groups of one row
+    if (sizeof(T) == 2 && 2 * upr <= U) {
+        // Rows that fill at most half the units (bf16 rows of <= 4 K elements, fp32 of <= 2 K):
+        // a wave streams TWO rows per pass (its rows q and q + 4), so each lane keeps the
+        // same bytes in flight as on a full-width fp32 row (one row per pass left the bf16
+        // headline encode at 3.9 TB/s)
+        constexpr int H = U / 2;
+        for (int64_t q = wave; q < t.nrows; q += 8) {
+            const bool has_b = q + 4 < t.nrows;
+            const int64_t ra = t.row0 + q * t.rstride, rb = t.row0 + (q + 4) * t.rstride;
+            const T* gp[2] = {G + s.offset + ra * m + c0, G + s.offset + rb * m + c0};
+            T* ep[2] = {E + s.offset + ra * m + c0, E + s.offset + rb * m + c0};
+            u4_t g[U], e[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int uu = u % H, hb = u / H;
+                if (uu < upr && (hb == 0 || has_b)) {  // wave-uniform
+                    const int c = min(uu * 64 + lane, mu - 1);
+                    g[u] = ld16raw<T, true>(gp[hb], c);
+                    if constexpr (LOAD_E) e[u] = ld16raw<T, true>(ep[hb], c);
+                }
+            }
+            float acc[2][R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc[0][j] = acc[1][j] = 0.f;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int uu = u % H, hb = u / H;
+                if (uu < upr && (hb == 0 || has_b)) {
+                    const int cu = uu * 64 + lane;
+                    const bool ok = cu < mu;
+                    const int c = ok ? cu : mu - 1;
+                    float4 x[PQ], eq[PQ];
+                    unpack16<T>(g[u], x);
+                    if constexpr (LOAD_E) unpack16<T>(e[u], eq);
+#pragma unroll
+                    for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(x[h], LOAD_E ? eq[h] : x[h]);
+                    if constexpr (WRITE_E) {
+                        if (ok) st16<T, true>(ep[hb], c, x);
+                    }
+                    if (!ok) {
+#pragma unroll
+                        for (int h = 0; h < PQ; ++h) x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        float a = acc[hb][j];
+#pragma unroll
+                        for (int h = 0; h < PQ; ++h) {
+                            const float4 v = vt4[j * m4 + c * PQ + h];
+                            a = fmaf(x[h].x, v.x, a);
+                            a = fmaf(x[h].y, v.y, a);
+                            a = fmaf(x[h].z, v.z, a);
+                            a = fmaf(x[h].w, v.w, a);
+                        }
+                        acc[hb][j] = a;
+                    }
+                }
+            }
+            put_row(ra, acc[0]);
+            if (has_b) put_row(rb, acc[1]);
+        }
+        return;
+    }
     for (int64_t q = wave; q < t.nrows; q += 4) {
         const int64_t row = t.row0 + q * t.rstride;
         const T* gp = G + s.offset + row * m + c0;
@@ -467,13 +555,13 @@ k_encode_rows(const SegDev* __restrict__ segs, const EncTile* __restrict__ tiles
 #pragma unroll
         for (int j = 0; j < R; ++j) acc[j] = 0.f;
         for (int cb = 0; cb < mu; cb += 64 * U) {
-            float4 g[U][PQ], e[U][PQ];
+            u4_t g[U], e[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (cb + u * 64 < mu) {  // wave-uniform: no loads past the row
                     const int c = min(cb + u * 64 + lane, mu - 1);
-                    ld16<T, true>(gp, c, g[u]);
-                    if constexpr (LOAD_E) ld16<T, true>(ep, c, e[u]);
+                    g[u] = ld16raw<T, true>(gp, c);
+                    if constexpr (LOAD_E) e[u] = ld16raw<T, true>(ep, c);
                 }
             }
 #pragma unroll
@@ -482,9 +570,11 @@ k_encode_rows(const SegDev* __restrict__ segs, const EncTile* __restrict__ tiles
                     const int cu = cb + u * 64 + lane;
                     const bool ok = cu < mu;
                     const int c = ok ? cu : mu - 1;
-                    float4 x[PQ];
+                    float4 x[PQ], eq[PQ];
+                    unpack16<T>(g[u], x);
+                    if constexpr (LOAD_E) unpack16<T>(e[u], eq);
 #pragma unroll
-                    for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(g[u][h], e[u][h]);
+                    for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(x[h], LOAD_E ? eq[h] : x[h]);
                     if constexpr (WRITE_E) {
                         if (ok) st16<T, true>(ep, c, x);
                     }

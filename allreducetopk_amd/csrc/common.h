@@ -181,6 +181,22 @@ __device__ __forceinline__ void ld16(const T* p, int64_t c, float4 (&q)[kQuadsPe
         q[1] = unpack_bf16x4(u2_t{w.z, w.w});
     }
 }
+// a 16-B unit kept as loaded (4 VGPRs whatever T), unpacked only where it is consumed: holding
+// bf16 units unpacked doubled the encode's load registers and spilled them to scratch
+template <typename T, bool NT>
+__device__ __forceinline__ u4_t ld16raw(const T* p, int64_t c) {
+    const u4_t* w4 = reinterpret_cast<const u4_t*>(p) + c;
+    return NT ? __builtin_nontemporal_load(w4) : *w4;
+}
+template <typename T>
+__device__ __forceinline__ void unpack16(u4_t w, float4 (&q)[kQuadsPer16<T>]) {
+    if constexpr (sizeof(T) == 4) {
+        q[0] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
+    } else {
+        q[0] = unpack_bf16x4(u2_t{w.x, w.y});
+        q[1] = unpack_bf16x4(u2_t{w.z, w.w});
+    }
+}
 template <typename T, bool NT>
 __device__ __forceinline__ void st16(T* p, int64_t c, const float4 (&q)[kQuadsPer16<T>]) {
     if constexpr (sizeof(T) == 4) {
