@@ -25,7 +25,13 @@ BF16 = 1
 DTYPE_CODE = {torch.float32: F32, torch.bfloat16: BF16}  # bucket dtype -> ARCTOPK_F32 / _BF16
 
 STATUS = {1001: "invalid argument", 1002: "ND tensor numel not divisible by 2*t^2",
-          1003: "unsupported dtype", 1004: "empty tensor"}
+          1003: "unsupported dtype", 1004: "empty tensor", 1005: "RCCL library not loadable"}
+ECOMM = 1100  # + ncclResult_t
+NMARKS = 8    # ARCTOPK_MARK_*: phase markers of a step
+MARKS = {"start": 0, "draw": 1, "encode": 2, "sketch_allreduce": 3, "select": 4, "pack": 5,
+         "packed_allreduce": 6, "decode": 7}
+# the exchange's all-reduce callback: fn(ctx, buf, count, dtype, stream) -> status
+ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int32, c_void_p, c_void_p, c_int64, c_int32, c_void_p)
 
 
 class PlanInfo(ctypes.Structure):
@@ -55,7 +61,17 @@ _SIGS = {
                                       c_uint64, c_void_p, c_void_p]),
     "arctopk_plan_bind": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "arctopk_step": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
-                               c_uint64, c_void_p, c_uint64, c_void_p]),
+                               c_uint64, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "arctopk_comm_unique_id": (c_int32, [c_char_p, c_void_p]),
+    "arctopk_comm_init_rccl": (c_int32, [c_char_p, c_char_p, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
+    "arctopk_comm_init_callback": (c_int32, [ALLREDUCE_FN, c_void_p, c_int32, c_int32, POINTER(c_void_p)]),
+    "arctopk_comm_destroy": (c_int32, [c_void_p]),
+    "arctopk_comm_size": (c_int32, [c_void_p]),
+    "arctopk_comm_allreduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
+    "arctopk_exchange_step": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                        c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p]),
+    "arctopk_plan_wait_exchange": (c_int32, [c_void_p, c_void_p]),
     "arctopk_row_energy": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                c_void_p]),
@@ -155,7 +171,8 @@ def _check_build(L) -> None:
 
 def check(status: int, what: str) -> None:
     if status:
-        msg = STATUS.get(int(status), f"hip error {int(status)}")
+        st = int(status)
+        msg = STATUS.get(st, f"RCCL error {st - ECOMM}" if ECOMM <= st < ECOMM + 100 else f"hip error {st}")
         raise RuntimeError(f"{what} failed: {msg} (status {int(status)})")
 
 

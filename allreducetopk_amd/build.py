@@ -27,7 +27,7 @@ INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libarctopk.so")
 SOURCES = ["plan.hip", "arctopk_kernels.hip", "sparse_kernels.hip", "mselect.hip", "vdraw.hip",
-           "codec.hip", "projection.cpp", "step.cpp"]
+           "projection.cpp", "step.cpp", "exchange.cpp"]
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
          "-Wno-unused-function"]
@@ -76,17 +76,32 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     if out == LIB and not defines and not force and not _stale():
         return LIB
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
     tmp = out + ".tmp"
     digest = source_hash(defines)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *[f"-D{d}" for d in defines],
-           f'-DARCTOPK_SRC_HASH="{digest}"', f"-I{INCLUDE}", f"-I{CSRC}", *srcs, "-o", tmp]
+    common = [f"--offload-arch={ARCH}", *FLAGS, *[f"-D{d}" for d in defines],
+              f'-DARCTOPK_SRC_HASH="{digest}"', f"-I{INCLUDE}", f"-I{CSRC}"]
+    objdir = tmp + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    objs = [os.path.join(objdir, os.path.basename(s_) + ".o") for s_ in srcs]
+    # one compiler process per source (the kernels file dominates; the others overlap it)
+    cmds = [[hipcc(), *[f for f in common if f != "-shared"], "-c", s_, "-o", o]
+            for s_, o in zip(srcs, objs)]
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+        for c in cmds:
+            print(" ".join(c), file=sys.stderr)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "8"))))
+    with ThreadPoolExecutor(jobs) as ex:
+        for r in ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds):
+            if r.returncode:
+                raise subprocess.CalledProcessError(r.returncode, r.args, r.stdout, r.stderr + "\n" + r.stdout)
+            if verbose and r.stderr:
+                print(r.stderr, file=sys.stderr)
+    subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-ldl", "-o", tmp], check=True)
+    shutil.rmtree(objdir, ignore_errors=True)
     os.replace(tmp, out)
     return out
-
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

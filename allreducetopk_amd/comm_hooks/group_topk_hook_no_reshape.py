@@ -43,6 +43,7 @@ import torch
 import torch.distributed as dist
 
 from allreducetopk_amd import _native as N
+from allreducetopk_amd import exchange as X
 from allreducetopk_amd.comm_hooks import default_hooks
 from allreducetopk_amd.comm_hooks.projections import SYNC_MAX_VALUES, ProjectionSource
 from allreducetopk_amd.comm_hooks.utils import HookState, dtype_bits, tensor_bits
@@ -126,13 +127,12 @@ class BucketPlan:
         self._done_upto = 0                   # every such encode up to this call is complete
         self._ev_free = []                    # completed checkpoint events, for reuse
         self.v_waits = 0                      # calls whose encode had to wait for its copy
-        self.decode_done = None  # recorded after this bucket's side-stream decode
         self.prestaged = None    # (seed, ring slot) of the next call's V, copied a call early
         # device projections: the seed whose V_ring[0] draw is already enqueued (drawn by the
         # previous call's select launch), and the stream of V_ring[0]'s last writer / reader
         self.v_drawn = None
         self.v_stream = None
-        self.groups = self._make_groups()
+        self.comm_registered = None  # the exchange communicator this plan's buffers are known to
         # the device generator's Philox offset after the reference's per-tensor
         # torch.randn(m, r, device=...) draws of one call (see _reseed_global)
         adv = N.c_uint64()
@@ -147,8 +147,6 @@ class BucketPlan:
         self.bits_sum = sum(((s.n if s.kind == N.SEG_RAW else s.n * r) + s.k_rows * s.m) * bits
                             for s in self.segments)
 
-    PIPELINE_GROUPS = 4             # packed all-reduce split into up to this many pieces
-    PIPELINE_MIN_BYTES = 4 << 20    # ... each at least this large (RCCL efficiency)
     V_RING = 4        # projection slots allocated up front per bucket
     V_RING_MAX = 32   # ... and at most (then the copy stream waits for the oldest reader)
     V_CHECK_EVERY = 8  # calls per slot-reuse checkpoint event
@@ -233,32 +231,6 @@ class BucketPlan:
         if self._ncalls % self.V_CHECK_EVERY == 0:
             self._checkpoint(stream)
 
-    def _make_groups(self):
-        """Contiguous segment ranges with roughly equal packed bytes: (b, e, lo, hi)."""
-        segs = self.segments
-        total = int(self.info.packed_len)
-        ng = max(1, min(self.PIPELINE_GROUPS, len(segs), (4 * total) // self.PIPELINE_MIN_BYTES))
-        groups, b, acc = [], 0, 0
-        for i, s in enumerate(segs):
-            acc += int(s.k_rows * s.m)
-            if acc * ng >= total * (len(groups) + 1) or i == len(segs) - 1:
-                lo = int(segs[b].packed_off)
-                hi = int(s.packed_off + s.k_rows * s.m)
-                groups.append((b, i + 1, lo, hi))
-                b = i + 1
-        return groups
-
-    def pack_range(self, b: int, e: int, grad, err, ef: int, stream: int):
-        N.check(N.lib().arctopk_pack_segments(self.handle, b, e, N.ptr(grad), N.ptr(err), ef,
-                                              self.rowlist.data_ptr(), self.slotmap.data_ptr(),
-                                              self.packed.data_ptr(), stream), "arctopk_pack_segments")
-
-    def decode_range(self, b: int, e: int, world_size: int, ef: int, gerr, out, stream: int):
-        N.check(N.lib().arctopk_decode_segments(self.handle, b, e, self.packed.data_ptr(),
-                                                self.slotmap.data_ptr(), world_size, ef,
-                                                N.ptr(gerr), out.data_ptr(), stream),
-                "arctopk_decode_segments")
-
     @property
     def sketch_view(self):
         return self.sketch[:self.info.sketch_len]
@@ -340,7 +312,6 @@ class GroupTopKState(HookState):
         # MI355X codec state (not in the reference)
         self._plans: Dict[int, Tuple[tuple, BucketPlan]] = {}
         self._proj = ProjectionSource(r)
-        self._order: List[int] = []  # bucket indices in call order within one backward
         # optional phase timing: a list that receives one dict of HIP events for every
         # `phase_event_every`-th call (HIP events on the hook's stream); `hook_events` receives
         # the light samples of every `hook_event_every`-th other call: only start, after the
@@ -349,33 +320,33 @@ class GroupTopKState(HookState):
         self.phase_event_every = 1
         self.hook_events = None
         self.hook_event_every = 0
-        self.phase_event_device_scope = True  # False: torch (system-scope) timing events
         self.prestage_hits = 0  # calls whose projections were copied during the previous call
         self._ev_calls = 0
         # measurement option (not in the reference): model a NIC-staged exchange by moving
         # the packed payload device -> pinned host -> device around the all-reduce
         self.host_staged = False
         self._host_buf = None
-        # multi-GPU overlap (not in the reference, which blocks per collective): at world
-        # size > 1 each bucket's packed all-reduce and decode leave the caller's stream
-        # (decode on a side stream, returned Future carries its event), so the next
-        # bucket's encode runs while this one is on the wire; sketches use a second
-        # communicator so they never queue behind a packed all-reduce
+        # The exchange (not in the reference, which blocks on every collective): at world size
+        # > 1 each call is ONE native step that issues the kernels and both all-reduces
+        # (arctopk_exchange_step); with `async_exchange` the packed all-reduce and the decode
+        # run on an exchange stream, so the next bucket's encode overlaps this bucket's time on
+        # the wire, and the returned Future is device-aware (wait() orders the waiter's stream
+        # after the decode).  `force_exchange` runs that same path at world size 1 (over a
+        # one-rank communicator): the code path of every N > 1 rank, measurable on one GPU.
         self.async_exchange = True
+        self.force_exchange = os.environ.get("ARCTOPK_FORCE_EXCHANGE", "0") == "1"
         # projection H2D on a copy stream (event-ordered) or in order on the caller's stream
         self.v_copy_side_stream = os.environ.get("ARCTOPK_V_COPY", "side") != "main"
         self._copy_streams: Dict[int, torch.cuda.Stream] = {}
-        self._decode_streams: Dict[int, torch.cuda.Stream] = {}
-        self._pending: Dict[int, torch.cuda.Event] = {}  # bucket -> its decode-done event
-        # Sketch all-reduces on a communicator of their own ("separate", created here,
-        # before any backward) or on the packed values' communicator ("shared": no second
-        # communicator; a sketch then queues behind the previous bucket's packed
-        # all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
+        self._xstreams: Dict[int, torch.cuda.Stream] = {}
+        self._x_outstanding = set()  # devices whose exchange stream may hold unwaited decodes
+        # Sketch all-reduces on a communicator of their own ("separate") or on the packed
+        # values' communicator ("shared": a sketch then queues behind the previous bucket's
+        # packed all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
         self.sketch_comm = os.environ.get("ARCTOPK_SKETCH_COMM", "separate")
         if self.sketch_comm not in ("separate", "shared"):
             raise ValueError("ARCTOPK_SKETCH_COMM must be 'separate' or 'shared'")
-        self._sketch_pg = None
-        self.init_sketch_comm()
+        self._comms = None  # (group, device, sketch Comm, packed Comm), see init_exchange_comms
         # The plan of a bucket is found by its buffer's identity (no gradients() walk per
         # call).  DDP rebuilds its buckets once, after the first iteration, and the caching
         # allocator may hand a rebuilt bucket the same block: for the first
@@ -399,7 +370,8 @@ class GroupTopKState(HookState):
         # launch off the critical path.
         self.predraw = os.environ.get("ARCTOPK_PREDRAW", "1") != "0"
         self.predraw_hits = 0
-        self._order_pos: Dict[int, int] = {}
+        self._succ: Dict[int, int] = {}  # bucket -> the bucket that followed it last time
+        self._last_b = None
 
     @property
     def rng(self) -> torch.Generator:
@@ -443,28 +415,32 @@ class GroupTopKState(HookState):
         self._rng_lag += 1
         return seed
 
-    def init_sketch_comm(self) -> None:
-        """Create the sketch communicator now (a collective over every rank of the default
-        group; register_comm_hook_for_ddp_model constructs the state on every rank).
-        Called by the constructor; a state built before init_process_group runs with the
-        shared communicator unless this is called once the group exists.  The hook itself
-        never creates a process group."""
-        if self.sketch_comm != "separate" or self._sketch_pg is not None:
+    def init_exchange_comms(self, device=None) -> None:
+        """Create the exchange's communicators now: collective over the ranks of the hook's
+        group (RCCL communicators block until every rank has called this).
+        register_comm_hook_for_ddp_model calls it on every rank; otherwise the hook does it
+        at its first compressed call (every rank reaches that call at the same point of the
+        same backward).  The constructor itself is not collective."""
+        if self._comms is not None:
             return
         if not (dist.is_available() and dist.is_initialized()):
-            return
+            raise RuntimeError("init_exchange_comms needs an initialised process group")
         group = self.process_group if self.process_group is not None else dist.group.WORLD
-        ws = dist.get_world_size()
-        if ws <= 1 or group.size() != ws:  # a subgroup: its ranks alone run this hook
-            return
-        kw = {}
-        try:  # a default group bound to a device initialises the new communicator eagerly
-            dev = dist.distributed_c10d._get_default_group().bound_device_id
-            if dev is not None:
-                kw["device_id"] = dev
-        except AttributeError:
-            pass
-        self._sketch_pg = dist.new_group(ranks=list(range(ws)), **kw)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        device = torch.device(device)
+        sk, pk = X.make_comms(group, device, self.sketch_comm)
+        self._comms = (group, device, sk, pk)
+
+    def _exchange_comms(self, group, dev):
+        if self._comms is None:
+            logger.info("ARC-TopK: creating the exchange communicators at the first compressed call")
+            self.init_exchange_comms(dev)
+        g, d, sk, pk = self._comms
+        if g is not group or d != dev:
+            raise RuntimeError("the exchange communicators were made for another group or device")
+        return sk, pk
 
     def _side_stream(self, table: Dict[int, "torch.cuda.Stream"], device,
                      priority: int = 0) -> "torch.cuda.Stream":
@@ -474,11 +450,6 @@ class GroupTopKState(HookState):
             s = torch.cuda.Stream(device=device, priority=priority)
             table[idx] = s
         return s
-
-    def _sketch_group(self, group):
-        """The communicator of the sketch all-reduces: the separate one made at
-        construction, else the packed values' own."""
-        return self._sketch_pg if self._sketch_pg is not None else group
 
     def _after_load(self) -> None:
         # prefetched projections were keyed on seeds of the old rng position
@@ -509,31 +480,27 @@ class GroupTopKState(HookState):
         self._plans[bucket.index()] = (key, plan, ident)
         return plan
 
+    def _note_call(self, b: int) -> None:
+        """Record the observed bucket order (the bucket that followed the previous call's);
+        the predictions below follow the latest observation, so a changed order (a DDP
+        bucket rebuild) costs one misprediction per bucket."""
+        if self._last_b is not None and self._last_b != b:
+            self._succ[self._last_b] = b
+        self._last_b = b
+
     def _next_plan(self, b: int):
-        """The plan of the bucket predicted to come after bucket b (order repeats)."""
-        order = self._order
-        pos = self._order_pos.get(b)
-        if pos is None:
-            if b in order:
-                pos = order.index(b)
-            else:
-                pos = len(order)
-                order.append(b)
-            self._order_pos[b] = pos
-        ent = self._plans.get(order[(pos + 1) % len(order)])
+        """The plan of the bucket predicted to come after bucket b."""
+        nb = self._succ.get(b)
+        ent = None if nb is None else self._plans.get(nb)
         return None if ent is None else ent[1]
 
     def _upcoming_ms(self, bucket) -> List[Tuple[int, ...]]:
-        """Column lists of the next calls, assuming the bucket order repeats."""
+        """Column lists of the next calls, following the observed bucket order."""
         b = bucket.index()
-        if b not in self._order:
-            self._order.append(b)
-        order = self._order
-        pos = order.index(b)
         out = []
-        for i in range(1, self._proj.depth + 1):
-            nb = order[(pos + i) % len(order)]
-            ent = self._plans.get(nb)
+        for _ in range(self._proj.depth):
+            b = self._succ.get(b)
+            ent = None if b is None else self._plans.get(b)
             if ent is None:
                 break
             out.append(ent[1].ms)
@@ -546,14 +513,9 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
     repeats) with the seed the rng will yield; a wrong prediction is simply not used (the
     next call compares seeds).  Copying a call early lets that call skip its stream wait
     on the copy (`BucketPlan.await_projection`)."""
-    order = state._order
-    b = bucket.index()
-    if b not in order:
+    nplan = state._next_plan(bucket.index())
+    if nplan is None:
         return
-    ent = state._plans.get(order[(order.index(b) + 1) % len(order)])
-    if ent is None:
-        return
-    nplan = ent[1]
     if not nplan.info.v_len or nplan.dtype != dtype or nplan.device != dev:
         return
     seed = state._proj.peek_next_seed()
@@ -574,6 +536,57 @@ def _prestage_next(state, bucket, dtype, dev) -> None:
 # two of them, several calls apart, gives the hook's device time per call) and the encode
 # kernel alone (after the V draw .. after encode)
 _LIGHT_MARKS = (frozenset(("decode",)), frozenset(("draw", "encode")))
+# the markers each path records (ARCTOPK_MARK_* of arctopk_step / arctopk_exchange_step)
+_STEP_MARKS = frozenset(("start", "draw", "encode", "select", "pack", "decode"))
+_EXCHANGE_MARKS = frozenset(N.MARKS)
+_PHASE_MARKS = ("start", "draw", "encode", "sketch_allreduce", "select", "pack", "h2d",
+                "packed_allreduce", "decode")
+
+
+def _phase_marks(state, names=_PHASE_MARKS):
+    """This call's timing markers (bench sampling, state.phase_events / hook_events): a dict
+    name -> timed device event, or None.  Each marker between two kernels idles the GPU a
+    few us, so only every `phase_event_every`-th call gets the full set and every
+    `hook_event_every`-th other call a light set (_LIGHT_MARKS)."""
+    if state.phase_events is None and state.hook_events is None:
+        return None
+    state._ev_calls += 1
+    c = state._ev_calls - 1
+    if state.phase_events is not None and c % state.phase_event_every == 0:
+        evs = {n: N.DeviceEvent(timing=True) for n in names}
+        state.phase_events.append(evs)
+        return evs
+    if state.hook_events is not None and state.hook_event_every and c % state.hook_event_every == 0:
+        light = _LIGHT_MARKS[(c // state.hook_event_every) % 2]
+        evs = {n: N.DeviceEvent(timing=True) for n in names if n in light}
+        evs["_call"] = c
+        state.hook_events.append(evs)
+        return evs
+    return None
+
+
+def _call_marks(state, names):
+    """The ARCTOPK_MARK_* event array a native step records, or None."""
+    evs = _phase_marks(state, names)
+    if evs is None:
+        return None
+    arr = (N.c_void_p * N.NMARKS)()
+    for n, e in evs.items():
+        if n != "_call":
+            arr[N.MARKS[n]] = e.handle
+    return arr
+
+
+def _order_after_exchange(state, dev) -> None:
+    """Before a collective on the torch process group (warm-up, EF21 init, phase path): the
+    caller's stream waits for the exchange stream's outstanding decodes, so collectives of
+    this library's communicators and of torch's are never in flight together."""
+    dix = torch.device(dev).index or 0
+    if dix in state._x_outstanding:
+        xs = state._xstreams.get(dix)
+        if xs is not None:
+            torch.cuda.current_stream(dev).wait_stream(xs)
+        state._x_outstanding.discard(dix)
 
 
 def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
@@ -608,12 +621,13 @@ def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
 def _claim_projections(state, plan, seed: int, sid: int, dev) -> bool:
     """Device projections of this call: True when V must be drawn now, False when the
     previous call's select launch already drew it for this seed (or there is no V).
-    Orders the caller's stream (raw handle `sid`) after V_ring[0]'s last user when that
-    ran on another stream."""
+    V_ring[0] is written and read on the caller's stream only; when the caller's stream
+    changed since its last user (raw handle `sid` differs), that stream may be gone by now,
+    so the device is synchronised once instead of waiting on a stored handle."""
     if not plan.info.v_len:
         return False
-    if plan.v_stream is not None and plan.v_stream != sid:  # V_ring[0]'s last user ran there
-        torch.cuda.current_stream(dev).wait_stream(torch.cuda.ExternalStream(plan.v_stream, device=dev))
+    if plan.v_stream is not None and plan.v_stream != sid:
+        torch.cuda.synchronize(dev)
     plan.v_stream = sid
     pre, plan.v_drawn = plan.v_drawn, None
     if pre == seed:
@@ -649,7 +663,10 @@ def _current_raw_stream(device_index: int) -> int:
 # stream, and its completion marker then waits behind the queued kernels, so the encode
 # always had to wait for the copy (~17 us idle per call).  A high-priority stream gets a
 # queue of its own: the copy is seen complete a call later and no wait is needed.
-COPY_PRIORITY = int(os.environ.get("ARCTOPK_COPY_PRIORITY", "-1"))
+COPY_PRIORITY = -1
+# The exchange stream runs the packed all-reduce and the decode beside the next bucket's
+# encode: high priority, so RCCL's blocks are dispatched ahead of the encode's queued blocks.
+XSTREAM_PRIORITY = -1
 HOST_TIMES = {} if os.environ.get("ARCTOPK_HOST_TIMING") == "1" else None
 _ht_last = [0.0]
 
@@ -748,7 +765,7 @@ def _stage_through_host(state: GroupTopKState, pv: torch.Tensor, stream, dev,
         state._host_buf = torch.empty(n, dtype=pv.dtype, pin_memory=True)
     hb = state._host_buf[:n]
     d2h = state._side_stream(state._copy_streams, dev, COPY_PRIORITY)
-    h2d = state._side_stream(state._decode_streams, dev)
+    h2d = state._side_stream(state._xstreams, dev)
     d2h.wait_stream(stream)
     h2d.wait_stream(stream)
     step = max(1, -(-n // chunks))
@@ -774,6 +791,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
 
     # warm-up: dense all-reduce for the first start_compress_iter iterations (:213-215)
     if state.iter < state.start_compress_iter:
+        if state._x_outstanding:
+            _order_after_exchange(state, input_tensor.device)
         state.maybe_increase_iter(bucket)
         return default_hooks._allreduce_fut(group, input_tensor, state)
 
@@ -797,6 +816,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             logger.info("A tensor of length %s that represents local/global error is created.", total)
             state.error_dict[b] = torch.clone(input_tensor).detach()
             state.comm_bits_this_round += tensor_bits(input_tensor)
+            if state._x_outstanding:
+                _order_after_exchange(state, input_tensor.device)
             dist.all_reduce(input_tensor, group=group, async_op=False)
             input_tensor.div_(world_size)
             state.global_error_dict[b] = torch.clone(input_tensor).detach()
@@ -818,25 +839,73 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     plan = state._plan_for(bucket, input_tensor)
     dev = input_tensor.device
     dix = dev.index or 0
-    _reseed_global(seed, dix, plan.philox_advance)
+    # host projections model the reference on CPU, whose draws move the CPU generator, not
+    # the device one: the generator-position guarantee covers device projections
+    _reseed_global(seed, dix, plan.philox_advance if device_v else 0)
+    state._note_call(b)
     _ht("seed+plan")
 
     sid = _current_raw_stream(dix)
     dtype = input_tensor.dtype
-    pend = state._pending.pop(b, None)
-    if pend is not None:  # this bucket's previous decode (side stream) must be done
-        torch.cuda.current_stream(dev).wait_event(pend)
-    _ht("plan+pending")
-    if device_v and world_size == 1 and not state.host_staged and not (
-            state.phase_events is not None or state.hook_events is not None):
-        # world size 1, no phase markers: the whole step in one native call (arctopk_step:
-        # [draw] -> encode -> select + the next call's projections -> pack -> decode)
+    L = _LIB[0]
+    exchange = (world_size > 1 or state.force_exchange) and not state.host_staged
+    if exchange:
+        # the code path of every rank at world size > 1: ONE native call issues the kernels
+        # and both all-reduces (arctopk_exchange_step)
+        sk, pk = state._exchange_comms(group, dev)
+        if plan.comm_registered is not pk:
+            sk.register(plan.sketch)
+            pk.register(plan.packed)
+            plan.comm_registered = pk
+        vslot, vptr, draw, nplan, nseed = -1, None, False, None, 0
+        if device_v:
+            draw = _claim_projections(state, plan, seed, sid, dev)
+            nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
+        else:
+            vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, torch.cuda.current_stream(dev))
+            vptr = V.data_ptr()
+        xs = state._side_stream(state._xstreams, dev, XSTREAM_PRIORITY) if state.async_exchange else None
+        if xs is not None and pk.kind == "callback" and xs.cuda_stream not in pk._streams:
+            pk.known_stream(xs)
+        marks = _call_marks(state, _EXCHANGE_MARKS)
+        st_ = L.arctopk_exchange_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
+                                      int(err_in), int(draw), seed,
+                                      nplan.handle if nplan is not None else None, nseed, sk.handle,
+                                      pk.handle, sid, xs.cuda_stream if xs is not None else None, vptr,
+                                      marks)
+        if st_:
+            for c in (sk, pk):
+                c.check(st_, "arctopk_exchange_step")
+            N.check(st_, "arctopk_exchange_step")
+        if nplan is not None:
+            nplan.v_drawn, nplan.v_stream = nseed, sid
+        if vslot >= 0:
+            plan.projection_consumed(vslot, torch.cuda.current_stream(dev))
+        _ht("exchange_step")
+        state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
+        state.maybe_increase_iter(bucket)
+        if xs is None:
+            fut = torch.futures.Future()
+            fut.set_result(input_tensor)
+            return fut
+        state._x_outstanding.add(dix)
+        input_tensor.record_stream(xs)
+        # a device-aware Future: wait()/value() make the waiter's stream wait for the decode
+        fut = torch.futures.Future(devices=[dev])
+        with torch.cuda.stream(xs):
+            fut.set_result(input_tensor)
+        _ht("tail")
+        return fut
+
+    if device_v and world_size == 1 and not state.host_staged:
+        # world size 1: the whole step in one native call (arctopk_step: [draw] -> encode ->
+        # select + the next call's projections -> pack -> decode); both all-reduces are
+        # identities (:264, :280)
         draw = _claim_projections(state, plan, seed, sid, dev)
         nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
-        N.check(_LIB[0].arctopk_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
-                                     int(err_in), int(draw), seed,
-                                     nplan.handle if nplan is not None else None, nseed, sid),
-                "arctopk_step")
+        N.check(L.arctopk_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
+                               int(err_in), int(draw), seed, nplan.handle if nplan is not None else None,
+                               nseed, sid, _call_marks(state, _STEP_MARKS)), "arctopk_step")
         if nplan is not None:
             nplan.v_drawn, nplan.v_stream = nseed, sid
         _ht("step")
@@ -846,107 +915,38 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         _ht("tail")
         return fut
 
+    # phase by phase on the caller's stream: host projections at world size 1, and the
+    # host-staged measurement mode (packed payload through pinned host memory, NIC model)
     stream = torch.cuda.current_stream(dev)
     vslot, V = -1, plan.V_ring[0]
     if not device_v:
         vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, stream)
+    evs = _phase_marks(state)
 
-    evs = None
-    light = None
-    if state.phase_events is not None or state.hook_events is not None:
-        state._ev_calls += 1
-        c = state._ev_calls - 1
-        if state.phase_events is not None and c % state.phase_event_every == 0:
-            evs = {}
-            state.phase_events.append(evs)
-        elif state.hook_events is not None and state.hook_event_every and c % state.hook_event_every == 0:
-            evs, light = {"_call": c}, _LIGHT_MARKS[(c // state.hook_event_every) % 2]
-            state.hook_events.append(evs)
-
-    def mark(name, on=None):
-        if evs is not None and (light is None or name in light):
-            s_ = on if on is not None else stream
-            if state.phase_event_device_scope:  # no system-scope L2 writeback per marker
-                e = N.DeviceEvent(timing=True)
-                e.record(s_.cuda_stream)
-            else:
-                e = torch.cuda.Event(enable_timing=True)
-                e.record(s_)
-            evs[name] = e
+    def mark(name):
+        if evs is not None and name in evs:
+            evs[name].record(sid)
 
     mark("start")
     if device_v and _claim_projections(state, plan, seed, sid, dev):
-        # V on this stream, right before the encode that reads it
-        N.check(N.lib().arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid),
-                "arctopk_draw_projections")
-        _ht("draw_v")
+        N.check(L.arctopk_draw_projections(plan.handle, seed, V.data_ptr(), sid), "arctopk_draw_projections")
     mark("draw")
-    _ht("events")
     plan.encode(input_tensor, err, ef, err_in, V, sid)
-    _ht("encode")
     if vslot >= 0:
         plan.projection_consumed(vslot, stream)
-    _ht("consumed")
     mark("encode")
-
-    overlap = world_size > 1 and state.async_exchange and not state.host_staged
-    if world_size > 1:  # a SUM over one rank is the identity: nothing to exchange
-        sk_group = state._sketch_group(group) if overlap else group
-        dist.all_reduce(plan.sketch_view, group=sk_group, async_op=False)
+    if world_size > 1:
+        _order_after_exchange(state, dev)
+        dist.all_reduce(plan.sketch_view, group=group, async_op=False)
     mark("sketch_allreduce")
     nplan, nseed = _predraw_target(state, b, dtype, dev, sid) if device_v else (None, 0)
     plan.select(world_size, sid, nplan, nseed)
     if nplan is not None:
         nplan.v_drawn, nplan.v_stream = nseed, sid
     mark("select")
-    _ht("select")
     state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum
-    if overlap:
-        # pack group g, start its all-reduce (RCCL stream), pack g+1 ...; decode runs on a
-        # side stream that waits for each group's collective, so the caller's stream is
-        # free for the next bucket's encode while this bucket is on the wire
-        works = []
-        for b_, e_, lo, hi in plan.groups:
-            plan.pack_range(b_, e_, input_tensor, err, ef, sid)
-            works.append(dist.all_reduce(plan.packed[lo:hi], group=group, async_op=True))
-        mark("pack")
-        ds = state._side_stream(state._decode_streams, dev)
-        ds.wait_stream(stream)  # select's slot map, the packed buffer's pack
-        input_tensor.record_stream(ds)
-        with torch.cuda.stream(ds):
-            for (b_, e_, lo, hi), w in zip(plan.groups, works):
-                w.wait()  # the side stream (current here) waits for the collective
-                plan.decode_range(b_, e_, world_size, ef, gerr, input_tensor, ds.cuda_stream)
-            mark("decode", ds)
-            if plan.decode_done is None:
-                plan.decode_done = torch.cuda.Event()
-            plan.decode_done.record(ds)
-            state._pending[b] = plan.decode_done
-            state.maybe_increase_iter(bucket)
-            # a device-aware Future: wait()/value() make the waiter's stream wait for decode
-            fut = torch.futures.Future(devices=[dev])
-            fut.set_result(input_tensor)
-        return fut
-    if world_size > 1 and len(plan.groups) > 1 and not state.host_staged:
-        # pipelined exchange on the caller's stream: pack group g, start its all-reduce,
-        # pack g+1; decode each group once its collective is done
-        works = []
-        for b_, e_, lo, hi in plan.groups:
-            plan.pack_range(b_, e_, input_tensor, err, ef, sid)
-            works.append(dist.all_reduce(plan.packed[lo:hi], group=group, async_op=True))
-        mark("pack")
-        mark("packed_allreduce")
-        for (b_, e_, lo, hi), w in zip(plan.groups, works):
-            w.wait()
-            plan.decode_range(b_, e_, world_size, ef, gerr, input_tensor, sid)
-        mark("decode")
-        state.maybe_increase_iter(bucket)
-        fut = torch.futures.Future()
-        fut.set_result(input_tensor)
-        return fut
     plan.pack(input_tensor, err, ef, sid)
     mark("pack")
-    _ht("pack")
     if state.host_staged:  # D2H to a pinned "NIC buffer" and back (NIC model)
         _stage_through_host(state, plan.packed_view, stream, dev)
         mark("h2d")

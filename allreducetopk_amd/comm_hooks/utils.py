@@ -152,6 +152,12 @@ def register_comm_hook_for_ddp_model(model, process_group, args, optimizer=None)
             process_group=process_group, r=args.r, use_error_feedback=args.use_error_feedback,
             seed=args.seed, start_compress_iter=args.start_compress_iter,
             compress_ratio=args.compress_ratio)
+        if dist.is_available() and dist.is_initialized():
+            group = process_group if process_group is not None else dist.group.WORLD
+            if group.size() > 1 or hook_state.force_exchange:
+                # the exchange's communicators, now, on every rank (collective)
+                dev = next((p.device for p in model.parameters() if p.is_cuda), None)
+                hook_state.init_exchange_comms(dev)
         model.register_comm_hook(hook_state, group_topk_hook)
     elif args.compressor == "noop":
         from torch.distributed.algorithms.ddp_comm_hooks.debugging_hooks import noop_hook

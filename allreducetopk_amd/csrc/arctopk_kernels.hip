@@ -13,8 +13,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
-#include <tuple>
-#include <utility>
 
 #include "common.h"
 #include "mselect.h"
@@ -23,42 +21,11 @@
 using namespace arctopk;
 
 namespace {
-// Launch record for the step graph (arctopk_step): while a step is being captured, the
-// launch that carries the next call's projection draw (VDrawJob, its last argument) keeps
-// a copy of its configuration and arguments, so the instantiated graph's node can be
-// given a new seed per call (hipGraphExecKernelNodeSetParams) without reading anything
-// back from the graph.
-struct LaunchRec {
-    const void* func = nullptr;
-    dim3 grid, block;
-    size_t shm = 0;
-    alignas(16) unsigned char args[512];
-    void* argp[16];
-    VDrawJob* job = nullptr;
-};
-thread_local LaunchRec* g_rec = nullptr;
-
-template <typename Tup, size_t... I>
-void rec_ptrs(Tup* t, void** out, std::index_sequence<I...>) {
-    ((out[I] = static_cast<void*>(&std::get<I>(*t))), ...);
-}
-
-// hipLaunchKernelGGL, recorded when a capture asks for it
+// a kernel launch whose argument list is checked against the kernel's parameter types
 template <typename... P, typename... A>
 void launch_job_kernel(void (*f)(P...), dim3 grid, dim3 block, size_t shm, hipStream_t st, A... a) {
     static_assert(sizeof...(P) == sizeof...(A), "argument count");
     hipLaunchKernelGGL(f, grid, block, shm, st, static_cast<P>(a)...);
-    if (LaunchRec* r = g_rec) {
-        using Tup = std::tuple<P...>;
-        static_assert(sizeof(Tup) <= sizeof(r->args) && sizeof...(P) <= 16, "launch record too small");
-        Tup* t = new (r->args) Tup(static_cast<P>(a)...);  // trivially copyable arguments
-        rec_ptrs(t, r->argp, std::index_sequence_for<P...>{});
-        r->func = reinterpret_cast<const void*>(f);
-        r->grid = grid;
-        r->block = block;
-        r->shm = shm;
-        r->job = &std::get<sizeof...(P) - 1>(*t);
-    }
 }
 }  // namespace
 
@@ -3097,166 +3064,37 @@ extern "C" int arctopk_round_bf16(const float* in, uint16_t* out, int64_t n, voi
 }
 
 // ---------------------------------------------------------------------------
-// World-size-1 step (arctopk_step): encode -> select (+ the next call's projections) ->
-// pack -> decode as plain launches, or (ARCTOPK_STEP_GRAPH=1) replayed as an instantiated
-// HIP graph: the kernels are the phase entry points' own, captured once per (next plan,
-// buffers, EF mode), and one kernel-node update carries the next call's seed.  A probe of
-// 8 empty kernels shows 2 us of host time per graph launch against 20 us for 8 launches,
-// but on the codec the graph saved no host time and lost device time (see use_graph), so
-// plain launches are the default.  The V draw of a call whose projections were not
-// pre-drawn is a plain launch in front of either.
+// World-size-1 step (arctopk_step): [draw] -> encode -> select (+ the next call's
+// projections) -> pack -> decode as plain launches on the caller's stream.  (Replaying the
+// step as a captured HIP graph was measured on MI355X / ROCm 7 in round 2: no host time
+// saved, 19.0 vs 19.4 us per ResNet-18 bucket call, and device time lost, headline 1193 ->
+// 1162 GB/s; it was removed.)
 // ---------------------------------------------------------------------------
 namespace {
-
-struct StepGraph {
-    bool used = false;
-    const arctopk_plan* next = nullptr;
-    const void* bucket = nullptr;
-    const void* err = nullptr;
-    const void* gerr = nullptr;
-    int ef = 0, err_in = 0;
-    hipGraph_t g = nullptr;
-    hipGraphExec_t ge = nullptr;
-    hipGraphNode_t job_node = nullptr;  // the kernel node carrying the next call's draw
-    LaunchRec rec;                      // its configuration and arguments
-    uint64_t tick = 0;
-};
-
-struct StepCache {
-    static constexpr int kEntries = 4;
-    StepGraph e[kEntries];
-    uint64_t tick = 0;
-    hipStream_t cap = nullptr;
-};
-
-void step_graph_reset(StepGraph& s) {
-    if (s.ge) (void)hipGraphExecDestroy(s.ge);
-    if (s.g) (void)hipGraphDestroy(s.g);
-    s = StepGraph{};
+inline int step_mark(void* const* marks, int i, hipStream_t st) {
+    if (!marks || !marks[i]) return 0;
+    return (int)hipEventRecord((hipEvent_t)marks[i], st);
 }
-
-int step_direct(const arctopk_plan* p, void* bucket, void* err, void* gerr, int32_t ef, int32_t err_in,
-                const arctopk_plan* next, uint64_t next_seed, hipStream_t st) {
-    int e = arctopk_encode(p, bucket, err, ef, err_in, p->b_V, p->b_sketch, st);
-    if (!e)
-        e = arctopk_select_draw(p, p->b_sketch, 1, p->b_rowlist, p->b_slotmap, next, next_seed,
-                                next ? next->b_V : nullptr, st);
-    if (!e) e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, st);
-    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, 1, ef, gerr, bucket, st);
-    return e;
-}
-
-// capture the step for this key into slot s; 0 on success (s.ge valid), else s is reset
-int step_capture(StepCache& c, StepGraph& s, const arctopk_plan* p, void* bucket, void* err, void* gerr,
-                 int32_t ef, int32_t err_in, const arctopk_plan* next, uint64_t next_seed) {
-    step_graph_reset(s);
-    hipError_t he = hipStreamBeginCapture(c.cap, hipStreamCaptureModeThreadLocal);
-    if (he != hipSuccess) return (int)he;
-    g_rec = &s.rec;
-    int e = step_direct(p, bucket, err, gerr, ef, err_in, next, next_seed, c.cap);
-    g_rec = nullptr;
-    he = hipStreamEndCapture(c.cap, &s.g);
-    if (!e) e = (int)he;
-    if (!e) e = (int)hipGraphInstantiate(&s.ge, s.g, nullptr, nullptr, 0);
-    const bool job = next && next->n_vchunk;
-    if (!e && job) {  // find the node that carries the draw job
-        size_t nn = 0;
-        e = (int)hipGraphGetNodes(s.g, nullptr, &nn);
-        hipGraphNode_t nodes[64];
-        if (!e && nn > 64) e = ARCTOPK_EINVAL;
-        if (!e) e = (int)hipGraphGetNodes(s.g, nodes, &nn);
-        for (size_t i = 0; !e && i < nn && !s.job_node; ++i) {
-            hipGraphNodeType ty;
-            if (hipGraphNodeGetType(nodes[i], &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
-            hipKernelNodeParams kp{};
-            if (hipGraphKernelNodeGetParams(nodes[i], &kp) == hipSuccess && kp.func == s.rec.func) s.job_node = nodes[i];
-        }
-        // the job went to a launch that was not recorded (e.g. a standalone draw): its seed
-        // would be frozen in the graph, so this key is not cached
-        if (!e && (!s.rec.func || !s.job_node)) e = ARCTOPK_EINVAL;
-    }
-    if (e) {
-        step_graph_reset(s);
-        return e;
-    }
-    s.used = true;
-    s.next = next;
-    s.bucket = bucket;
-    s.err = err;
-    s.gerr = gerr;
-    s.ef = ef;
-    s.err_in = err_in;
-    return 0;
-}
-
 }  // namespace
-
-namespace arctopk {
-void step_cache_free(void* cache) {
-    StepCache* c = static_cast<StepCache*>(cache);
-    for (auto& s : c->e) step_graph_reset(s);
-    if (c->cap) (void)hipStreamDestroy(c->cap);
-    delete c;
-}
-}  // namespace arctopk
 
 extern "C" int arctopk_step(const arctopk_plan* p, void* bucket, void* err, void* gerr, int32_t ef,
                             int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
-                            uint64_t next_seed, void* stream) {
+                            uint64_t next_seed, void* stream, void* const* marks) {
     if (!p || !bucket || !p->b_sketch) return ARCTOPK_EINVAL;  // unbound plan
     if (next && (!next->b_sketch || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    if (draw && p->info.v_len > 0) {
-        const int e = arctopk_draw_projections(p, seed, p->b_V, stream);
-        if (e) return e;
-    }
-    // opt-in (ARCTOPK_STEP_GRAPH=1): measured on MI355X / ROCm 7, replaying the step as a
-    // graph saved no host time here (19.0 vs 19.4 us per ResNet-18 bucket call) and cost
-    // device time (headline 1193 -> 1162 GB/s, ResNet-18 DDP 236 -> 215 GB/s)
-    static const bool use_graph = [] {
-        const char* env = std::getenv("ARCTOPK_STEP_GRAPH");
-        return env && env[0] == '1';
-    }();
-    if (!use_graph) return step_direct(p, bucket, err, gerr, ef, err_in, next, next_seed, st);
-    arctopk_plan* pm = const_cast<arctopk_plan*>(p);  // the graph cache is the plan's own
-    if (!pm->step_cache) {
-        StepCache* c = new (std::nothrow) StepCache;
-        if (!c) return step_direct(p, bucket, err, gerr, ef, err_in, next, next_seed, st);
-        if (hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking) != hipSuccess) {
-            delete c;
-            return step_direct(p, bucket, err, gerr, ef, err_in, next, next_seed, st);
-        }
-        pm->step_cache = c;
-    }
-    StepCache& c = *static_cast<StepCache*>(pm->step_cache);
-    StepGraph* hit = nullptr;
-    for (auto& s : c.e)
-        if (s.used && s.next == next && s.bucket == bucket && s.err == err && s.gerr == gerr && s.ef == ef &&
-            s.err_in == err_in)
-            hit = &s;
-    if (!hit) {
-        StepGraph* slot = &c.e[0];
-        for (auto& s : c.e)
-            if (!s.used || s.tick < slot->tick) {
-                slot = &s;
-                if (!s.used) break;
-            }
-        if (step_capture(c, *slot, p, bucket, err, gerr, ef, err_in, next, next_seed))
-            return step_direct(p, bucket, err, gerr, ef, err_in, next, next_seed, st);
-        hit = slot;
-    }
-    hit->tick = ++c.tick;
-    if (hit->job_node) {  // this call's seed for the next call's projections
-        hit->rec.job->seed = next_seed;
-        hipKernelNodeParams kp{};
-        kp.func = const_cast<void*>(hit->rec.func);
-        kp.gridDim = hit->rec.grid;
-        kp.blockDim = hit->rec.block;
-        kp.sharedMemBytes = (unsigned int)hit->rec.shm;
-        kp.kernelParams = hit->rec.argp;
-        kp.extra = nullptr;
-        const hipError_t he = hipGraphExecKernelNodeSetParams(hit->ge, hit->job_node, &kp);
-        if (he != hipSuccess) return (int)he;
-    }
-    return (int)hipGraphLaunch(hit->ge, st);
+    int e = step_mark(marks, ARCTOPK_MARK_START, st);
+    if (!e && draw && p->info.v_len > 0) e = arctopk_draw_projections(p, seed, p->b_V, stream);
+    if (!e) e = step_mark(marks, ARCTOPK_MARK_DRAW, st);
+    if (!e) e = arctopk_encode(p, bucket, err, ef, err_in, p->b_V, p->b_sketch, st);
+    if (!e) e = step_mark(marks, ARCTOPK_MARK_ENCODE, st);
+    if (!e)
+        e = arctopk_select_draw(p, p->b_sketch, 1, p->b_rowlist, p->b_slotmap, next, next_seed,
+                                next ? next->b_V : nullptr, st);
+    if (!e) e = step_mark(marks, ARCTOPK_MARK_SELECT, st);
+    if (!e) e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, st);
+    if (!e) e = step_mark(marks, ARCTOPK_MARK_PACK, st);
+    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, 1, ef, gerr, bucket, st);
+    if (!e) e = step_mark(marks, ARCTOPK_MARK_DECODE, st);
+    return e;
 }

@@ -334,6 +334,7 @@ struct arctopk_plan {
     int32_t* b_slotmap;
     void* b_packed;
     void* b_V;
-    void* step_cache;                   // arctopk_step's instantiated graphs (arctopk_kernels.hip)
+    void* x_ev_packed;                  // exchange step (exchange.cpp): packed values ready,
+    void* x_ev_done;                    // ... and this bucket's exchange-stream decode done
+    int x_pending;                      // x_ev_done recorded and not yet known complete
 };
-namespace arctopk { void step_cache_free(void* cache); }

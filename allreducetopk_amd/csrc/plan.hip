@@ -367,7 +367,8 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_part) (void)hipFree(p->d_part);
     delete[] p->h_segs;
     delete[] p->h_pack_begin;
-    if (p->step_cache) arctopk::step_cache_free(p->step_cache);
+    if (p->x_ev_packed) (void)hipEventDestroy((hipEvent_t)p->x_ev_packed);
+    if (p->x_ev_done) (void)hipEventDestroy((hipEvent_t)p->x_ev_done);
     delete[] p->h_large_batches;
     if (p->d_large_batches) (void)hipFree(p->d_large_batches);
     if (p->d_mws) (void)hipFree(p->d_mws);

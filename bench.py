@@ -175,8 +175,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-events", action="store_true")
-    ap.add_argument("--system-events", action="store_true",
-                    help="time phases with torch (system-scope) events instead of device-scope ones")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="at N = 1, run the N > 1 code path: the native exchange step with its "
+                         "all-reduces on one-rank RCCL communicators and the exchange stream")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (real runs); gloo lets N ranks share one GPU (rehearsal)")
     ap.add_argument("--host-staged", action="store_true",
@@ -222,6 +223,9 @@ def main():
         st = GroupTopKState(None, r=args.r, compress_ratio=args.ratio, start_compress_iter=0,
                             use_error_feedback=args.ef, seed=1234)
         st.host_staged = args.host_staged
+        st.force_exchange = args.force_exchange
+        if world > 1 or args.force_exchange:
+            st.init_exchange_comms(dev)  # collective, before any step (as the registry does)
         hook = group_topk_hook
     else:  # the reference's TopK / RandK baselines on the same buckets (sparse_hook.py)
         from allreducetopk_amd.comm_hooks.sparse_hook import SparseState, sparse_hook_sync
@@ -239,22 +243,10 @@ def main():
     for _ in range(max(args.warmup, 2 if args.ef == "ef21" else 1)):
         step()
     torch.cuda.synchronize()
-    if not args.no_phase_events and args.hook == "arc":
-        # HIP events on the hook's stream(s) inside the timed region, sparse because each
-        # marker between two kernels idles the GPU a few us: on every 16th call a marker after
-        # the decode (the device timeline between two of them, 16 calls apart, over 16 = the
-        # hook's device time per call, marker costs amortised), on the 8th calls between them
-        # the encode kernel alone (after the V draw .. after encode), and the full per-phase
-        # breakdown on every 64th call
-        st.hook_events = []
-        st.hook_event_every = 8
-        st.phase_events = []
-        st.phase_event_every = 64
-        st.phase_event_device_scope = not args.system_events
-
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as _G
     if _G.HOST_TIMES is not None:  # ARCTOPK_HOST_TIMING=1: steady-state calls only
         _G.HOST_TIMES.clear()
+    # the timed region: K steps, no markers
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -266,31 +258,51 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    host_times = dict(_G.HOST_TIMES) if _G.HOST_TIMES is not None else None
 
     phase_ms = {}
     light = {}
-    if getattr(st, "phase_events", None):
-        order = [p for p in ["start", "draw", "encode", "sketch_allreduce", "select", "pack", "d2h",
-                             "h2d", "packed_allreduce", "decode"] if p in st.phase_events[0]]
-        for a, b in zip(order[:-1], order[1:]):
-            ds = [ev[a].elapsed_time(ev[b]) for ev in st.phase_events]
-            phase_ms[b] = statistics.mean(ds)
-        phase_ms["hook_device_total"] = statistics.mean(
-            ev["start"].elapsed_time(ev["decode"]) for ev in st.phase_events)
-    if getattr(st, "hook_events", None):
-        hs = st.hook_events
+    sample_steps = 0
+    if not args.no_phase_events and args.hook == "arc":
+        # a separate marker pass (not in `value`): device-scope HIP events recorded by the native
+        # step itself on the streams the kernels run on.  Each marker between two kernels idles
+        # the GPU a few us, so they are sparse: on every 2nd call alternately a marker after the
+        # decode (the device timeline between two of them, 4 calls apart, over 4 = the hook's
+        # device time per call, marker costs amortised) and the encode alone (after the V draw
+        # .. after the encode); the full per-phase breakdown on every 32nd call
+        st.hook_events = hs = []
+        st.hook_event_every = 2
+        st.phase_events = pe_list = []
+        pe = st.phase_event_every = 32
+        sample_steps = max(args.steps, 16)
+        for _ in range(sample_steps):
+            step()
+        torch.cuda.synchronize()
+        st.hook_events = st.phase_events = None
+        if pe_list:
+            order = [p for p in ["start", "draw", "encode", "sketch_allreduce", "select", "pack", "h2d",
+                                 "packed_allreduce", "decode"] if p in pe_list[0]]
+            for a, b in zip(order[:-1], order[1:]):
+                phase_ms[b] = statistics.median(ev[a].elapsed_time(ev[b]) for ev in pe_list)
+            phase_ms["hook_device_total"] = statistics.median(
+                ev["start"].elapsed_time(ev["decode"]) for ev in pe_list)
         he = [ev for ev in hs if "encode" in ev]
         hd = sorted((ev for ev in hs if "decode" in ev), key=lambda ev: ev["_call"])
-        # consecutive decode markers with no full-phase sample (every 64th call) between them
-        pe = st.phase_event_every
+        # consecutive decode markers with no full-phase sample (every 32nd call) between them
         per_call = [a_["decode"].elapsed_time(b_["decode"]) / (b_["_call"] - a_["_call"])
                     for a_, b_ in zip(hd, hd[1:])
                     if not any(c % pe == 0 for c in range(a_["_call"] + 1, b_["_call"] + 1))]
         if he and per_call:
             light = {"samples": len(he), "hook_samples": len(per_call),
-                     "encode": statistics.mean(ev["draw"].elapsed_time(ev["encode"]) for ev in he),
-                     "hook": statistics.mean(per_call)}
-
+                     "encode": statistics.median(ev["draw"].elapsed_time(ev["encode"]) for ev in he),
+                     "hook": statistics.median(per_call),
+                     "calls_apart": hd[1]["_call"] - hd[0]["_call"] if len(hd) > 1 else None}
+    if args.hook != "arc":
+        hook_path = "sparse_hook_sync"
+    elif args.host_staged:
+        hook_path = "phase (host-staged)"
+    else:
+        hook_path = "exchange" if (world > 1 or args.force_exchange) else "step"
     value = world * args.steps * bytes_per_step / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     per_bucket = [algorithmic_bytes(args.ef, sh, args.ratio, args.r, eb) for sh in layouts]
@@ -304,7 +316,7 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "algorithmic_bytes_per_launch": alg["encode"],
                 "avg_launch_us": round(light["encode"] * 1e3, 2),
-                "event_scope": "system" if args.system_events else "device",
+                "event_scope": "device", "statistic": "median",
                 "event_samples": light["samples"]}
         hook_s = light["hook"] / 1e3
         wall_s = elapsed / args.steps / nb
@@ -313,7 +325,8 @@ def main():
         # (the north star's "HBM-read roofline"), over the same time
         roof["hook"] = {"algorithmic_bytes": alg["total"], "read_bytes": alg["read"],
                         "device_us": round(hook_s * 1e6, 1),
-                        "device_time": "device timeline between decode-end markers 16 calls apart, per call",
+                        "device_time": f"device timeline between decode-end markers "
+                                       f"{light['calls_apart']} calls apart, per call (median)",
                         "event_samples": light["hook_samples"],
                         "achieved": round(alg["total"] / hook_s / 1e9, 1),
                         "frac": round(alg["total"] / hook_s / 1e9 / HBM_PEAK_GBS, 4),
@@ -334,10 +347,14 @@ def main():
                    "compress_ratio": args.ratio, "r": args.r, "use_error_feedback": args.ef,
                    "bucket_bytes": bucket_bytes, "buckets_per_step": nb,
                    "parallelism": f"dp{world}",
-                   "collectives": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
-                                  + " all_reduce: sketch (own communicator) + packed values "
-                                    "(pipelined in groups, decode overlapped with the next "
-                                    "bucket)"},
+                   "hook_path": hook_path,
+                   "collectives": ("none (world size 1: both all-reduces are identities)"
+                                   if hook_path == "step" else
+                                   ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
+                                   + f" all_reduce over {world} rank(s): sketch (own communicator) + "
+                                     "packed values, issued by the native exchange step; packed "
+                                     "all-reduce + decode on the exchange stream, overlapping the "
+                                     "next bucket")},
         "per_gpu_value": round(value / world, 2),
         "ms_per_bucket": round(ms_per_step / nb, 4),
         "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
@@ -347,10 +364,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, args.workload, label,
                                            eb * bucket_numel(shapes), args.hook)
-    if _G.HOST_TIMES is not None and rank == 0:  # ARCTOPK_HOST_TIMING=1: host us per hook call
+    if host_times is not None and rank == 0:  # ARCTOPK_HOST_TIMING=1: host us per hook call
         calls = max(1, args.steps * nb)
         print("host_us_per_call " + json.dumps({k: round(v / calls * 1e6, 1)
-                                                for k, v in _G.HOST_TIMES.items()}), flush=True)
+                                                for k, v in host_times.items()}), flush=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.barrier()

@@ -41,6 +41,8 @@ extern "C" {
 #define ARCTOPK_ERESHAPE 1002   /* ND tensor numel not divisible by m = 2*t^2 (ref :76 raises) */
 #define ARCTOPK_EDTYPE 1003     /* unsupported element type */
 #define ARCTOPK_EEMPTY 1004     /* empty tensor: torch.topk(k=1) on 0 elements raises */
+#define ARCTOPK_ENOCOMM 1005    /* the RCCL library could not be loaded / lacks entry points */
+#define ARCTOPK_ECOMM 1100      /* RCCL error: ARCTOPK_ECOMM + ncclResult_t */
 
 /* error-feedback modes (ref GroupTopKState.use_error_feedback, :149, :224-250) */
 #define ARCTOPK_EF_NONE 0
@@ -141,6 +143,23 @@ int arctopk_select_draw(const arctopk_plan* plan, const void* sketch, int32_t wo
                         uint64_t next_seed, void* next_V, void* stream);
 
 /*
+ * Phase markers of a step (arctopk_step / arctopk_exchange_step): `marks` is NULL or an array
+ * of ARCTOPK_NMARKS hipEvent_t handles; every non-NULL entry is recorded at that point (for
+ * per-phase timing; each record between two kernels idles the GPU a few microseconds).
+ * PACKED_AR and DECODE are recorded on the stream that runs them (the exchange stream when
+ * there is one).
+ */
+#define ARCTOPK_MARK_START 0      /* before the projection draw                       */
+#define ARCTOPK_MARK_DRAW 1       /* after the draw, before the encode                */
+#define ARCTOPK_MARK_ENCODE 2
+#define ARCTOPK_MARK_SKETCH_AR 3  /* exchange step only                               */
+#define ARCTOPK_MARK_SELECT 4
+#define ARCTOPK_MARK_PACK 5
+#define ARCTOPK_MARK_PACKED_AR 6  /* exchange step only                               */
+#define ARCTOPK_MARK_DECODE 7
+#define ARCTOPK_NMARKS 8
+
+/*
  * One-call step at world size 1, where both all-reduces of the hook are identities
  * (group_topk_hook_no_reshape.py:264, :280): [draw V for `seed` when draw != 0] -> encode
  * -> select (+ the next call's projections: next / next_seed, as arctopk_select_draw) ->
@@ -152,7 +171,47 @@ int arctopk_plan_bind(arctopk_plan* plan, void* sketch, int32_t* rowlist, int32_
                       void* packed, void* V);
 int arctopk_step(const arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
                  int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
-                 uint64_t next_seed, void* stream);
+                 uint64_t next_seed, void* stream, void* const* marks);
+
+/* ---- the exchange: collectives of the hook (group_topk_hook_no_reshape.py:58, :280) ---- */
+/*
+ * A communicator for the hook's SUM all-reduces: an RCCL communicator owned by this library
+ * (RCCL loaded at run time from `rccl_path`, normally the librccl.so torch itself loaded, so
+ * the process holds one RCCL), or a callback (`fn(ctx, buf, count, dtype, stream)` must
+ * all-reduce `count` elements at `buf` in place, ordered on `stream`; returns 0 or nonzero).
+ * Creating an RCCL communicator is collective: every rank calls arctopk_comm_init_rccl with
+ * the id rank 0 obtained from arctopk_comm_unique_id (128 bytes), and it blocks until all have.
+ */
+typedef struct arctopk_comm arctopk_comm;
+typedef int (*arctopk_allreduce_fn)(void* ctx, void* buf, int64_t count, int32_t dtype, void* stream);
+int arctopk_comm_unique_id(const char* rccl_path, void* id_out);
+int arctopk_comm_init_rccl(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
+                           int32_t device, arctopk_comm** out);
+int arctopk_comm_init_callback(arctopk_allreduce_fn fn, void* ctx, int32_t nranks, int32_t rank,
+                               arctopk_comm** out);
+int arctopk_comm_destroy(arctopk_comm* comm);
+int arctopk_comm_size(const arctopk_comm* comm);
+/* in-place SUM all-reduce of `count` elements (ARCTOPK_F32 / ARCTOPK_BF16), stream-ordered */
+int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t dtype, void* stream);
+
+/*
+ * One bucket call of the hook with its collectives, in one host call (world size =
+ * the communicators' size; at size 1 the all-reduces are identities but still issued):
+ *   stream  : [draw] -> encode -> all_reduce(sketch, sketch_comm) -> select (+ next V) -> pack
+ *   xstream : all_reduce(packed, packed_comm) -> decode          (xstream NULL: on `stream`)
+ * With an exchange stream the caller's stream records one device-scope event after the pack
+ * and is then free for the next bucket while this one is on the wire; the next exchange step
+ * of the same plan first orders `stream` after this decode (arctopk_plan_wait_exchange does
+ * just that; the hook's Future makes the waiter's stream wait for xstream itself).
+ * `V`: the projections to encode with (NULL: the plan's bound projection buffer, drawn there
+ * for `seed` when draw != 0).
+ * Replaces: the whole of group_topk_hook's compressed path (:254-290) given the seed.
+ */
+int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
+                          int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
+                          uint64_t next_seed, arctopk_comm* sketch_comm, arctopk_comm* packed_comm,
+                          void* stream, void* xstream, const void* V, void* const* marks);
+int arctopk_plan_wait_exchange(arctopk_plan* plan, void* stream);
 
 /*
  * K2 variant for tests/bit-exact checks: the per-row energy keys only

@@ -197,25 +197,55 @@ def test_product_host_paths_ws2():
 
 
 # ---------------------------------------------------------------------------
-def _sketch_comm_worker(rank, ws, port, td, mode):
+def _exchange_comm_worker(rank, ws, port, td, mode):
     os.environ["ARCTOPK_SKETCH_COMM"] = mode
     _setup(rank, ws, port)
+    from allreducetopk_amd import _native as N
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
     st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0)
-    world = dist.group.WORLD
-    if mode == "separate":  # created by the constructor, collectively, before any backward
-        assert st._sketch_pg is not None and st._sketch_pg is not world
-        assert st._sketch_group(world) is st._sketch_pg
-        t = torch.ones(3) * (rank + 1)
-        dist.all_reduce(t, group=st._sketch_pg)
-        assert torch.equal(t, torch.full((3,), 3.0))
-    else:
-        assert st._sketch_pg is None and st._sketch_group(world) is world
+    assert st._comms is None, "the constructor must not be collective"
+    st.init_exchange_comms("cpu")  # collective: every rank, same point (as the registry does)
+    group, _, sk, pk = st._comms
+    assert group is dist.group.WORLD and pk.kind == "callback" and pk.size == ws
+    assert (sk is not pk) == (mode == "separate")
+    if mode == "separate":
+        assert sk.group is not pk.group
+    # an all-reduce through the native communicator (libarctopk -> callback -> gloo)
+    for c in {id(sk): sk, id(pk): pk}.values():
+        t = torch.arange(6, dtype=torch.float32) * (rank + 1)
+        c.register(t)
+        c.check(N.lib().arctopk_comm_allreduce(c.handle, t.data_ptr(), 5, N.F32, None), "allreduce")
+        want = torch.arange(6, dtype=torch.float32) * 3
+        want[5] = 5 * (rank + 1)  # beyond `count`: untouched
+        assert torch.equal(t, want)
+    # an unregistered buffer is refused with the callback's own error
+    u = torch.ones(4)
+    with pytest.raises(KeyError):
+        pk.check(N.lib().arctopk_comm_allreduce(pk.handle, u.data_ptr(), 4, N.F32, None), "allreduce")
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("mode", ["separate", "shared"])
-def test_sketch_communicator_created_at_construction(mode):
-    """The hook never calls new_group: the separate sketch communicator is made by the
-    state's constructor (on every rank, as register_comm_hook_for_ddp_model does)."""
-    _spawn(_sketch_comm_worker, mode)
+def test_exchange_communicators(mode):
+    """The exchange's communicators are made by init_exchange_comms (collective; the
+    registry calls it on every rank), never by the constructor, and all-reduce through the
+    native library."""
+    _spawn(_exchange_comm_worker, mode)
+
+
+def _registry_worker(rank, ws, port, td):
+    _setup(rank, ws, port)
+    import argparse
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from allreducetopk_amd.comm_hooks.utils import add_comm_hook_args, register_comm_hook_for_ddp_model
+    p = argparse.ArgumentParser()
+    add_comm_hook_args(p)
+    p.add_argument("--seed", type=int, default=0)
+    args = p.parse_args(["--compressor", "group_topk_no_reshape", "--compress_ratio", "0.2"])
+    st = register_comm_hook_for_ddp_model(DDP(_Net()), None, args)
+    assert st._comms is not None and st._comms[3].size == ws
+    dist.destroy_process_group()
+
+
+def test_registry_creates_exchange_communicators():
+    _spawn(_registry_worker)

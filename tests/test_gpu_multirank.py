@@ -1,7 +1,13 @@
-"""Multi-rank HIP path on one MI355X: two ranks share cuda:0 over gloo (RCCL needs one
-GPU per rank; the driver's 8-GPU bench covers RCCL).  Every rank must select the same
-rows and produce the oracle's two-rank result bit for bit given those rows.  Plus the
-shipped hook inside real DDP (NCCL=RCCL, world size 1)."""
+"""Multi-rank HIP path on one MI355X.
+
+* Two ranks share cuda:0 over gloo (RCCL needs one GPU per rank): the native exchange step
+  (arctopk_exchange_step) runs with its all-reduces routed through gloo, so the orchestration
+  every rank runs at N > 1 is the one tested.  Every rank must select the same rows and
+  produce the oracle's two-rank result bit for bit given those rows; including the hook
+  inside a real two-rank DDP model on cuda:0.
+* The forced exchange at world size 1 over one-rank RCCL communicators: the same native
+  step with RCCL, buckets in flight, in DDP.
+"""
 import os
 import sys
 import tempfile
@@ -31,16 +37,13 @@ def _worker(rank, ws, port, td, ef, kind):
     from oracle import sparse as S
     dev = "cuda:0"
     n = bucket_numel(MIX)
-    if kind == "arc_pipe":  # force the pipelined pack / all-reduce / decode on the caller's stream
-        G.BucketPlan.PIPELINE_MIN_BYTES = 64
+    sync = kind == "arc_sync"  # the exchange without an exchange stream (all on the caller's)
+    if sync:
         kind = "arc"
-        pipe = True
-    else:
-        pipe = False
     if kind == "arc":
         st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                               use_error_feedback=ef, seed=77)
-        st.async_exchange = not pipe
+        st.async_exchange = not sync
         ost = A.OracleState(seed=77)
     else:
         st = SH.SparseState(None, compress_ratio=0.2, start_compress_iter=0, sparse_type="tensor",
@@ -67,8 +70,7 @@ def _worker(rank, ws, port, td, ef, kind):
             plan = st._plans[0][1]
             rl = plan.rowlist.cpu()
             rows = [rl[s.sel_off:s.sel_off + s.k_rows].long() for s in plan.segments]
-            if G.BucketPlan.PIPELINE_MIN_BYTES == 64:
-                assert len(plan.groups) > 1, "pipelined path not exercised"
+            assert st._comms is not None and st._comms[3].size == ws  # the exchange step ran
             other = [torch.empty_like(rl) for _ in range(ws)]
             dist.all_gather(other, rl)
             assert torch.equal(other[0], other[1]), "ranks selected different rows"
@@ -101,7 +103,7 @@ def _worker(rank, ws, port, td, ef, kind):
 
 
 @pytest.mark.parametrize("kind,ef", [("arc", "noef"), ("arc", "ef14"), ("arc", "ef21"),
-                                     ("arc_pipe", "ef14"), ("arc_pipe", "ef21"),
+                                     ("arc_sync", "ef14"), ("arc_sync", "ef21"),
                                      ("topk", "ef14"), ("topk", "ef21"), ("randk", "ef14")])
 def test_two_ranks_one_gpu(kind, ef):
     from parity import free_port
@@ -135,7 +137,6 @@ def _worker_multi(rank, ws, port, ef, sketch_comm, steps):
     st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                           use_error_feedback=ef, seed=31)
     assert st.async_exchange
-    assert (st._sketch_pg is not None) == (sketch_comm == "separate")
     ost = A.OracleState(seed=31)
     order = [2, 1, 0]
     E = {b: None for b in order}
@@ -154,6 +155,9 @@ def _worker_multi(rank, ws, port, ef, sketch_comm, steps):
         outs = {b: futs[b].wait() for b in order}  # the caller's stream waits for each decode
         torch.cuda.synchronize()
         assert st.iter == step + 1
+        if st._comms is not None:  # (EF21's first backward is the dense init: no exchange yet)
+            sk, pk = st._comms[2], st._comms[3]
+            assert (sk is not pk) == (sketch_comm == "separate") and pk.kind == "callback"
         for b in order:
             shapes = MULTI[b]
             if ef == "ef21" and E[b] is None:  # dense init call (no seed drawn)
@@ -179,6 +183,7 @@ def _worker_multi(rank, ws, port, ef, sketch_comm, steps):
             if ef == "ef21":
                 assert torch.equal(st.global_error_dict[b].cpu(), res["gE_new"]), f"step{step} bucket{b} gE"
                 gE[b] = res["gE_new"]
+    assert st._comms is not None
     dist.destroy_process_group()
 
 
@@ -189,72 +194,194 @@ def test_two_ranks_buckets_in_flight(ef, sketch_comm):
     mp.spawn(_worker_multi, args=(2, free_port(), ef, sketch_comm, 3), nprocs=2, join=True)
 
 
-def test_hook_inside_ddp_rccl():
-    """group_topk_hook registered on a real DDP model (RCCL backend, world size 1): every
-    bucket of every compressed backward is captured before the hook, replayed through the
-    oracle with the rows the device selected, and the gradients DDP hands the parameters
-    must equal the oracle's output bit for bit (the reference's check_grad_identity intent,
+class _DdpNet(torch.nn.Module):
+    """Conv (ND, m = 18), linear weights (2-D) and biases (1-D): several DDP buckets at a
+    0.5 MB cap (1.2 MB + 1.05 MB of linear weights)."""
+
+    def __init__(self):
+        super().__init__()
+        self.body = torch.nn.Sequential(torch.nn.Conv2d(3, 16, 3), torch.nn.ReLU(), torch.nn.Flatten(),
+                                        torch.nn.Linear(16 * 6 * 6, 512), torch.nn.ReLU(),
+                                        torch.nn.Linear(512, 512), torch.nn.ReLU(),
+                                        torch.nn.Linear(512, 10))
+
+    def forward(self, x):
+        return self.body(x)
+
+
+def _ddp_check(model, st, ost, ws, rank, ef, steps, x, flips_ok=2):
+    """Run `steps` backwards of DDP(model) with group_topk_hook; every compressed bucket's
+    input (all ranks) and residuals are captured before the hook, replayed through the
+    oracle's ws-rank simulation with the rows the device selected, and the gradients DDP
+    hands the parameters (after its finalize waited the hook's Future) must equal the
+    oracle's output bit for bit (the reference's check_grad_identity intent,
     glue_fine-tuning/run_glue_no_trainer_new.py:78-98, made exact)."""
-    from parity import ensure_group
-    ensure_group("nccl")
-    from torch.nn.parallel import DistributedDataParallel as DDP
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
     from oracle import arctopk as A
     from parity import check_rows_tie_aware
-    torch.manual_seed(0)
-    net = torch.nn.Sequential(torch.nn.Conv2d(3, 16, 3), torch.nn.ReLU(), torch.nn.Flatten(),
-                              torch.nn.Linear(16 * 6 * 6, 512), torch.nn.ReLU(),
-                              torch.nn.Linear(512, 512), torch.nn.ReLU(),
-                              torch.nn.Linear(512, 10)).cuda()
-    # 1.2 MB + 1.05 MB of linear weights: several buckets per backward at a 0.5 MB cap
-    model = DDP(net, device_ids=[0], bucket_cap_mb=0.5)
-    st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=1,
-                          use_error_feedback="ef14", seed=3)
-    ost = A.OracleState(seed=3)
     calls = []
+
+    def gather(t):
+        if ws == 1:
+            return [t]
+        parts = [torch.empty_like(t) for _ in range(ws)]
+        dist.all_gather(parts, t)
+        return parts
 
     def hook(state, bucket):
         it = state.iter
         b = bucket.index()
         E = state.error_dict.get(b)
-        rec = dict(b=b, it=it, G=bucket.buffer().detach().clone().cpu(),
-                   E=None if E is None else E.detach().clone().cpu(),
+        gE = state.global_error_dict.get(b)
+        rec = dict(b=b, it=it, G=gather(bucket.buffer().detach().clone().cpu()),
+                   E=None if E is None else gather(E.detach().clone().cpu()),
+                   gE=None if gE is None else gE.detach().clone().cpu(),
                    shapes=[tuple(t.shape) for t in bucket.gradients()],
                    params=list(bucket.parameters()))
         fut = G.group_topk_hook(state, bucket)
         if it >= state.start_compress_iter:
-            plan = state._plans[b][1]
-            rec["plan"] = plan
+            rec["plan"] = state._plans[b][1]
         calls.append(rec)
         return fut
 
     model.register_comm_hook(st, hook)
-    x = torch.randn(8, 3, 8, 8, device="cuda")
     flips = 0
-    for step in range(4):
+    checked = 0
+    for step in range(steps):
         model.zero_grad()
         start = len(calls)
         model(x).pow(2).mean().backward()
         torch.cuda.synchronize()
         step_calls = calls[start:]
-        assert len({c["b"] for c in step_calls}) >= 2 or step == 0
+        assert len({c["b"] for c in step_calls}) >= 2 or step == 0  # (DDP rebuilds its buckets after step 0)
         for c in step_calls:
-            if c["it"] < st.start_compress_iter:
+            if c["it"] < st.start_compress_iter or (ef == "ef21" and c["E"] is None):
                 continue
             seed = ost.next_seed()
             plan = c["plan"]
             rl = plan.rowlist.cpu()
-            rows = [rl[s.sel_off:s.sel_off + s.k_rows].long() for s in plan.segments]
-            res = A.simulate_step([c["G"]], [c["E"]], None, c["shapes"], 0.2, 4, "ef14", seed,
-                                  rows_override=rows, proj_device="cuda:0")
-            for r_, nrm, s in zip(rows, res["norms"], plan.segments):
-                flips += check_rows_tie_aware(r_, nrm, int(s.k_rows), band=2e-4)
+            rows = [rl[s_.sel_off:s_.sel_off + s_.k_rows].long() for s_ in plan.segments]
+            first = ef == "ef14" and c["E"] is None
+            res = A.simulate_step(c["G"], [None] * ws if (ef == "noef" or first) else c["E"], c["gE"],
+                                  c["shapes"], 0.2, 4, ef, seed, rows_override=rows, proj_device="cuda:0")
+            for r_, nrm, s_ in zip(rows, res["norms"], plan.segments):
+                flips += check_rows_tie_aware(r_, nrm, int(s_.k_rows), band=2e-4)
             off = 0
             for p, shp in zip(c["params"], c["shapes"]):
                 nel = p.numel()
                 assert torch.equal(p.grad.detach().flatten().cpu(), res["out"][off:off + nel]), \
-                    f"step{step} bucket{c['b']} param grad differs from the oracle"
+                    f"rank{rank} step{step} bucket{c['b']} param grad differs from the oracle"
                 off += nel
-            assert torch.equal(st.error_dict[c["b"]].cpu(), res["E_new"][0])
-    assert st.iter == 4
-    assert flips <= 2, f"{flips} rows differ from the oracle's selection (near-ties only)"
+            if ef != "noef":
+                assert torch.equal(st.error_dict[c["b"]].cpu(), res["E_new"][rank])
+            if ef == "ef21":
+                assert torch.equal(st.global_error_dict[c["b"]].cpu(), res["gE_new"])
+            checked += 1
+    assert st.iter == steps
+    assert checked >= 2 * (steps - st.start_compress_iter - (ef == "ef21"))
+    assert flips <= flips_ok, f"{flips} rows differ from the oracle's selection (near-ties only)"
+
+
+@pytest.mark.parametrize("force_exchange", [False, True])
+def test_hook_inside_ddp_rccl(force_exchange):
+    """The shipped hook registered on a real DDP model (RCCL backend, world size 1): the
+    one-call step, and the forced exchange (the N > 1 code path: one-rank RCCL communicators,
+    exchange stream, device-aware Future through the Reducer's finalize)."""
+    from parity import ensure_group
+    ensure_group("nccl")
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
+    from oracle import arctopk as A
+    torch.manual_seed(0)
+    model = DDP(_DdpNet().cuda(), device_ids=[0], bucket_cap_mb=0.5)
+    st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=1,
+                          use_error_feedback="ef14", seed=3)
+    st.force_exchange = force_exchange
+    x = torch.randn(8, 3, 8, 8, device="cuda")
+    _ddp_check(model, st, A.OracleState(seed=3), 1, 0, "ef14", 4, x)
+    if force_exchange:
+        assert st._comms is not None and st._comms[3].kind == "rccl" and st._comms[3].size == 1
+
+
+def _ddp_two_ranks_worker(rank, ws, port, ef):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, HERE)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
+    from oracle import arctopk as A
+    torch.manual_seed(0)
+    model = DDP(_DdpNet().cuda(), device_ids=[0], bucket_cap_mb=0.5)
+    st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=1,
+                          use_error_feedback=ef, seed=9)
+    assert st.async_exchange
+    x = torch.randn(8, 3, 8, 8, generator=torch.Generator().manual_seed(50 + rank)).cuda()
+    _ddp_check(model, st, A.OracleState(seed=9), ws, rank, ef, 4, x)
+    assert st._comms[3].kind == "callback" and st._comms[3].size == ws
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ef", ["ef14", "ef21"])
+def test_hook_inside_ddp_two_ranks(ef):
+    """Two DDP ranks on cuda:0 (gloo): the exchange step with its exchange-stream decode
+    and device-aware Future through the Reducer's finalize, every parameter gradient vs the
+    two-rank oracle."""
+    from parity import free_port
+    mp.spawn(_ddp_two_ranks_worker, args=(2, free_port(), ef), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize("ef,sketch_comm", [("ef14", "separate"), ("ef21", "separate"),
+                                            ("ef14", "shared"), ("noef", "separate")])
+def test_forced_exchange_buckets_in_flight(ef, sketch_comm):
+    """The N > 1 code path at world size 1: one-rank RCCL communicators (both sketch modes),
+    three buckets per backward hooked before any Future is waited (each bucket's packed
+    all-reduce and decode on the exchange stream beside the next bucket's encode), three
+    backwards; every output, E and gE vs the oracle bit for bit given the rows."""
+    from parity import ensure_group
+    ensure_group("nccl")
+    from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
+    from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
+    from oracle import arctopk as A
+    st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
+                          use_error_feedback=ef, seed=41)
+    st.force_exchange = True
+    st.sketch_comm = sketch_comm
+    ost = A.OracleState(seed=41)
+    order = [2, 1, 0]
+    E = {b: None for b in order}
+    gE = {b: None for b in order}
+    dev = "cuda:0"
+    for step in range(3):
+        ins, futs = {}, {}
+        for b in order:
+            shapes = MULTI[b]
+            Gl = torch.randn(bucket_numel(shapes), generator=torch.Generator().manual_seed(7000 * step + b))
+            ins[b] = Gl
+            futs[b] = G.group_topk_hook(st, SyntheticBucket(Gl.to(dev), shapes, index=b, is_last=(b == 0)))
+        outs = {b: futs[b].wait() for b in order}
+        torch.cuda.synchronize()
+        if st._comms is not None:  # (EF21's first backward is the dense init: no exchange yet)
+            sk, pk = st._comms[2], st._comms[3]
+            assert pk.kind == "rccl" and pk.size == 1 and (sk is not pk) == (sketch_comm == "separate")
+        for b in order:
+            shapes = MULTI[b]
+            if ef == "ef21" and E[b] is None:
+                E[b] = [ins[b].clone()]
+                gE[b] = ins[b].clone()
+                assert torch.equal(outs[b].cpu(), gE[b])
+                continue
+            seed = ost.next_seed()
+            plan = st._plans[b][1]
+            rl = plan.rowlist.cpu()
+            rows = [rl[s_.sel_off:s_.sel_off + s_.k_rows].long() for s_ in plan.segments]
+            first = ef == "ef14" and E[b] is None
+            res = A.simulate_step([ins[b]], [None] if (ef == "noef" or first) else E[b], gE[b], shapes, 0.2, 4,
+                                  ef, seed, rows_override=rows, proj_device=dev)
+            assert torch.equal(outs[b].cpu(), res["out"]), f"step{step} bucket{b} output"
+            if ef != "noef":
+                assert torch.equal(st.error_dict[b].cpu(), res["E_new"][0])
+                E[b] = res["E_new"]
+            if ef == "ef21":
+                assert torch.equal(st.global_error_dict[b].cpu(), res["gE_new"])
+                gE[b] = res["gE_new"]
