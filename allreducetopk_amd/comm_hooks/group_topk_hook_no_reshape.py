@@ -338,8 +338,11 @@ class GroupTopKState(HookState):
         # projection H2D on a copy stream (event-ordered) or in order on the caller's stream
         self.v_copy_side_stream = os.environ.get("ARCTOPK_V_COPY", "side") != "main"
         self._copy_streams: Dict[int, torch.cuda.Stream] = {}
-        self._xstreams: Dict[int, torch.cuda.Stream] = {}
-        self._x_outstanding = set()  # devices whose exchange stream may hold unwaited decodes
+        self._ar_streams: Dict[int, torch.cuda.Stream] = {}   # packed all-reduces
+        self._side_streams: Dict[int, torch.cuda.Stream] = {}  # host-staged copies
+        # the overlapped step whose decode is deferred to the next call (at most one):
+        # (plan, its Future, its markers, bucket tensor, stream handle)
+        self._x_pend = None
         # Sketch all-reduces on a communicator of their own ("separate") or on the packed
         # values' communicator ("shared": a sketch then queues behind the previous bucket's
         # packed all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
@@ -432,6 +435,21 @@ class GroupTopKState(HookState):
         device = torch.device(device)
         sk, pk = X.make_comms(group, device, self.sketch_comm)
         self._comms = (group, device, sk, pk)
+
+    def flush_exchange(self) -> None:
+        """Enqueue the deferred decode of the last overlapped exchange step (on the stream
+        of that call) and complete its Future.  The hook does this itself at the next call;
+        a Python wait()/value() on that Future does it too."""
+        pend, self._x_pend = self._x_pend, None
+        if pend is None:
+            return
+        plan, fut, marks, t, sid = pend
+        N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
+        fut.set_result(t)
+
+    def state_dict(self) -> dict:
+        self.flush_exchange()  # the deferred decode writes gE (EF21)
+        return super().state_dict()
 
     def _exchange_comms(self, group, dev):
         if self._comms is None:
@@ -577,16 +595,30 @@ def _call_marks(state, names):
     return arr
 
 
+class ExchangeFuture(torch.futures.Future):
+    """The Future of an overlapped exchange step, whose decode is deferred to the next hook
+    call.  It completes once that decode is enqueued on the caller's
+    stream (the reference's completed-Future semantics from then on).  wait() / value() from
+    Python enqueue the decode first, so a caller that waits before its next hook call never
+    blocks; DDP waits (from C++) only in its finalize, after the backward's last bucket,
+    whose call runs inline and leaves nothing deferred."""
+
+    def wait(self):
+        if not self.done():
+            self._arctopk_state.flush_exchange()
+        return super().wait()
+
+    def value(self):
+        if not self.done():
+            self._arctopk_state.flush_exchange()
+        return super().value()
+
+
 def _order_after_exchange(state, dev) -> None:
     """Before a collective on the torch process group (warm-up, EF21 init, phase path): the
-    caller's stream waits for the exchange stream's outstanding decodes, so collectives of
-    this library's communicators and of torch's are never in flight together."""
-    dix = torch.device(dev).index or 0
-    if dix in state._x_outstanding:
-        xs = state._xstreams.get(dix)
-        if xs is not None:
-            torch.cuda.current_stream(dev).wait_stream(xs)
-        state._x_outstanding.discard(dix)
+    deferred decode is enqueued (its stream then follows the last packed all-reduce), so
+    collectives of this library's communicators and of torch's are never in flight together."""
+    state.flush_exchange()
 
 
 def _host_projections(state, plan, bucket, seed, dtype, dev, stream):
@@ -664,7 +696,7 @@ def _current_raw_stream(device_index: int) -> int:
 # always had to wait for the copy (~17 us idle per call).  A high-priority stream gets a
 # queue of its own: the copy is seen complete a call later and no wait is needed.
 COPY_PRIORITY = -1
-# The exchange stream runs the packed all-reduce and the decode beside the next bucket's
+# The exchange streams run the packed all-reduce and the decode beside the next bucket's
 # encode: high priority, so RCCL's blocks are dispatched ahead of the encode's queued blocks.
 XSTREAM_PRIORITY = -1
 HOST_TIMES = {} if os.environ.get("ARCTOPK_HOST_TIMING") == "1" else None
@@ -765,7 +797,7 @@ def _stage_through_host(state: GroupTopKState, pv: torch.Tensor, stream, dev,
         state._host_buf = torch.empty(n, dtype=pv.dtype, pin_memory=True)
     hb = state._host_buf[:n]
     d2h = state._side_stream(state._copy_streams, dev, COPY_PRIORITY)
-    h2d = state._side_stream(state._xstreams, dev)
+    h2d = state._side_stream(state._side_streams, dev)
     d2h.wait_stream(stream)
     h2d.wait_stream(stream)
     step = max(1, -(-n // chunks))
@@ -791,7 +823,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
 
     # warm-up: dense all-reduce for the first start_compress_iter iterations (:213-215)
     if state.iter < state.start_compress_iter:
-        if state._x_outstanding:
+        if state._x_pend is not None:
             _order_after_exchange(state, input_tensor.device)
         state.maybe_increase_iter(bucket)
         return default_hooks._allreduce_fut(group, input_tensor, state)
@@ -816,7 +848,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             logger.info("A tensor of length %s that represents local/global error is created.", total)
             state.error_dict[b] = torch.clone(input_tensor).detach()
             state.comm_bits_this_round += tensor_bits(input_tensor)
-            if state._x_outstanding:
+            if state._x_pend is not None:
                 _order_after_exchange(state, input_tensor.device)
             dist.all_reduce(input_tensor, group=group, async_op=False)
             input_tensor.div_(world_size)
@@ -864,19 +896,28 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         else:
             vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, torch.cuda.current_stream(dev))
             vptr = V.data_ptr()
-        xs = state._side_stream(state._xstreams, dev, XSTREAM_PRIORITY) if state.async_exchange else None
-        if xs is not None and pk.kind == "callback" and xs.cuda_stream not in pk._streams:
-            pk.known_stream(xs)
+        # overlapped (packed all-reduce on the all-reduce stream, decode deferred to the next
+        # call) except for the last bucket of a backward: nothing follows it to overlap, so it
+        # runs inline, after the previous bucket's decode, and leaves nothing in flight
+        overlap = state.async_exchange and not bucket.is_last()
+        ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY) if overlap else None
+        if ars is not None and pk.kind == "callback" and ars.cuda_stream not in pk._streams:
+            pk.known_stream(ars)
+        prev = state._x_pend
+        state._x_pend = None
         marks = _call_marks(state, _EXCHANGE_MARKS)
         st_ = L.arctopk_exchange_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
                                       int(err_in), int(draw), seed,
                                       nplan.handle if nplan is not None else None, nseed, sk.handle,
-                                      pk.handle, sid, xs.cuda_stream if xs is not None else None, vptr,
-                                      marks)
+                                      pk.handle, sid, ars.cuda_stream if ars is not None else None,
+                                      prev[0].handle if prev is not None else None,
+                                      prev[2] if prev is not None else None, vptr, marks)
         if st_:
             for c in (sk, pk):
                 c.check(st_, "arctopk_exchange_step")
             N.check(st_, "arctopk_exchange_step")
+        if prev is not None:  # its decode is now enqueued (on this call's stream)
+            prev[1].set_result(prev[3])
         if nplan is not None:
             nplan.v_drawn, nplan.v_stream = nseed, sid
         if vslot >= 0:
@@ -884,19 +925,18 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         _ht("exchange_step")
         state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
         state.maybe_increase_iter(bucket)
-        if xs is None:
+        if overlap:
+            fut = ExchangeFuture()
+            fut._arctopk_state = state
+            state._x_pend = (plan, fut, marks, input_tensor, sid)
+        else:
             fut = torch.futures.Future()
-            fut.set_result(input_tensor)
-            return fut
-        state._x_outstanding.add(dix)
-        input_tensor.record_stream(xs)
-        # a device-aware Future: wait()/value() make the waiter's stream wait for the decode
-        fut = torch.futures.Future(devices=[dev])
-        with torch.cuda.stream(xs):
             fut.set_result(input_tensor)
         _ht("tail")
         return fut
 
+    if state._x_pend is not None:  # (force_exchange was switched off mid-backward)
+        state.flush_exchange()
     if device_v and world_size == 1 and not state.host_staged:
         # world size 1: the whole step in one native call (arctopk_step: [draw] -> encode ->
         # select + the next call's projections -> pack -> decode); both all-reduces are

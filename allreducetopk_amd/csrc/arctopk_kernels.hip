@@ -7,6 +7,7 @@
 //
 // All kernels are HBM-streaming except K2 (latency-bound, a few KiB per segment).
 // Reference: comm_hooks/group_topk_hook_no_reshape.py (see include/arctopk.h).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -2849,20 +2850,35 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
     return (int)hipGetLastError();
 }
 
+// `done`: an event the launch itself completes (hipExtLaunchKernelGGL's stop event, carried
+// by the kernel's own completion signal): another stream can wait for the pack without a
+// marker packet on this stream (a marker between two kernels idles the GPU ~12 us)
+template <typename T, int EF>
+void pack_launch(dim3 grid, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
+                 const T* grad, T* err, const int32_t* rowlist, const int32_t* slotmap, T* packed) {
+    if (done)
+        hipExtLaunchKernelGGL((k_pack<T, EF>), grid, dim3(256), 0, st, nullptr, done, 0, segs, ch, grad, err,
+                              rowlist, slotmap, packed);
+    else
+        hipLaunchKernelGGL((k_pack<T, EF>), grid, dim3(256), 0, st, segs, ch, grad, err, rowlist, slotmap,
+                           packed);
+}
+
 template <typename T>
 int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* err_, int32_t ef,
-                const int32_t* rowlist, const int32_t* slotmap, void* packed_, hipStream_t st) {
+                const int32_t* rowlist, const int32_t* slotmap, void* packed_, hipStream_t st,
+                hipEvent_t done = nullptr) {
     const T* grad = static_cast<const T*>(grad_);
     T* err = static_cast<T*>(err_);
     T* packed = static_cast<T*>(packed_);
-    dim3 grid(c1 - c0), block(256);
+    dim3 grid(c1 - c0);
     const Chunk* ch = p->d_pack + c0;
     if (ef == ARCTOPK_EF_NONE)
-        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF_NONE>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
+        pack_launch<T, ARCTOPK_EF_NONE>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
     else if (ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF14>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
+        pack_launch<T, ARCTOPK_EF14>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
     else if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL((k_pack<T, ARCTOPK_EF21>), grid, block, 0, st, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
+        pack_launch<T, ARCTOPK_EF21>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -2957,6 +2973,23 @@ extern "C" int arctopk_pack(const arctopk_plan* p, const void* grad, void* err, 
     if (!p) return ARCTOPK_EINVAL;
     return arctopk_pack_segments(p, 0, p->nseg, grad, err, ef, rowlist, slotmap, packed, stream);
 }
+
+namespace arctopk {
+// arctopk_pack whose kernel completes `done` (exchange.cpp)
+int pack_signal(const arctopk_plan* p, const void* grad, void* err, int32_t ef, const int32_t* rowlist,
+                const int32_t* slotmap, void* packed, void* stream, void* done) {
+    if (!p || !rowlist || !slotmap || !packed || !done) return ARCTOPK_EINVAL;
+    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF_NONE ? !grad : !err) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF21 && !grad) return ARCTOPK_EINVAL;
+    const int c0 = p->h_pack_begin[0], c1 = p->h_pack_begin[p->nseg];
+    if (c1 == c0) return (int)hipEventRecord((hipEvent_t)done, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    if (p->dtype == ARCTOPK_BF16)
+        return launch_pack<bf16_t>(p, c0, c1, grad, err, ef, rowlist, slotmap, packed, st, (hipEvent_t)done);
+    return launch_pack<float>(p, c0, c1, grad, err, ef, rowlist, slotmap, packed, st, (hipEvent_t)done);
+}
+}  // namespace arctopk
 
 extern "C" int arctopk_decode_segments(const arctopk_plan* p, int32_t seg_begin, int32_t seg_end,
                                        const void* packed, const int32_t* slotmap, int32_t ws,

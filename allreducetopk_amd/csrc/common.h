@@ -335,6 +335,13 @@ struct arctopk_plan {
     void* b_packed;
     void* b_V;
     void* x_ev_packed;                  // exchange step (exchange.cpp): packed values ready,
-    void* x_ev_done;                    // ... and this bucket's exchange-stream decode done
-    int x_pending;                      // x_ev_done recorded and not yet known complete
+    void* x_ev_ar;                      // ... and their all-reduce done
+    int x_deferred;                     // a decode waits for arctopk_exchange_finish, on:
+    void* x_bucket;                     //   the bucket,
+    void* x_gerr;                       //   the global residual (EF21),
+    int x_ef, x_ws;                     //   the EF mode and world size of that call
 };
+namespace arctopk {
+int pack_signal(const arctopk_plan* p, const void* grad, void* err, int32_t ef, const int32_t* rowlist,
+                const int32_t* slotmap, void* packed, void* stream, void* done);
+}

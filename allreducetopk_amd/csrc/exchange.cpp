@@ -2,17 +2,17 @@
 // collectives included, enqueued by ONE host call.
 //
 // The reference blocks on two NCCL all-reduces per bucket (group_topk_hook_no_reshape.py:58
-// per tensor, :280 for the packed values).  Here the whole call is stream-ordered:
+// per tensor, :280 for the packed values).  Here every call is stream-ordered:
 //
-//   caller's stream : [draw V] -> encode -> all_reduce(sketch) -> select (+ next V) -> pack
-//                     -> record(packed_ready)
-//   exchange stream : wait(packed_ready) -> all_reduce(packed) -> decode -> record(done)
+//   caller's stream   : [draw V] -> encode -> all_reduce(sketch) -> select (+ next V) -> pack
+//                       -> decode of the PREVIOUS bucket (after its all-reduce)
+//   all-reduce stream : all_reduce(packed)          (waits for the pack kernel's own signal)
 //
-// so the caller's stream is free for the next bucket's encode while this bucket's packed
-// values are on the wire (one event record on the caller's stream per bucket).  The next
-// call on the same bucket orders itself after `done` (the bucket, E, gE and the packed buffer
-// are rewritten).  Without an exchange stream every phase runs in order on the caller's
-// stream.
+// so the packed values of bucket b are on the wire while the caller's stream encodes,
+// selects and packs bucket b+1; the decode of b then follows on the caller's stream, where
+// it does not compete with the next encode for HBM and needs no event of its own.  The last
+// bucket of a backward runs inline (its all-reduce and decode on the caller's stream, after
+// the previous bucket's decode): nothing is left in flight when the hook returns for it.
 //
 // Collectives go through an arctopk_comm: an RCCL communicator this library owns (RCCL is
 // resolved at run time from the library torch itself loaded, so the process holds one RCCL),
@@ -162,10 +162,10 @@ inline int mark(void* const* marks, int i, hipStream_t st) {
     return (int)hipEventRecord((hipEvent_t)marks[i], st);
 }
 
-int ensure_event(void** ev) {
+int ensure_event(void** ev, unsigned flags) {
     if (*ev) return 0;
     hipEvent_t e = nullptr;
-    const hipError_t st = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice);
+    const hipError_t st = hipEventCreateWithFlags(&e, flags);
     if (st != hipSuccess) return (int)st;
     *ev = e;
     return 0;
@@ -173,33 +173,39 @@ int ensure_event(void** ev) {
 
 }  // namespace
 
-// The caller's stream waits for this plan's last exchange-stream decode, if the host does
-// not already see it complete (a wait packet between two kernels idles the GPU).
-extern "C" int arctopk_plan_wait_exchange(arctopk_plan* p, void* stream) {
+// The deferred decode of plan p's last exchange step, on `stream`: after that step's packed
+// all-reduce (a stream wait only when the host does not already see it complete).
+extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* const* marks) {
     if (!p) return ARCTOPK_EINVAL;
-    if (!p->x_pending) return 0;
-    const hipError_t q = hipEventQuery((hipEvent_t)p->x_ev_done);
+    if (!p->x_deferred) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const hipError_t q = hipEventQuery((hipEvent_t)p->x_ev_ar);
     if (q == hipErrorNotReady) {
-        const hipError_t w = hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)p->x_ev_done, 0);
+        const hipError_t w = hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
         if (w != hipSuccess) return (int)w;
     } else if (q != hipSuccess) {
         return (int)q;
     }
-    p->x_pending = 0;
-    return 0;
+    int e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
+    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, stream);
+    if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
+    if (!e) p->x_deferred = 0;
+    return e;
 }
 
 extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, void* gerr, int32_t ef,
                                      int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
                                      uint64_t next_seed, arctopk_comm* sketch_comm, arctopk_comm* packed_comm,
-                                     void* stream, void* xstream, const void* V, void* const* marks) {
+                                     void* stream, void* ar_stream, arctopk_plan* prev, void* const* prev_marks,
+                                     const void* V, void* const* marks) {
     if (!p || !bucket || !p->b_sketch || !sketch_comm || !packed_comm) return ARCTOPK_EINVAL;
     if (sketch_comm->nranks != packed_comm->nranks) return ARCTOPK_EINVAL;
     if (next && (!next->b_sketch || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
-    if (xstream == stream) xstream = nullptr;
+    if (ar_stream && ar_stream == stream) return ARCTOPK_EINVAL;
     const int ws = packed_comm->nranks;
-    hipStream_t st = (hipStream_t)stream, xs = (hipStream_t)xstream;
-    int e = arctopk_plan_wait_exchange(p, stream);
+    hipStream_t st = (hipStream_t)stream, as = (hipStream_t)ar_stream;
+    // this bucket's own previous decode, if a caller never finished it (the hook always does)
+    int e = arctopk_exchange_finish(p, stream, nullptr);
     if (!e) e = mark(marks, ARCTOPK_MARK_START, st);
     if (!V) V = p->b_V;
     if (!e && draw && p->info.v_len > 0) e = arctopk_draw_projections(p, seed, const_cast<void*>(V), stream);
@@ -213,27 +219,38 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk_select_draw(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
                                 next ? next->b_V : nullptr, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_SELECT, st);
-    if (!e) e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
+    if (e) return e;
+    if (!as) {  // inline: the previous bucket's decode, then this bucket's exchange, all on `stream`
+        e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
+        if (!e) e = mark(marks, ARCTOPK_MARK_PACK, st);
+        if (!e && prev && prev != p) e = arctopk_exchange_finish(prev, stream, prev_marks);
+        // the index-free all-reduce of the packed values (:280)
+        if (!e) e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
+        if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
+        if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream);
+        if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
+        return e;
+    }
+    // overlapped: the pack kernel completes x_ev_packed itself (no marker packet on the
+    // caller's stream, where one idles the GPU ~12 us); the all-reduce stream waits for it
+    if ((e = ensure_event(&p->x_ev_packed, 0)) ||
+        (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
+        return e;
+    e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream, p->x_ev_packed);
     if (!e) e = mark(marks, ARCTOPK_MARK_PACK, st);
     if (e) return e;
-    hipStream_t ds = st;  // the stream of the packed all-reduce and the decode
-    if (xs) {
-        if ((e = ensure_event(&p->x_ev_packed)) || (e = ensure_event(&p->x_ev_done))) return e;
-        hipError_t he = hipEventRecord((hipEvent_t)p->x_ev_packed, st);
-        if (he == hipSuccess) he = hipStreamWaitEvent(xs, (hipEvent_t)p->x_ev_packed, 0);
-        if (he != hipSuccess) return (int)he;
-        ds = xs;
-    }
-    // the index-free all-reduce of the packed values (:280)
-    e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, ds);
-    if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, ds);
-    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, ds);
-    if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, ds);
+    hipError_t he = hipStreamWaitEvent(as, (hipEvent_t)p->x_ev_packed, 0);
+    if (he != hipSuccess) return (int)he;
+    e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, as);
     if (e) return e;
-    if (xs) {
-        const hipError_t he = hipEventRecord((hipEvent_t)p->x_ev_done, xs);
-        if (he != hipSuccess) return (int)he;
-        p->x_pending = 1;
-    }
-    return 0;
+    he = hipEventRecord((hipEvent_t)p->x_ev_ar, as);
+    if (he != hipSuccess) return (int)he;
+    p->x_deferred = 1;
+    p->x_bucket = bucket;
+    p->x_gerr = gerr;
+    p->x_ef = ef;
+    p->x_ws = ws;
+    // the previous bucket's decode (its all-reduce ran beside this bucket's encode)
+    if (prev && prev != p) e = arctopk_exchange_finish(prev, stream, prev_marks);
+    return e;
 }

@@ -368,7 +368,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     delete[] p->h_segs;
     delete[] p->h_pack_begin;
     if (p->x_ev_packed) (void)hipEventDestroy((hipEvent_t)p->x_ev_packed);
-    if (p->x_ev_done) (void)hipEventDestroy((hipEvent_t)p->x_ev_done);
+    if (p->x_ev_ar) (void)hipEventDestroy((hipEvent_t)p->x_ev_ar);
     delete[] p->h_large_batches;
     if (p->d_large_batches) (void)hipFree(p->d_large_batches);
     if (p->d_mws) (void)hipFree(p->d_mws);

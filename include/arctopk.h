@@ -196,22 +196,29 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
 
 /*
  * One bucket call of the hook with its collectives, in one host call (world size =
- * the communicators' size; at size 1 the all-reduces are identities but still issued):
- *   stream  : [draw] -> encode -> all_reduce(sketch, sketch_comm) -> select (+ next V) -> pack
- *   xstream : all_reduce(packed, packed_comm) -> decode          (xstream NULL: on `stream`)
- * With an exchange stream the caller's stream records one device-scope event after the pack
- * and is then free for the next bucket while this one is on the wire; the next exchange step
- * of the same plan first orders `stream` after this decode (arctopk_plan_wait_exchange does
- * just that; the hook's Future makes the waiter's stream wait for xstream itself).
- * `V`: the projections to encode with (NULL: the plan's bound projection buffer, drawn there
- * for `seed` when draw != 0).
+ * the communicators' size; at size 1 the all-reduces are identities but still issued).
+ * Overlapped (ar_stream given):
+ *   stream    : [draw] -> encode -> all_reduce(sketch, sketch_comm) -> select (+ next V) -> pack
+ *               -> arctopk_exchange_finish(prev): the previous step's decode
+ *   ar_stream : all_reduce(packed, packed_comm), after the pack kernel (which completes the
+ *               event the stream waits for: no marker packet on `stream`)
+ *   This step's own decode is deferred to arctopk_exchange_finish(plan, ...) -- the next step's
+ *   `prev`, or an explicit call -- so the caller's stream encodes the next bucket while these
+ *   packed values are on the wire, and the decode never competes with an encode for HBM.
+ * Inline (ar_stream NULL): pack -> finish(prev) -> all_reduce(packed) -> decode, on `stream`
+ *   (the last bucket of a backward: nothing is left in flight).
+ * `prev_marks` are the markers of prev's step (its PACKED_AR / DECODE are recorded by the
+ * finish).  `V`: the projections to encode with (NULL: the plan's bound projection buffer,
+ * drawn there for `seed` when draw != 0).
  * Replaces: the whole of group_topk_hook's compressed path (:254-290) given the seed.
  */
 int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
                           int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
                           uint64_t next_seed, arctopk_comm* sketch_comm, arctopk_comm* packed_comm,
-                          void* stream, void* xstream, const void* V, void* const* marks);
-int arctopk_plan_wait_exchange(arctopk_plan* plan, void* stream);
+                          void* stream, void* ar_stream, arctopk_plan* prev, void* const* prev_marks,
+                          const void* V, void* const* marks);
+/* The deferred decode of `plan`'s last overlapped exchange step, on `stream` (no-op if none). */
+int arctopk_exchange_finish(arctopk_plan* plan, void* stream, void* const* marks);
 
 /*
  * K2 variant for tests/bit-exact checks: the per-row energy keys only

@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/x1
-timeout -k 10 400 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 120 --timeout-method thread > gpurun_out/x1/pytest.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_multirank.py ${PYTEST_ARGS} -x -v --timeout 120 --timeout-method thread > gpurun_out/x1/pytest.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR" gpurun_out/x1/pytest.log | tail -20
 if [ $rc -ne 0 ]; then grep -E "Error|assert|Traceback" -A3 gpurun_out/x1/pytest.log | head -60; exit $rc; fi

@@ -239,7 +239,7 @@ def _ddp_check(model, st, ost, ws, rank, ef, steps, x, flips_ok=2):
                    shapes=[tuple(t.shape) for t in bucket.gradients()],
                    params=list(bucket.parameters()))
         fut = G.group_topk_hook(state, bucket)
-        if it >= state.start_compress_iter:
+        if it >= state.start_compress_iter and b in state._plans:  # (not on EF21's dense init)
             rec["plan"] = state._plans[b][1]
         calls.append(rec)
         return fut
