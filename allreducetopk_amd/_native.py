@@ -91,10 +91,11 @@ _SIGS = {
     "arctopk_sparse_gather": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
                                         POINTER(c_int64), c_void_p, c_void_p, c_int32, c_void_p]),
     "arctopk_sparse_residual": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
-                                          POINTER(c_int64), c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+                                          POINTER(c_int64), c_void_p, c_void_p, c_int32, c_float, c_int32,
+                                          c_void_p]),
     "arctopk_sparse_decode": (c_int32, [c_void_p, c_int64, c_int32, POINTER(c_int64), POINTER(c_int64),
                                         POINTER(c_int64), c_int64, c_void_p, c_void_p, c_int32, c_int32,
-                                        c_int32, c_void_p, c_int32, c_void_p]),
+                                        c_int32, c_void_p, c_float, c_int32, c_void_p]),
     "arctopk_ef_apply": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p]),
     "arctopk_draw_bf16_normal": (c_int32, [c_uint64, c_int64, c_void_p]),
     "arctopk_draw_normal": (c_int32, [c_uint64, c_int32, c_int32, POINTER(c_int64), c_void_p]),

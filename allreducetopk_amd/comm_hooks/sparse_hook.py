@@ -104,11 +104,6 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
         # (both constructors hard-code False)
         raise NotImplementedError("the large_batch_init EF21 path is not implemented by the "
                                   "MI355X codec")
-    if state.use_error_feedback == "ef21" and state.error_decay != 1.0:
-        # the reference scales the EF21 residual updates by error_decay (sparse_hook.py:265,
-        # :296); the fused kernels implement the default error_decay = 1.0 only
-        raise NotImplementedError(f"error_decay={state.error_decay} (EF21 residual scaling) is "
-                                  "not implemented by the MI355X codec; only 1.0")
     state.maybe_accumulate_momentum_on_bucket(bucket)
     group = state.process_group if state.process_group is not None else dist.group.WORLD
     world_size = group.size()
@@ -133,6 +128,8 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
     stream = torch.cuda.current_stream(device).cuda_stream
     ef = N.EF_CODE[state.use_error_feedback]
     dt = N.DTYPE_CODE[dtype]
+    # EF21 residual scaling: E += error_decay * C(D), gE += error_decay * out (:265, :296)
+    decay = float(state.error_decay)
 
     if ef == N.EF14:
         err_in = b in state.error_dict
@@ -213,7 +210,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
     state.last_indices, state.last_k = indices, ks
     if ef != N.EF_NONE and not (fold14 and not state.random):  # residual persistence (:257-267)
         N.check(L.arctopk_sparse_residual(state.error_dict[b].data_ptr(), nt, a_off, a_k, a_ko,
-                                          indices.data_ptr(), values.data_ptr(), ef, dt, stream),
+                                          indices.data_ptr(), values.data_ptr(), ef, decay, dt, stream),
                 "arctopk_sparse_residual")
     gerr = state.global_error_dict[b].data_ptr() if ef == N.EF21 else None
 
@@ -222,7 +219,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
         if world_size > 1:
             dist.all_reduce(values, group=group, async_op=False)
         N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, indices.data_ptr(),
-                                        values.data_ptr(), 1, world_size, 0, gerr, dt, stream),
+                                        values.data_ptr(), 1, world_size, 0, gerr, decay, dt, stream),
                 "arctopk_sparse_decode")
     else:
         state.comm_bits_this_round += (world_size - 1) * world_size * bits_sum
@@ -235,7 +232,7 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
             all_vals, all_idx = values, indices
         N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, all_idx.data_ptr(),
                                         all_vals.data_ptr(), world_size, world_size, 1, gerr,
-                                        dt, stream), "arctopk_sparse_decode")
+                                        decay, dt, stream), "arctopk_sparse_decode")
 
     state.maybe_increase_iter(bucket)
     fut = torch.futures.Future()

@@ -357,235 +357,6 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     }
 }
 
-// Sum each of R per-lane values over the 64 lanes of a wave.  R = 4: halving exchange (2 +
-// 1 + 4 = 7 cross-lane steps instead of 4 x 6); afterwards lane 16 * j holds sum j
-// (j = 2 * (lane >> 5) + ((lane >> 4) & 1)).  Generic R: every lane holds every sum.
-template <int R>
-__device__ __forceinline__ void wave_sum_r(float (&a)[R], int lane) {
-    if constexpr (R == 4) {
-        const bool hi = lane >= 32;
-        float k0 = hi ? a[2] : a[0], k1 = hi ? a[3] : a[1];
-        const float s0 = hi ? a[0] : a[2], s1 = hi ? a[1] : a[3];
-        k0 += __shfl_xor(s0, 32, 64);
-        k1 += __shfl_xor(s1, 32, 64);
-        const bool odd = (lane & 16) != 0;
-        float c = odd ? k1 : k0;
-        c += __shfl_xor(odd ? k0 : k1, 16, 64);
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        a[0] = c;
-    } else {
-#pragma unroll
-        for (int j = 0; j < R; ++j) a[j] = wave_sum(a[j]);
-    }
-}
-
-// K1 encode, wave-per-row tiles (ENC_ROW_VEC: m and the offset 16-B aligned), in a launch of
-// its own so the register budget is this loop's alone.  A wave streams a whole row (up to
-// 64 * kEncRowUnits 16-B units per pass) with every load of the pass issued before its first
-// use, stores E := X with nontemporal stores, and forms the R dot products from V^T in LDS;
-// the other waves of the CU cover the latency (occupancy, not double buffers).
-#ifndef ARCTOPK_ENC_ROW_UNITS
-#define ARCTOPK_ENC_ROW_UNITS 8
-#endif
-#ifndef ARCTOPK_ENC_ROW_WPE
-#define ARCTOPK_ENC_ROW_WPE 4
-#endif
-constexpr int kEncRowUnits = ARCTOPK_ENC_ROW_UNITS;
-#ifndef ARCTOPK_ENC_ROW_UNITS_BF16
-#define ARCTOPK_ENC_ROW_UNITS_BF16 4  // tuning switch (A/B builds): a bf16 unit is 8 elements
-#endif
-constexpr int kEncRowUnitsBf16 = ARCTOPK_ENC_ROW_UNITS_BF16;
-template <typename T, int R, int EF, bool ERR_IN>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ARCTOPK_ENC_ROW_WPE)))
-k_encode_rows(const SegDev* __restrict__ segs, const EncTile* __restrict__ tiles,
-              const T* __restrict__ G, T* __restrict__ E, const T* __restrict__ V,
-              T* __restrict__ sketch, float* __restrict__ part_buf) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const EncTile t = tiles[blockIdx.x];
-    const SegDev s = segs[t.seg];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr bool WRITE_E = (EF == ARCTOPK_EF14);
-    constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
-    constexpr int PQ = kQuadsPer16<T>;
-    constexpr int U = sizeof(T) == 2 ? kEncRowUnitsBf16 : kEncRowUnits;
-    const int m = (int)s.m;
-    const int c0 = t.c0, cl = t.clen;
-    const T* __restrict__ Vs = V + s.v_off;
-    if constexpr (R == 4) {
-        for (int c = tid; c < cl; c += 256) {
-            const float4 v = ldq<T, false>(Vs, c0 + c);
-            lds[c] = v.x;
-            lds[cl + c] = v.y;
-            lds[2 * cl + c] = v.z;
-            lds[3 * cl + c] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < R; ++j)
-            for (int c = tid; c < cl; c += 256) lds[j * cl + c] = to_f(Vs[(int64_t)(c0 + c) * R + j]);
-    }
-    __syncthreads();
-    T* const sk_out = sketch + s.sketch_off;
-    float* const pt_out = t.part < 0 ? nullptr : part_buf + s.part_off + (int64_t)t.part * s.n * R;
-    const int m4 = cl >> 2;
-    const int mu = m4 / PQ;
-    const float4* vt4 = reinterpret_cast<const float4*>(lds);
-    // the row's R sums, reduced over the wave, to the sketch (or a column part's partials)
-    auto put_row = [&](int64_t row, float (&acc)[R]) {
-        wave_sum_r<R>(acc, lane);
-        if constexpr (R == 4) {
-            if ((lane & 15) == 0) {
-                const int j = ((lane >> 5) << 1) | ((lane >> 4) & 1);
-                if (pt_out) pt_out[row * R + j] = acc[0];
-                else st1<T>(sk_out + row * R + j, acc[0]);
-            }
-        } else {
-            if (lane < R) {
-                float v = acc[0];
-#pragma unroll
-                for (int j = 1; j < R; ++j)
-                    if (lane == j) v = acc[j];
-                if (pt_out) pt_out[row * R + lane] = v;
-                else st1<T>(sk_out + row * R + lane, v);
-            }
-        }
-    };
-    const int upr = (mu + 63) >> 6;  // 64-unit groups of one row
-    if (sizeof(T) == 2 && 2 * upr <= U) {
-        // Rows that fill at most half the units (bf16 rows of <= 4 K elements, fp32 of <= 2 K):
-        // a wave streams TWO rows per pass (its rows q and q + 4), so each lane keeps the
-        // same bytes in flight as on a full-width fp32 row (one row per pass left the bf16
-        // headline encode at 3.9 TB/s)
-        constexpr int H = U / 2;
-        for (int64_t q = wave; q < t.nrows; q += 8) {
-            const bool has_b = q + 4 < t.nrows;
-            const int64_t ra = t.row0 + q * t.rstride, rb = t.row0 + (q + 4) * t.rstride;
-            const T* gp[2] = {G + s.offset + ra * m + c0, G + s.offset + rb * m + c0};
-            T* ep[2] = {E + s.offset + ra * m + c0, E + s.offset + rb * m + c0};
-            u4_t g[U], e[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int uu = u % H, hb = u / H;
-                if (uu < upr && (hb == 0 || has_b)) {  // wave-uniform
-                    const int c = min(uu * 64 + lane, mu - 1);
-                    g[u] = ld16raw<T, true>(gp[hb], c);
-                    if constexpr (LOAD_E) e[u] = ld16raw<T, true>(ep[hb], c);
-                }
-            }
-            float acc[2][R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) acc[0][j] = acc[1][j] = 0.f;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int uu = u % H, hb = u / H;
-                if (uu < upr && (hb == 0 || has_b)) {
-                    const int cu = uu * 64 + lane;
-                    const bool ok = cu < mu;
-                    const int c = ok ? cu : mu - 1;
-                    float4 x[PQ], eq[PQ];
-                    unpack16<T>(g[u], x);
-                    if constexpr (LOAD_E) unpack16<T>(e[u], eq);
-#pragma unroll
-                    for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(x[h], LOAD_E ? eq[h] : x[h]);
-                    if constexpr (WRITE_E) {
-                        if (ok) st16<T, true>(ep[hb], c, x);
-                    }
-                    if (!ok) {
-#pragma unroll
-                        for (int h = 0; h < PQ; ++h) x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-#pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        float a = acc[hb][j];
-#pragma unroll
-                        for (int h = 0; h < PQ; ++h) {
-                            const float4 v = vt4[j * m4 + c * PQ + h];
-                            a = fmaf(x[h].x, v.x, a);
-                            a = fmaf(x[h].y, v.y, a);
-                            a = fmaf(x[h].z, v.z, a);
-                            a = fmaf(x[h].w, v.w, a);
-                        }
-                        acc[hb][j] = a;
-                    }
-                }
-            }
-            put_row(ra, acc[0]);
-            if (has_b) put_row(rb, acc[1]);
-        }
-        return;
-    }
-    for (int64_t q = wave; q < t.nrows; q += 4) {
-        const int64_t row = t.row0 + q * t.rstride;
-        const T* gp = G + s.offset + row * m + c0;
-        T* ep = E + s.offset + row * m + c0;
-        float acc[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) acc[j] = 0.f;
-        for (int cb = 0; cb < mu; cb += 64 * U) {
-            u4_t g[U], e[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (cb + u * 64 < mu) {  // wave-uniform: no loads past the row
-                    const int c = min(cb + u * 64 + lane, mu - 1);
-                    g[u] = ld16raw<T, true>(gp, c);
-                    if constexpr (LOAD_E) e[u] = ld16raw<T, true>(ep, c);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (cb + u * 64 < mu) {
-                    const int cu = cb + u * 64 + lane;
-                    const bool ok = cu < mu;
-                    const int c = ok ? cu : mu - 1;
-                    float4 x[PQ], eq[PQ];
-                    unpack16<T>(g[u], x);
-                    if constexpr (LOAD_E) unpack16<T>(e[u], eq);
-#pragma unroll
-                    for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(x[h], LOAD_E ? eq[h] : x[h]);
-                    if constexpr (WRITE_E) {
-                        if (ok) st16<T, true>(ep, c, x);
-                    }
-                    if (!ok) {
-#pragma unroll
-                        for (int h = 0; h < PQ; ++h) x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-#pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        float a = acc[j];
-#pragma unroll
-                        for (int h = 0; h < PQ; ++h) {
-                            const float4 v = vt4[j * m4 + c * PQ + h];
-                            a = fmaf(x[h].x, v.x, a);
-                            a = fmaf(x[h].y, v.y, a);
-                            a = fmaf(x[h].z, v.z, a);
-                            a = fmaf(x[h].w, v.w, a);
-                        }
-                        acc[j] = a;
-                    }
-                }
-            }
-        }
-        wave_sum_r<R>(acc, lane);
-        if constexpr (R == 4) {
-            if ((lane & 15) == 0) {
-                const int j = ((lane >> 5) << 1) | ((lane >> 4) & 1);
-                if (pt_out) pt_out[row * R + j] = acc[0];
-                else st1<T>(sk_out + row * R + j, acc[0]);
-            }
-        } else {
-            if (lane < R) {
-                float v = acc[0];
-#pragma unroll
-                for (int j = 1; j < R; ++j)
-                    if (lane == j) v = acc[j];
-                if (pt_out) pt_out[row * R + lane] = v;
-                else st1<T>(sk_out + row * R + lane, v);
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // K2 select
 // ---------------------------------------------------------------------------
@@ -2638,22 +2409,6 @@ __global__ void __launch_bounds__(256) k_sketch_combine(const SegDev* __restrict
 template <typename T, int R>
 int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
                     hipStream_t st) {
-    if (p->n_enc_rows > 0) {  // wave-per-row tiles
-        dim3 grid(p->n_enc_rows), block(256);
-        const size_t lds = (size_t)p->enc_rows_lds_bytes;
-        const EncTile* tiles = p->d_enc_rows;
-        float* pb = p->d_part;
-        if (ef == ARCTOPK_EF_NONE)
-            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-        else if (ef == ARCTOPK_EF14 && err_in)
-            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-        else if (ef == ARCTOPK_EF14)
-            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-        else
-            hipLaunchKernelGGL((k_encode_rows<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
-        const int e = (int)hipGetLastError();
-        if (e) return e;
-    }
     if (p->n_enc > 0) {
         dim3 grid(p->n_enc), block(256);
         const size_t lds = (size_t)p->enc_lds_bytes;
@@ -2729,10 +2484,7 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
     if (p->n_small && !ARCTOPK_DIAG_NOSMALL && p->n_large_batches == 0) {
         // one block per segment: 1024 threads once a segment has more than 4096 rows (the
         // radix rounds and the compaction are per-block latency chains)
-        static const int64_t big_rows = [] {  // tuning switch (A/B): rows for 1024 threads
-            const char* env = std::getenv("ARCTOPK_SEL_BIG_ROWS");
-            return env ? std::max<int64_t>(1, std::atoll(env)) : (int64_t)4096;
-        }();
+        constexpr int64_t big_rows = ARCTOPK_SEL_BIG_ROWS;  // rows for 1024 threads (build-time A/B)
         const dim3 grid(p->n_small + job.n);
         static_assert(((kSmallSelRows + 3) & ~3) * 4 + 16 <= kRefineLdsCap * 4, "small-select keys fit the LDS cap");
         if (p->small_lds > 48 * 1024) {  // > 48 KiB of keys: the dynamic LDS attribute
@@ -2761,18 +2513,11 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         // few blocks, since each block merges its histogram with memory-side atomics on the
         // same hot words (measured on ResNet-50's bucket: 1120 x 256-thread blocks spent ~10 us
         // in that merge tail)
-        static const int keys_threads = [] {  // tuning switch (A/B): key-pass block size
-            const char* env = std::getenv("ARCTOPK_KEYS_THREADS");
-            return env && std::atoi(env) == 256 ? 256 : 1024;
-        }();
-        static const int64_t target_blocks = [] {  // tuning switch (A/B): key-pass grid target
-            const char* env = std::getenv("ARCTOPK_KEYS_BLOCKS");  // 1024-thread blocks: ~one
-            return env ? std::max(1, std::atoi(env)) : 224;  // per CU fits (263 did not: 2 rounds)
-        }();
-        static const int64_t min_rpb = [] {  // tuning switch (A/B): rows per block at least
-            const char* env = std::getenv("ARCTOPK_KEYS_MIN_ROWS");
-            return env ? std::max(256, std::atoi(env)) : 4096;
-        }();
+        // (build-time A/B switches: key-pass block size; grid target -- 1024-thread blocks:
+        // ~one per CU fits, 263 did not: 2 rounds; rows per block at least)
+        constexpr int keys_threads = ARCTOPK_KEYS_THREADS == 256 ? 256 : 1024;
+        constexpr int64_t target_blocks = ARCTOPK_KEYS_BLOCKS;
+        constexpr int64_t min_rpb = ARCTOPK_KEYS_MIN_ROWS;
         int64_t rows = 0;
         for (int i = 0; i < b.cnt; ++i) rows += b.it[i].n;
         const int64_t rpb = std::max<int64_t>(min_rpb, (rows + target_blocks - 1) / target_blocks);
@@ -2798,10 +2543,7 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
         // items of at most kFuseMaxRows rows: the refine runs inside the write blocks (one
         // launch fewer)
-        static const bool fuse_ok = [] {  // tuning switch (A/B): ARCTOPK_FUSED_WRITE=0 disables
-            const char* env = std::getenv("ARCTOPK_FUSED_WRITE");
-            return !(env && std::atoi(env) == 0);
-        }();
+        constexpr bool fuse_ok = ARCTOPK_FUSED_WRITE != 0;  // build-time A/B switch
         int nflat = 0;
         for (int i = 0; i < b.cnt; ++i) nflat += b.it[i].nranges;
         // ... and only while every write block is resident at once: each one now carries a

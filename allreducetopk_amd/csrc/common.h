@@ -19,6 +19,46 @@
 #define DIAG_STAMP(arr, i) do {} while (0)
 #endif
 
+// Build-time A/B switches (build(defines=[...]) makes variants; the product library has
+// no run-time tuning knobs).  Selects:
+#ifndef ARCTOPK_SEL_BIG_ROWS
+#define ARCTOPK_SEL_BIG_ROWS 4096      // single-block select: 1024 threads above this many rows
+#endif
+#ifndef ARCTOPK_KEYS_THREADS
+#define ARCTOPK_KEYS_THREADS 1024      // multi-block select key pass: block size (256 or 1024)
+#endif
+#ifndef ARCTOPK_KEYS_BLOCKS
+#define ARCTOPK_KEYS_BLOCKS 224        // ... grid target per batch
+#endif
+#ifndef ARCTOPK_KEYS_MIN_ROWS
+#define ARCTOPK_KEYS_MIN_ROWS 4096     // ... rows per block at least
+#endif
+#ifndef ARCTOPK_FUSED_WRITE
+#define ARCTOPK_FUSED_WRITE 1          // refine folded into the write blocks where it fits
+#endif
+#ifndef ARCTOPK_TOPK_HIST_BLOCKS
+#define ARCTOPK_TOPK_HIST_BLOCKS 1024  // TopK select: histogram blocks per batch
+#endif
+// Plans:
+#ifndef ARCTOPK_ENC_TARGET_BLOCKS
+#define ARCTOPK_ENC_TARGET_BLOCKS 2048 // encode blocks a bucket's wave-per-row work aims at
+#endif
+#ifndef ARCTOPK_PACK_CHUNK
+#define ARCTOPK_PACK_CHUNK 8192        // elements per pack chunk (rows >= 256)
+#endif
+#ifndef ARCTOPK_DEC_CHUNK
+#define ARCTOPK_DEC_CHUNK 8192         // elements per decode chunk (rows >= 256)
+#endif
+#ifndef ARCTOPK_STREAM_PACK_CHUNK
+#define ARCTOPK_STREAM_PACK_CHUNK 2048 // elements per m <= 2 stream-pack chunk
+#endif
+#ifndef ARCTOPK_SHORT_DEC_CHUNK
+#define ARCTOPK_SHORT_DEC_CHUNK 4096   // elements per short-row (m < 256) decode chunk
+#endif
+#ifndef ARCTOPK_ENC_INTERLEAVE
+#define ARCTOPK_ENC_INTERLEAVE 1       // encode row tiles interleaved (1) or contiguous ranges (0)
+#endif
+
 namespace arctopk {
 
 constexpr int kMaxR = 8;           // sketch rank supported by the kernels
@@ -31,8 +71,8 @@ constexpr int kSmallM = 64;        // m below this: thread-per-row tiles; else w
 constexpr int kVLdsMaxBytes = 64 * 1024;  // V staged in LDS up to this size, else read from L2
 constexpr int kChunkElems = 8192;  // target elements per pack/decode work chunk (8192 beat
                                    // 16384 by 3 % on the headline, one 2048-row per wave)
-constexpr int kEncTargetBlocks = 2048;  // encode blocks a bucket's wave-per-row work aims at
-                                        // (measured: 2048 beats 1024 on 256 CUs at 3 blocks/CU)
+constexpr int kEncTargetBlocks = ARCTOPK_ENC_TARGET_BLOCKS;  // (measured: 2048 beats 1024 on
+                                                              // 256 CUs at 3 blocks/CU)
 #ifndef ARCTOPK_SMALL_SEL_ROWS
 #define ARCTOPK_SMALL_SEL_ROWS 15360
 #endif
@@ -294,12 +334,9 @@ struct arctopk_plan {
     arctopk_plan_info info;
     arctopk_segment* h_segs;      // host copy
     arctopk::SegDev* d_segs;
-    arctopk::EncTile* d_enc;      // RAW / small-m / scalar-row tiles (k_encode)
+    arctopk::EncTile* d_enc;      // encode tiles (k_encode)
     int n_enc;
     int enc_lds_bytes;            // dynamic LDS of the encode launch
-    arctopk::EncTile* d_enc_rows; // 16-B aligned wave-per-row tiles (k_encode_rows)
-    int n_enc_rows;
-    int enc_rows_lds_bytes;
     float* d_part;                // partial sketches of column-split segments
     int32_t* d_split;             // ids of column-split segments
     int n_split;

@@ -608,10 +608,7 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
     uint32_t* cidx = ckey + cap_total;
     // histogram blocks per item: every block merges its LDS histogram with memory-side
     // atomics on the same hot words, so the batch's total is capped (tuning switch)
-    static const int64_t hist_total = [] {
-        const char* env = std::getenv("ARCTOPK_TOPK_HIST_BLOCKS");
-        return env ? std::max(1, std::atoi(env)) : 1024;  // headline TopK: 387 -> 404 GB/s (512: 399, 2048: 387)
-    }();
+    constexpr int64_t hist_total = ARCTOPK_TOPK_HIST_BLOCKS;  // headline TopK: 387 -> 404 GB/s (512: 399, 2048: 387)
     const int hb = (int)std::max<int64_t>(
         1, std::min<int64_t>(std::min<int64_t>(kMHistBlocks, (maxn + 8191) / 8192), hist_total / cnt));
     const dim3 gh(hb, cnt), gt(gr, cnt), gflat(total_ranges(b));

@@ -12,11 +12,6 @@
 
 using namespace arctopk;
 
-#ifndef ARCTOPK_ENC_ROWS_KERNEL
-#define ARCTOPK_ENC_ROWS_KERNEL 0  // A/B switch: 1 = row tiles in k_encode_rows (measured 2-4 us slower)
-#endif
-constexpr bool kEncRowsKernel = ARCTOPK_ENC_ROWS_KERNEL != 0;
-
 namespace {
 
 int build_segments(const int64_t* dims, const int32_t* ndims, int32_t ntensors, int r, double ratio,
@@ -103,8 +98,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     std::vector<SegDev> dsegs(segs.size());
     std::vector<int32_t> small_ids, large_ids, split_ids;
     int64_t small_rows = 0;
-    std::vector<EncTile> enc, enc_rows;
-    int rows_lds = 0;
+    std::vector<EncTile> enc;
     std::vector<Chunk> pack, dec;
     std::vector<int32_t> pack_begin, dec_begin;
     int lds = 0;
@@ -116,20 +110,15 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     for (const arctopk_segment& s : segs)
         if (s.kind != ARCTOPK_SEG_RAW && !(s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536))
             row_work += s.n * s.m;
-    int64_t target = kEncTargetBlocks;
-    if (const char* env = std::getenv("ARCTOPK_ENC_TARGET_BLOCKS")) target = std::max(1, std::atoi(env));  // tuning
+    const int64_t target = kEncTargetBlocks;
     const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(8192, row_work / target));
-    int64_t pack_elems = kChunkElems, dec_elems = kChunkElems;  // tuning switches (A/B)
-    // short rows (m < 256) and the m <= 2 streams: smaller chunks, more blocks in flight
-    // (ResNet-50 1x1 mix, 2048-element stream pack chunks: 346 -> 356 GB/s; 4096-element
-    // decode chunks: +3 %; rows of >= 256 elements keep kChunkElems)
-    int64_t stream_pack_elems = 2048, short_dec_elems = 4096;
-    if (const char* env = std::getenv("ARCTOPK_PACK_CHUNK")) pack_elems = std::max(64, std::atoi(env));
-    if (const char* env = std::getenv("ARCTOPK_DEC_CHUNK")) dec_elems = std::max(64, std::atoi(env));
-    if (const char* env = std::getenv("ARCTOPK_STREAM_PACK_CHUNK")) stream_pack_elems = std::max(64, std::atoi(env));
-    if (const char* env = std::getenv("ARCTOPK_SHORT_DEC_CHUNK")) short_dec_elems = std::max(64, std::atoi(env));
-    bool interleave = true;  // tuning switch (A/B): interleaved row tiles vs contiguous ranges
-    if (const char* env = std::getenv("ARCTOPK_ENC_INTERLEAVE")) interleave = std::atoi(env) != 0;
+    // chunk sizes (build-time A/B switches, common.h): short rows (m < 256) and the m <= 2
+    // streams get smaller chunks, more blocks in flight (ResNet-50 1x1 mix, 2048-element
+    // stream pack chunks: 346 -> 356 GB/s; 4096-element decode chunks: +3 %)
+    constexpr int64_t pack_elems = ARCTOPK_PACK_CHUNK, dec_elems = ARCTOPK_DEC_CHUNK;
+    constexpr int64_t stream_pack_elems = ARCTOPK_STREAM_PACK_CHUNK;
+    constexpr int64_t short_dec_elems = ARCTOPK_SHORT_DEC_CHUNK;
+    constexpr bool interleave = ARCTOPK_ENC_INTERLEAVE != 0;  // interleaved row tiles
     int64_t part_len = 0, split_rows_max = 0;
     // vector paths: 16-B encode units (4 fp32 / 8 bf16 elements) need m and the offset to be
     // multiples of va; pack / decode quads need 4
@@ -183,7 +172,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             for (int part = 0; part < nparts; ++part) {
                 const int64_t c0 = part * clen;
                 const int64_t cl = std::min<int64_t>(clen, s.m - c0);
-                std::vector<EncTile>& dst = (mode == ENC_ROW_VEC && kEncRowsKernel) ? enc_rows : enc;
+                std::vector<EncTile>& dst = enc;
                 for (int64_t ti = 0; ti < ntiles; ++ti) {
                     if (interleave)  // rows ti, ti + ntiles, ...: consecutive blocks, adjacent rows
                         dst.push_back(EncTile{(int32_t)i, mode, ti, (s.n - ti + ntiles - 1) / ntiles,
@@ -193,8 +182,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                         dst.push_back(EncTile{(int32_t)i, mode, ti * per, std::min(per, s.n - ti * per),
                                               (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1, 1});
                 }
-                int& l = (mode == ENC_ROW_VEC && kEncRowsKernel) ? rows_lds : lds;
-                l = std::max<int>(l, (int)(cl * r * 4));
+                lds = std::max<int>(lds, (int)(cl * r * 4));
             }
         }
         // ---- pack chunks: selected rows, ~kChunkElems elements each (small m: at most
@@ -244,8 +232,6 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     p->h_segs = new arctopk_segment[segs.size()];
     std::copy(segs.begin(), segs.end(), p->h_segs);
     p->n_enc = (int)enc.size();
-    p->n_enc_rows = (int)enc_rows.size();
-    p->enc_rows_lds_bytes = rows_lds;
     p->n_pack = (int)pack.size();
     p->n_dec = (int)dec.size();
     pack_begin.push_back((int32_t)pack.size());
@@ -268,7 +254,6 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     } while (0)
     ALLOC_COPY(p->d_segs, dsegs);
     ALLOC_COPY(p->d_enc, enc);
-    ALLOC_COPY(p->d_enc_rows, enc_rows);
     ALLOC_COPY(p->d_pack, pack);
     ALLOC_COPY(p->d_dec, dec);
     ALLOC_COPY(p->d_small, small_ids);
@@ -357,7 +342,6 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     (void)hipSetDevice(p->device);
     if (p->d_segs) (void)hipFree(p->d_segs);
     if (p->d_enc) (void)hipFree(p->d_enc);
-    if (p->d_enc_rows) (void)hipFree(p->d_enc_rows);
     if (p->d_pack) (void)hipFree(p->d_pack);
     if (p->d_dec) (void)hipFree(p->d_dec);
     if (p->d_keys) (void)hipFree(p->d_keys);

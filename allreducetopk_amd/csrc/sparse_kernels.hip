@@ -82,17 +82,20 @@ __global__ void __launch_bounds__(256) k_gather(SparseBatch b, const T* __restri
         vals[b.koff[t] + j] = xs[idx[b.koff[t] + j]];
 }
 
+// EF21: E[i] = E[i] + decay * v, one rounding (torch's add_(C, alpha) on CPU: a fused
+// multiply-add per element, sparse_hook.py:265; decay = 1 gives E[i] + v exactly)
 template <typename T, int EF>
 __global__ void __launch_bounds__(256) k_residual(SparseBatch b, T* __restrict__ E,
                                                   const int32_t* __restrict__ idx,
-                                                  const T* __restrict__ vals) {
+                                                  const T* __restrict__ vals, float decay) {
     const int t = blockIdx.y;
     const int64_t k = b.k[t];
     T* es = E + b.off[t];
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
         const int32_t i = idx[b.koff[t] + j];
         if constexpr (EF == ARCTOPK_EF14) es[i] = arctopk::from_f<T>(0.f);
-        else es[i] = arctopk::from_f<T>(arctopk::to_f(es[i]) + arctopk::to_f(vals[b.koff[t] + j]));
+        else
+            es[i] = arctopk::from_f<T>(__fmaf_rn(decay, arctopk::to_f(vals[b.koff[t] + j]), arctopk::to_f(es[i])));
     }
 }
 
@@ -172,16 +175,18 @@ __global__ void __launch_bounds__(256) k_scatter_first(SparseBatch b, T* __restr
     for (int64_t e = threadIdx.x; e < c1 - c0; e += 256) o[e] = chunk[e];
 }
 
+// TopK's out /= ws; EF21: gE = gE + decay * out (one rounding, as torch's add_ with alpha,
+// sparse_hook.py:296), out = gE
 template <typename T>
 __global__ void __launch_bounds__(256) k_div_gE(T* __restrict__ out, T* __restrict__ gE,
-                                                int64_t n, float wsf, int do_div) {
+                                                int64_t n, float wsf, int do_div, float decay) {
     using arctopk::from_f;
     using arctopk::to_f;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         float v = to_f(out[i]);
         if (do_div) v = to_f(from_f<T>(__fdiv_rn(v, wsf)));
         if (gE) {
-            v = to_f(from_f<T>(to_f(gE[i]) + v));
+            v = to_f(from_f<T>(__fmaf_rn(decay, v, to_f(gE[i]))));
             gE[i] = from_f<T>(v);
         }
         out[i] = from_f<T>(v);
@@ -315,7 +320,8 @@ extern "C" int arctopk_sparse_gather(const void* x, int32_t nt, const int64_t* o
 
 extern "C" int arctopk_sparse_residual(void* E, int32_t nt, const int64_t* offsets,
                                        const int64_t* ks, const int64_t* k_off, const int32_t* idx,
-                                       const void* vals, int32_t ef, int32_t dtype, void* stream) {
+                                       const void* vals, int32_t ef, float decay, int32_t dtype,
+                                       void* stream) {
     if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF_NONE) return 0;
     if (!E || !offsets || !ks || !k_off || !idx || nt < 1) return ARCTOPK_EINVAL;
@@ -333,18 +339,18 @@ extern "C" int arctopk_sparse_residual(void* E, int32_t nt, const int64_t* offse
             bf16_t* Eb = static_cast<bf16_t*>(E);
             const bf16_t* vb = static_cast<const bf16_t*>(vals);
             if (ef == ARCTOPK_EF14)
-                hipLaunchKernelGGL((k_residual<bf16_t, ARCTOPK_EF14>), grid, dim3(256), 0, st, b, Eb, idx, vb);
+                hipLaunchKernelGGL((k_residual<bf16_t, ARCTOPK_EF14>), grid, dim3(256), 0, st, b, Eb, idx, vb, decay);
             else if (ef == ARCTOPK_EF21)
-                hipLaunchKernelGGL((k_residual<bf16_t, ARCTOPK_EF21>), grid, dim3(256), 0, st, b, Eb, idx, vb);
+                hipLaunchKernelGGL((k_residual<bf16_t, ARCTOPK_EF21>), grid, dim3(256), 0, st, b, Eb, idx, vb, decay);
             else
                 return ARCTOPK_EINVAL;
         } else {
             float* Ef = static_cast<float*>(E);
             const float* vf = static_cast<const float*>(vals);
             if (ef == ARCTOPK_EF14)
-                hipLaunchKernelGGL((k_residual<float, ARCTOPK_EF14>), grid, dim3(256), 0, st, b, Ef, idx, vf);
+                hipLaunchKernelGGL((k_residual<float, ARCTOPK_EF14>), grid, dim3(256), 0, st, b, Ef, idx, vf, decay);
             else if (ef == ARCTOPK_EF21)
-                hipLaunchKernelGGL((k_residual<float, ARCTOPK_EF21>), grid, dim3(256), 0, st, b, Ef, idx, vf);
+                hipLaunchKernelGGL((k_residual<float, ARCTOPK_EF21>), grid, dim3(256), 0, st, b, Ef, idx, vf, decay);
             else
                 return ARCTOPK_EINVAL;
         }
@@ -358,7 +364,8 @@ namespace {
 template <typename T>
 int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, const int64_t* ks,
                     const int64_t* k_off, int64_t packed_len, const int32_t* idx, const T* vals,
-                    int32_t nranks, int32_t world_size, int32_t accumulate, T* gerr, hipStream_t st) {
+                    int32_t nranks, int32_t world_size, int32_t accumulate, T* gerr, float decay,
+                    hipStream_t st) {
     // TopK (accumulate, ascending indices per tensor): rank 0's payload writes the whole
     // bucket, zeros included (k_scatter_first); the tensors tile the bucket in order
     bool tiled = accumulate != 0;
@@ -407,7 +414,7 @@ int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, c
     const bool div = accumulate && world_size > 1;
     if (div || gerr) {
         hipLaunchKernelGGL(k_div_gE<T>, dim3(grid_for(numel, 8192)), dim3(256), 0, st, out, gerr,
-                           numel, wsf, div ? 1 : 0);
+                           numel, wsf, div ? 1 : 0, decay);
     }
     return (int)hipGetLastError();
 }
@@ -417,7 +424,7 @@ extern "C" int arctopk_sparse_decode(void* out, int64_t numel, int32_t nt, const
                                      const int64_t* ks, const int64_t* k_off, int64_t packed_len,
                                      const int32_t* idx, const void* vals, int32_t nranks,
                                      int32_t world_size, int32_t accumulate, void* gerr,
-                                     int32_t dtype, void* stream) {
+                                     float decay, int32_t dtype, void* stream) {
     if (!out || !offsets || !ks || !k_off || !idx || !vals || nt < 1 || nranks < 1 ||
         world_size < 1 || numel < 0)
         return ARCTOPK_EINVAL;
@@ -427,8 +434,8 @@ extern "C" int arctopk_sparse_decode(void* out, int64_t numel, int32_t nt, const
     if (dtype == ARCTOPK_BF16)
         return sparse_decode_t<bf16_t>(static_cast<bf16_t*>(out), numel, nt, offsets, ks, k_off, packed_len, idx,
                                        static_cast<const bf16_t*>(vals), nranks, world_size, accumulate,
-                                       static_cast<bf16_t*>(gerr), st);
+                                       static_cast<bf16_t*>(gerr), decay, st);
     return sparse_decode_t<float>(static_cast<float*>(out), numel, nt, offsets, ks, k_off, packed_len, idx,
                                   static_cast<const float*>(vals), nranks, world_size, accumulate,
-                                  static_cast<float*>(gerr), st);
+                                  static_cast<float*>(gerr), decay, st);
 }

@@ -316,11 +316,12 @@ int arctopk_sparse_gather(const void* x, int32_t ntensors, const int64_t* offset
 /*
  * Residual persistence at the selected entries (sparse_hook.py:103-109, :257-267):
  *   EF14 : E[off + idx] = 0        (E already holds x = G + E_prev, see arctopk_ef_apply)
- *   EF21 : E[off + idx] += vals    (E_new = E + C(G - E); C(.) is zero elsewhere)
+ *   EF21 : E[off + idx] = E + decay * vals, one rounding (E.add_(C(G - E), alpha=error_decay),
+ *          :265; C(.) is zero elsewhere; decay = 1 is the default state)
  */
 int arctopk_sparse_residual(void* E, int32_t ntensors, const int64_t* offsets,
                             const int64_t* ks, const int64_t* k_off, const int32_t* idx,
-                            const void* vals, int32_t ef, int32_t dtype, void* stream);
+                            const void* vals, int32_t ef, float decay, int32_t dtype, void* stream);
 
 /*
  * Decode into `out` (every element written):
@@ -328,13 +329,14 @@ int arctopk_sparse_residual(void* E, int32_t ntensors, const int64_t* offsets,
  *   accumulate = 1 (TopK) : out = 0; for rank q = 0..nranks-1 in order:
  *                           out[off + idx_q[j]] += vals_q[j]; then out /= world_size (:285-292)
  * `vals`/`idx` hold nranks consecutive payloads of packed_len entries each.
- * EF21 (gerr != NULL): gE += out; out = gE (:295-297).
+ * EF21 (gerr != NULL): gE = gE + decay * out (one rounding: gE.add_(out, alpha=error_decay));
+ * out = gE (:295-297).
  */
 int arctopk_sparse_decode(void* out, int64_t numel, int32_t ntensors, const int64_t* offsets,
                           const int64_t* ks, const int64_t* k_off, int64_t packed_len,
                           const int32_t* idx, const void* vals, int32_t nranks,
-                          int32_t world_size, int32_t accumulate, void* gerr, int32_t dtype,
-                          void* stream);
+                          int32_t world_size, int32_t accumulate, void* gerr, float decay,
+                          int32_t dtype, void* stream);
 
 /*
  * EF pre-apply on a whole bucket, one pass (ARC-TopK fuses this into arctopk_encode):

@@ -123,11 +123,13 @@ def decode_topk(all_vals: List[torch.Tensor], all_idx: List[torch.Tensor], shape
 
 
 def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed: Optional[int],
-                  indices_override=None):
+                  indices_override=None, error_decay: float = 1.0):
     """One steady-state compressed call on len(Gs) ranks in one process.
 
     ``indices_override``: per rank, a list of per-tensor index tensors (RandK draws
-    made elsewhere, e.g. by the device generator).
+    made elsewhere, e.g. by the device generator).  ``error_decay``: EF21's residual scaling
+    (``E.add_(C, alpha=error_decay)``, ``gE.add_(out, alpha=error_decay)``, sparse_hook.py:265,
+    :296; sparse_hook_c4.py:311, :342).
     """
     ws = len(Gs)
     Xs, packs = [], []
@@ -149,13 +151,13 @@ def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed:
     for X, E in zip(Xs, Es):
         if ef == "ef14":
             E_new.append(X.clone())
-        elif ef == "ef21":
-            E_new.append(E + X)  # error_decay = 1.0 (sparse_hook.py:145)
+        elif ef == "ef21":  # X holds C(D): zero except the selection (:265)
+            E_new.append(E.clone().add_(X, alpha=error_decay))
         else:
             E_new.append(None)
     gE_new = None
-    if ef == "ef21":
-        gE_new = gE + out
+    if ef == "ef21":  # (:296-297)
+        gE_new = gE.clone().add_(out, alpha=error_decay)
         out = gE_new.clone()
     return dict(X=Xs, values=[p[0] for p in packs], indices=[p[1] for p in packs], ks=ks,
                 bits=packs[0][3], out=out, E_new=E_new, gE_new=gE_new)

@@ -87,6 +87,14 @@ CASES += [
          ratio=0.2, ef="ef14", ws=1, iters=4, start=1, seed=5),
     dict(name="randk_c4_gradual_ef21_ws1", hook="sparse_c4", random=True, shapes=SPARSE_MIX,
          ratio=0.1, ef="ef21", ws=1, iters=4, start=1, seed=21),
+    # EF21 residual scaling (state.error_decay, set by hand: sparse_hook.py:145 fixes 1.0;
+    # applied at :265 and :296)
+    dict(name="topk_mix_ef21_decay09_ws1", hook="sparse", random=False, shapes=SPARSE_MIX,
+         ratio=0.2, ef="ef21", ws=1, iters=3, start=0, seed=5, error_decay=0.9),
+    dict(name="topk_mix_ef21_decay07_ws2", hook="sparse", random=False, shapes=SPARSE_MIX,
+         ratio=0.2, ef="ef21", ws=2, iters=3, start=0, seed=5, error_decay=0.7),
+    dict(name="topk_c4_gradual_ef21_decay09_ws1", hook="sparse_c4", random=False, shapes=SPARSE_MIX,
+         ratio=0.2, ef="ef21", ws=1, iters=3, start=1, seed=5, error_decay=0.9),
 ]
 
 
@@ -160,6 +168,13 @@ def capture(rec):
 
 
 def make_state(case):
+    st, hook = _make_state(case)
+    if "error_decay" in case:
+        st.error_decay = case["error_decay"]
+    return st, hook
+
+
+def _make_state(case):
     if case["hook"] == "arc":
         from comm_hooks.group_topk_hook_no_reshape import GroupTopKState, group_topk_hook
         st = GroupTopKState(process_group=None, r=case["r"], compress_ratio=case["ratio"],

@@ -414,6 +414,7 @@ def _golden_ws2_worker(rank, ws, port, name):
         st = mod.SparseState(None, compress_ratio=m["ratio"], start_compress_iter=m["start"],
                              sparse_type="tensor", random=m["random"], use_error_feedback=m["ef"],
                              random_seed=m["seed"])
+        st.error_decay = m.get("error_decay", 1.0)
         hook = mod.sparse_hook_sync
     bf16 = m.get("dtype") == "bf16"
     from oracle import arctopk as A
@@ -452,7 +453,8 @@ def _golden_ws2_worker(rank, ws, port, name):
 
 
 @pytest.mark.parametrize("name", ["arc_mix_ef14_ws2", "arc_mix_ef21_ws2", "arc_warmup_ef21_ws2",
-                                  "arc_mix_noef_bf16_ws2", "topk_mix_ef14_ws2", "topk_mix_ef21_ws2"])
+                                  "arc_mix_noef_bf16_ws2", "topk_mix_ef14_ws2", "topk_mix_ef21_ws2",
+                                  "topk_mix_ef21_decay07_ws2"])
 def test_reference_ws2_golden_through_hip_hook(name):
     """(randk_mix_noef_ws2 holds CPU torch.randperm draws, which no device index source
     reproduces; RandK at ws 2 is checked against the oracle in test_two_ranks_one_gpu.)"""

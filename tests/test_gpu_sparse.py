@@ -176,6 +176,7 @@ def test_topk_golden_on_gpu(name):
     st = mod.SparseState(None, compress_ratio=m["ratio"], start_compress_iter=m["start"],
                          sparse_type="tensor", random=False, use_error_feedback=m["ef"],
                          random_seed=m["seed"])
+    st.error_decay = m.get("error_decay", 1.0)  # EF21 residual scaling (set by hand, as a driver would)
     shapes = [tuple(s) for s in m["shapes"]]
     for it in range(m["iters"]):
         out = mod.sparse_hook_sync(st, SyntheticBucket(g.t(0, it, "G").to(DEV), shapes)).wait()
@@ -183,6 +184,8 @@ def test_topk_golden_on_gpu(name):
         assert_bitwise(out, g.t(0, it, "out"), f"{name} it{it} out")
         if g.has(0, it, "E"):
             assert_bitwise(st.error_dict[0], g.t(0, it, "E"), f"{name} it{it} E")
+        if g.has(0, it, "gE"):
+            assert_bitwise(st.global_error_dict[0], g.t(0, it, "gE"), f"{name} it{it} gE")
         assert st.comm_bits_this_round == int(g.np(0, it, "bits"))
 
 

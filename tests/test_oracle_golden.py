@@ -128,7 +128,8 @@ def test_sparse_oracle_matches_reference(name):
         if random:
             seed = int(torch.randint(0, 1_000_000_000, (1,), generator=rng).item())
             assert int(g.np(0, it, "seed")[0]) == seed
-        res = S.simulate_step(Gs, Es, gE, shapes, ratio, ef, random, seed)
+        res = S.simulate_step(Gs, Es, gE, shapes, ratio, ef, random, seed,
+                              error_decay=m.get("error_decay", 1.0))
         if random:
             off = 0
             for j, s in enumerate(shapes):
