@@ -340,9 +340,12 @@ class GroupTopKState(HookState):
         self._copy_streams: Dict[int, torch.cuda.Stream] = {}
         self._ar_streams: Dict[int, torch.cuda.Stream] = {}   # packed all-reduces
         self._side_streams: Dict[int, torch.cuda.Stream] = {}  # host-staged copies
-        # the overlapped step whose decode is deferred to the next call (at most one):
-        # (plan, its Future, its markers, bucket tensor, stream handle)
-        self._x_pend = None
+        # Deferred decodes: a step's decode runs inside a later call (in
+        # that call's select launch, whose latency it hides; or, with collectives, once the
+        # packed all-reduce on the exchange stream is done), and the backward's last bucket
+        # finishes them all.  FIFO of (plan, its Future, its markers, bucket tensor, stream).
+        self.defer_decode = True
+        self._x_pend: List[tuple] = []
         # Sketch all-reduces on a communicator of their own ("separate") or on the packed
         # values' communicator ("shared": a sketch then queues behind the previous bucket's
         # packed all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
@@ -436,16 +439,16 @@ class GroupTopKState(HookState):
         sk, pk = X.make_comms(group, device, self.sketch_comm)
         self._comms = (group, device, sk, pk)
 
-    def flush_exchange(self) -> None:
-        """Enqueue the deferred decode of the last overlapped exchange step (on the stream
-        of that call) and complete its Future.  The hook does this itself at the next call;
-        a Python wait()/value() on that Future does it too."""
-        pend, self._x_pend = self._x_pend, None
-        if pend is None:
-            return
-        plan, fut, marks, t, sid = pend
-        N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
-        fut.set_result(t)
+    def flush_exchange(self, upto=None) -> None:
+        """Enqueue deferred decodes in call order (each on the stream of its call) and
+        complete their Futures: all of them, or up to and including `upto`'s.  The hook does
+        this itself in later calls; a Python wait()/value() on such a Future does it too."""
+        while self._x_pend:
+            plan, fut, marks, t, sid = self._x_pend.pop(0)
+            N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
+            fut.set_result(t)
+            if fut is upto:
+                break
 
     def state_dict(self) -> dict:
         self.flush_exchange()  # the deferred decode writes gE (EF21)
@@ -605,12 +608,12 @@ class ExchangeFuture(torch.futures.Future):
 
     def wait(self):
         if not self.done():
-            self._arctopk_state.flush_exchange()
+            self._arctopk_state.flush_exchange(upto=self)
         return super().wait()
 
     def value(self):
         if not self.done():
-            self._arctopk_state.flush_exchange()
+            self._arctopk_state.flush_exchange(upto=self)
         return super().value()
 
 
@@ -823,7 +826,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
 
     # warm-up: dense all-reduce for the first start_compress_iter iterations (:213-215)
     if state.iter < state.start_compress_iter:
-        if state._x_pend is not None:
+        if state._x_pend:
             _order_after_exchange(state, input_tensor.device)
         state.maybe_increase_iter(bucket)
         return default_hooks._allreduce_fut(group, input_tensor, state)
@@ -848,7 +851,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             logger.info("A tensor of length %s that represents local/global error is created.", total)
             state.error_dict[b] = torch.clone(input_tensor).detach()
             state.comm_bits_this_round += tensor_bits(input_tensor)
-            if state._x_pend is not None:
+            if state._x_pend:
                 _order_after_exchange(state, input_tensor.device)
             dist.all_reduce(input_tensor, group=group, async_op=False)
             input_tensor.div_(world_size)
@@ -880,15 +883,18 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
     sid = _current_raw_stream(dix)
     dtype = input_tensor.dtype
     L = _LIB[0]
-    exchange = (world_size > 1 or state.force_exchange) and not state.host_staged
-    if exchange:
-        # the code path of every rank at world size > 1: ONE native call issues the kernels
-        # and both all-reduces (arctopk_exchange_step)
-        sk, pk = state._exchange_comms(group, dev)
-        if plan.comm_registered is not pk:
-            sk.register(plan.sketch)
-            pk.register(plan.packed)
-            plan.comm_registered = pk
+    if not state.host_staged:
+        # ONE native call per bucket (arctopk_exchange_step): the kernels, the collectives at
+        # world size > 1 (or with force_exchange: the N > 1 code path over one-rank
+        # communicators), and earlier buckets' deferred decodes
+        comms = world_size > 1 or state.force_exchange
+        sk = pk = None
+        if comms:
+            sk, pk = state._exchange_comms(group, dev)
+            if plan.comm_registered is not pk:
+                sk.register(plan.sketch)
+                pk.register(plan.packed)
+                plan.comm_registered = pk
         vslot, vptr, draw, nplan, nseed = -1, None, False, None, 0
         if device_v:
             draw = _claim_projections(state, plan, seed, sid, dev)
@@ -896,28 +902,45 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         else:
             vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, torch.cuda.current_stream(dev))
             vptr = V.data_ptr()
-        # overlapped (packed all-reduce on the all-reduce stream, decode deferred to the next
-        # call) except for the last bucket of a backward: nothing follows it to overlap, so it
-        # runs inline, after the previous bucket's decode, and leaves nothing in flight
-        overlap = state.async_exchange and not bucket.is_last()
-        ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY) if overlap else None
-        if ars is not None and pk.kind == "callback" and ars.cuda_stream not in pk._streams:
-            pk.known_stream(ars)
-        prev = state._x_pend
-        state._x_pend = None
+        # deferred except for the last bucket of a backward (nothing follows it), which then
+        # finishes every earlier deferred decode: nothing is left in flight when it returns
+        defer = state.defer_decode and state.async_exchange and not bucket.is_last()
+        pend = state._x_pend
+        if any(e_[0] is plan for e_ in pend):  # (a caller that skipped buckets: finish first)
+            state.flush_exchange()
+        # the decode riding in this call's select launch: the previous bucket's without
+        # collectives, the one before it with them (its all-reduce has had a whole call to
+        # finish, so the select is not held back waiting for it)
+        depth = 2 if comms else 1
+        ride = pend.pop(0) if len(pend) >= depth else None
+        fin = pend[:] if not defer else []
+        if not defer:
+            pend.clear()
+        ars = None
+        if defer and comms:
+            ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
+            if pk.kind == "callback" and ars.cuda_stream not in pk._streams:
+                pk.known_stream(ars)
         marks = _call_marks(state, _EXCHANGE_MARKS)
+        nf = len(fin)
+        fin_plans = (N.c_void_p * max(1, nf))(*[e_[0].handle for e_ in fin])
+        fin_marks = (N.c_void_p * max(1, nf))(*[N.ctypes.cast(e_[2], N.c_void_p).value if e_[2] is not None
+                                                else None for e_ in fin])
         st_ = L.arctopk_exchange_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
                                       int(err_in), int(draw), seed,
-                                      nplan.handle if nplan is not None else None, nseed, sk.handle,
-                                      pk.handle, sid, ars.cuda_stream if ars is not None else None,
-                                      prev[0].handle if prev is not None else None,
-                                      prev[2] if prev is not None else None, vptr, marks)
+                                      nplan.handle if nplan is not None else None, nseed,
+                                      sk.handle if comms else None, pk.handle if comms else None, sid,
+                                      ars.cuda_stream if ars is not None else None, int(defer),
+                                      ride[0].handle if ride is not None else None,
+                                      ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
+                                      vptr, marks)
         if st_:
-            for c in (sk, pk):
-                c.check(st_, "arctopk_exchange_step")
+            if comms:
+                for c in (sk, pk):
+                    c.check(st_, "arctopk_exchange_step")
             N.check(st_, "arctopk_exchange_step")
-        if prev is not None:  # its decode is now enqueued (on this call's stream)
-            prev[1].set_result(prev[3])
+        for e_ in ([ride] if ride is not None else []) + fin:  # their decodes are enqueued now
+            e_[1].set_result(e_[3])
         if nplan is not None:
             nplan.v_drawn, nplan.v_stream = nseed, sid
         if vslot >= 0:
@@ -925,38 +948,20 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         _ht("exchange_step")
         state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
         state.maybe_increase_iter(bucket)
-        if overlap:
+        if defer:
             fut = ExchangeFuture()
             fut._arctopk_state = state
-            state._x_pend = (plan, fut, marks, input_tensor, sid)
+            pend.append((plan, fut, marks, input_tensor, sid))
         else:
             fut = torch.futures.Future()
             fut.set_result(input_tensor)
         _ht("tail")
         return fut
 
-    if state._x_pend is not None:  # (force_exchange was switched off mid-backward)
+    # host-staged measurement mode (packed payload through pinned host memory, NIC model):
+    # phase by phase on the caller's stream
+    if state._x_pend:
         state.flush_exchange()
-    if device_v and world_size == 1 and not state.host_staged:
-        # world size 1: the whole step in one native call (arctopk_step: [draw] -> encode ->
-        # select + the next call's projections -> pack -> decode); both all-reduces are
-        # identities (:264, :280)
-        draw = _claim_projections(state, plan, seed, sid, dev)
-        nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
-        N.check(L.arctopk_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
-                               int(err_in), int(draw), seed, nplan.handle if nplan is not None else None,
-                               nseed, sid, _call_marks(state, _STEP_MARKS)), "arctopk_step")
-        if nplan is not None:
-            nplan.v_drawn, nplan.v_stream = nseed, sid
-        _ht("step")
-        state.maybe_increase_iter(bucket)
-        fut = torch.futures.Future()
-        fut.set_result(input_tensor)
-        _ht("tail")
-        return fut
-
-    # phase by phase on the caller's stream: host projections at world size 1, and the
-    # host-staged measurement mode (packed payload through pinned host memory, NIC model)
     stream = torch.cuda.current_stream(dev)
     vslot, V = -1, plan.V_ring[0]
     if not device_v:

@@ -218,7 +218,18 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     // of one j).  Column-split tensors write per-part partial sketches, summed in fixed
     // part order by k_sketch_combine.
     const int c0 = t.c0, cl = t.clen;
-    {
+    // bf16 rows: V^T kept as bf16 pairs, X used as the packed bf16 words it is stored as, and
+    // the sketch formed by v_dot2c_f32_bf16 (two products, exact in fp32, per instruction):
+    // no unpacking of X and half the VALU instructions of the fp32-FMA form
+    constexpr bool kDot2 = sizeof(T) == 2;
+    if (kDot2 && t.mode == ENC_ROW_VEC) {
+        uint16_t* l16 = reinterpret_cast<uint16_t*>(lds);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            for (int c = tid; c < cl; c += 256)
+                l16[j * cl + c] = reinterpret_cast<const uint16_t*>(Vs)[(int64_t)(c0 + c) * R + j];
+        __syncthreads();
+    } else {
         if constexpr (R == 4) {
             for (int c = tid; c < cl; c += 256) {
                 const float4 v = ldq<T, false>(Vs, c0 + c);  // V[c0 + c][0..3]
@@ -242,14 +253,112 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         else st1<T>(sk_out + i, v);
     };
     const int64_t rs = t.rstride;
+    if constexpr (kDot2) {
+        if (t.mode == ENC_ROW_VEC) {
+            constexpr int U = 2;  // 16-B units (8 bf16) per lane per step, two buffers
+            constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
+            constexpr bool COMBINE = LOAD_E;  // x = rnd(g +- e); else x = g (already bf16)
+            const int mu = cl >> 3;           // units of this tile row (cl is a multiple of 8)
+            const int steps = (mu + 64 * U - 1) / (64 * U);
+            const u4_t* vp = reinterpret_cast<const u4_t*>(lds);  // [R][mu] units of V^T pairs
+            u4_t ga[U], ea[U], gb[U], eb[U];
+            float acc[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc[j] = 0.f;
+            auto issue = [&](u4_t (&gx)[U], u4_t (&ex)[U], int64_t r_, int st_) {
+                const T* gp = G + s.offset + r_ * m + c0;
+                const T* ep = E + s.offset + r_ * m + c0;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int c = min(st_ * 64 * U + u * 64 + lane, mu - 1);
+                    gx[u] = ld16raw<T, true>(gp, c);
+                    if constexpr (LOAD_E) ex[u] = ld16raw<T, true>(ep, c);
+                }
+            };
+            auto combine = [&](uint32_t g, uint32_t e) -> uint32_t {
+                const float gl = __uint_as_float(g << 16), gh = __uint_as_float(g & 0xFFFF0000u);
+                const float el = __uint_as_float(e << 16), eh = __uint_as_float(e & 0xFFFF0000u);
+                if constexpr (EF == ARCTOPK_EF21) return cvt_pk_bf16(gl - el, gh - eh);
+                else return cvt_pk_bf16(gl + el, gh + eh);
+            };
+            auto consume = [&](u4_t (&gx)[U], u4_t (&ex)[U], int64_t r_, int st_) {
+                T* ep = E + s.offset + r_ * m + c0;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int cu = st_ * 64 * U + u * 64 + lane;
+                    const bool ok = cu < mu;  // lanes past the row end loaded a clamped copy
+                    const int c = ok ? cu : mu - 1;
+                    u4_t x = gx[u];
+                    if constexpr (COMBINE)
+                        x = u4_t{combine(x.x, ex[u].x), combine(x.y, ex[u].y), combine(x.z, ex[u].z),
+                                 combine(x.w, ex[u].w)};
+                    if constexpr (WRITE_E) {
+                        if (ok) __builtin_nontemporal_store(x, reinterpret_cast<u4_t*>(ep) + c);
+                    }
+                    if (!ok) x = u4_t{0u, 0u, 0u, 0u};
+                    const bf2_t x0 = __builtin_bit_cast(bf2_t, x.x), x1 = __builtin_bit_cast(bf2_t, x.y);
+                    const bf2_t x2 = __builtin_bit_cast(bf2_t, x.z), x3 = __builtin_bit_cast(bf2_t, x.w);
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        const u4_t v = vp[j * mu + c];
+                        float a = acc[j];
+                        a = __builtin_amdgcn_fdot2_f32_bf16(x0, __builtin_bit_cast(bf2_t, v.x), a, false);
+                        a = __builtin_amdgcn_fdot2_f32_bf16(x1, __builtin_bit_cast(bf2_t, v.y), a, false);
+                        a = __builtin_amdgcn_fdot2_f32_bf16(x2, __builtin_bit_cast(bf2_t, v.z), a, false);
+                        a = __builtin_amdgcn_fdot2_f32_bf16(x3, __builtin_bit_cast(bf2_t, v.w), a, false);
+                        acc[j] = a;
+                    }
+                }
+                if (st_ == steps - 1) {
+#pragma unroll
+                    for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
+#ifdef ARCTOPK_ENC_LANE0_BF16  // A/B: lane 0 stores all R sums
+                    if (lane == 0) {
+#pragma unroll
+                        for (int j = 0; j < R; ++j) put(r_ * R + j, acc[j]);
+                    }
+#else
+                    if (lane < R) {
+                        float v = acc[0];
+#pragma unroll
+                        for (int j = 1; j < R; ++j)
+                            if (lane == j) v = acc[j];
+                        put(r_ * R + lane, v);
+                    }
+#endif
+#pragma unroll
+                    for (int j = 0; j < R; ++j) acc[j] = 0.f;
+                }
+            };
+            const int64_t nq = t.nrows;
+            int64_t qa = wave;
+            int sa = 0;
+            if (qa < nq) issue(ga, ea, t.row0 + qa * rs, sa);
+            while (qa < nq) {
+                int64_t qb = qa;
+                int sb = sa + 1;
+                if (sb == steps) { sb = 0; qb += 4; }
+                if (qb < nq) issue(gb, eb, t.row0 + qb * rs, sb);
+                consume(ga, ea, t.row0 + qa * rs, sa);
+                if (qb >= nq) break;
+                qa = qb;
+                sa = sb + 1;
+                if (sa == steps) { sa = 0; qa += 4; }
+                if (qa < nq) issue(ga, ea, t.row0 + qa * rs, sa);
+                consume(gb, eb, t.row0 + qb * rs, sb);
+            }
+            return;
+        }
+    }
     if (t.mode == ENC_ROW_VEC) {
         // Software-pipelined stream: a wave walks its rows in steps of 64*U 16-B units
         // (U per lane; a unit is 4 fp32 or 8 bf16 elements) with two register buffers: the
         // loads of the next step are in flight while the current step forms its dot
         // products, stores E and (at a row end) reduces.  V^T comes from LDS.
         constexpr int PQ = kQuadsPer16<T>;  // quads per 16-B unit
-        constexpr int U = 4 / PQ;
         constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
+        // units per lane per step: a stream of G alone keeps more of them in flight
+        constexpr int U = (LOAD_E ? 4 : ARCTOPK_ENC_UNITS_G_ONLY) / PQ;
         const int m4 = cl >> 2;   // quads of this tile row
         const int mu = m4 / PQ;   // 16-B units (the plan makes m4 a multiple of PQ)
         const int steps = (mu + 64 * U - 1) / (64 * U);
@@ -258,6 +367,11 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         float acc[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) acc[j] = 0.f;
+#if ARCTOPK_ENC_PKFMA
+        f2_t acc2[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc2[j] = f2_t{0.f, 0.f};
+#endif
 
         auto issue = [&](float4 (&gx)[U][PQ], float4 (&ex)[U][PQ], int64_t r_, int st_) {
             const T* gp = G + s.offset + r_ * m + c0;
@@ -285,6 +399,21 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int h = 0; h < PQ; ++h)
                     if (!ok) x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+#if ARCTOPK_ENC_PKFMA
+                // packed FMA (v_pk_fma_f32): even / odd columns accumulate separately, two
+                // products per instruction; the halves are added at the row end
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    f2_t a = acc2[j];
+#pragma unroll
+                    for (int h = 0; h < PQ; ++h) {
+                        const float4 v = vt4[j * m4 + c * PQ + h];
+                        a = __builtin_elementwise_fma(f2_t{x[h].x, x[h].y}, f2_t{v.x, v.y}, a);
+                        a = __builtin_elementwise_fma(f2_t{x[h].z, x[h].w}, f2_t{v.z, v.w}, a);
+                    }
+                    acc2[j] = a;
+                }
+#else
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     float a = acc[j];
@@ -298,10 +427,22 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                     }
                     acc[j] = a;
                 }
+#endif
             }
             if (st_ == steps - 1) {
+#if ARCTOPK_ENC_PKFMA
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    acc[j] = acc2[j].x + acc2[j].y;
+                    acc2[j] = f2_t{0.f, 0.f};
+                }
+#endif
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
+                // every lane holds all R sums; lanes 0..R-1 store one each.  (The compiler
+                // makes the pick a dynamically indexed private array, i.e. a few bytes of
+                // scratch per row; the alternative, lane 0 storing all R, measured 10 us
+                // slower per headline encode, 148 vs 138 us.)
                 if (lane < R) {
                     float v = acc[0];
 #pragma unroll
@@ -346,12 +487,9 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
             }
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
-            if (lane < R) {
-                float v = acc[0];
+            if (lane == 0) {
 #pragma unroll
-                for (int j = 1; j < R; ++j)
-                    if (lane == j) v = acc[j];
-                put(row * R + lane, v);
+                for (int j = 0; j < R; ++j) put(row * R + j, acc[j]);
             }
         }
     }
@@ -2078,17 +2216,17 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
 // ---------------------------------------------------------------------------
 // K4 decode
 // ---------------------------------------------------------------------------
+// One decode chunk (256 threads): k_decode's block, or a block of another launch that a
+// deferred decode rides in (k_select_small_dec).  dlds: the small-m chunk tile (dynamic LDS).
 template <typename T, int EF>
-__global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
-                                                const Chunk* __restrict__ chunks,
-                                                const T* __restrict__ packed,
-                                                const int32_t* __restrict__ slotmap, Scale sc,
-                                                T* __restrict__ gE, T* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) float dlds[];  // small-m chunk tile
+__device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                             const T* __restrict__ packed,
+                                             const int32_t* __restrict__ slotmap, Scale sc,
+                                             T* __restrict__ gE, T* __restrict__ out,
+                                             float* __restrict__ dlds) {
     // mean of the all-reduced values (ref values_memory.div_(ws)), rounded to T
     auto mean4 = [&](float4 v) { return rnd4<T>(sc(v)); };
     auto mean1 = [&](float v) { return rnd<T>(sc(v)); };
-    const Chunk ch = chunks[blockIdx.x];
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
     const int64_t base = s.offset + ch.row0 * m;
@@ -2330,6 +2468,49 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
             st1<T>(out + base + e, v);
         }
     }
+}
+
+template <typename T, int EF>
+__global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
+                                                const Chunk* __restrict__ chunks,
+                                                const T* __restrict__ packed,
+                                                const int32_t* __restrict__ slotmap, Scale sc,
+                                                T* __restrict__ gE, T* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float dlds[];  // small-m chunk tile
+    decode_chunk<T, EF>(segs, chunks[blockIdx.x], packed, slotmap, sc, gE, out, dlds);
+}
+
+// A deferred decode (an earlier bucket's, arctopk_exchange_step's `ride`) riding in the
+// single-block select launch of the current bucket: the select blocks are latency-bound
+// (a few KiB each), the decode chunks stream the bucket, so the select is hidden behind the
+// decode's HBM time instead of idling the GPU between encode and pack.
+template <typename T>
+struct DecodeRide {
+    const SegDev* segs;
+    const Chunk* chunks;
+    const T* packed;
+    const int32_t* slotmap;
+    T* gE;
+    T* out;
+    Scale sc;
+    int32_t n;  // chunks (blocks); 0: none
+};
+
+template <typename T, int EF>
+__global__ void __launch_bounds__(kST) k_select_small_dec(const SegDev* __restrict__ segs,
+                                                          const int32_t* __restrict__ seg_ids, int nsel,
+                                                          const T* __restrict__ sketch, int R, Scale sc,
+                                                          int32_t* __restrict__ rowlist,
+                                                          int32_t* __restrict__ slotmap, DecodeRide<T> dr,
+                                                          VDrawJob job) {
+    if (maybe_draw_v<T>(job, kST)) return;  // trailing blocks: the next call's projections
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    if ((int)blockIdx.x < nsel) {  // first: the latency-bound selects
+        select_small_seg<T, kST>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, dyn);
+        return;
+    }
+    decode_chunk<T, EF>(dr.segs, dr.chunks[blockIdx.x - nsel], dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
+                        reinterpret_cast<float*>(dyn));
 }
 
 // WRITE_X = false (EF14 fold): E := x + E only; the caller reads the pre-compression
@@ -2688,6 +2869,84 @@ extern "C" int arctopk_select_draw(const arctopk_plan* p, const void* sketch, in
     if (job.n && !drawn) return arctopk_draw_projections(next, next_seed, next_V, stream);
     return 0;
 }
+
+namespace {
+template <typename T>
+int launch_select_ride(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_t* rowlist,
+                       int32_t* slotmap, VDrawJob job, const arctopk_plan* rp, int32_t rp_ws, int32_t rp_ef,
+                       void* rp_gerr, void* rp_out, hipStream_t st) {
+    DecodeRide<T> dr;
+    dr.segs = rp->d_segs;
+    dr.chunks = rp->d_dec;
+    dr.packed = static_cast<const T*>(rp->b_packed);
+    dr.slotmap = rp->b_slotmap;
+    dr.gE = static_cast<T*>(rp_gerr);
+    dr.out = static_cast<T*>(rp_out);
+    dr.sc = make_scale(rp_ws);
+    dr.n = rp->n_dec;
+    const size_t shm = (size_t)std::max(p->small_lds, rp->dec_lds_bytes);
+    const dim3 grid(p->n_small + dr.n + job.n);
+    const T* sketch = static_cast<const T*>(sketch_);
+    if (rp_ef == ARCTOPK_EF21) {
+        if (shm > 48 * 1024) {
+            static const hipError_t ok = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&k_select_small_dec<T, ARCTOPK_EF21>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+            if (ok != hipSuccess) return (int)ok;
+        }
+        launch_job_kernel(&k_select_small_dec<T, ARCTOPK_EF21>, grid, dim3(kST), shm, st, (const SegDev*)p->d_segs,
+                          (const int32_t*)p->d_small, p->n_small, sketch, (int)p->r, make_scale(ws), rowlist,
+                          slotmap, dr, job);
+    } else {
+        if (shm > 48 * 1024) {
+            static const hipError_t ok = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&k_select_small_dec<T, ARCTOPK_EF_NONE>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+            if (ok != hipSuccess) return (int)ok;
+        }
+        launch_job_kernel(&k_select_small_dec<T, ARCTOPK_EF_NONE>, grid, dim3(kST), shm, st,
+                          (const SegDev*)p->d_segs, (const int32_t*)p->d_small, p->n_small, sketch, (int)p->r,
+                          make_scale(ws), rowlist, slotmap, dr, job);
+    }
+    return (int)hipGetLastError();
+}
+}  // namespace
+
+namespace arctopk {
+// arctopk_select_draw with the deferred decode of plan rp (its bound packed buffer and slot map,
+// rp_ws, rp_ef, gE and output bucket) in the same launch, when this plan's select is one launch
+// of 256-thread single-block selects (*rode = 1); otherwise only the select (*rode = 0: the
+// caller decodes rp itself).
+int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
+                const arctopk_plan* next, uint64_t next_seed, void* next_V, const arctopk_plan* rp,
+                int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream) {
+    *rode = 0;
+    constexpr int64_t big_rows = ARCTOPK_SEL_BIG_ROWS;
+    const bool fusable = rp && rp->dtype == p->dtype && rp->device == p->device && rp->n_dec > 0 &&
+                         rp->b_packed && rp->b_slotmap && rp_out && (rp_ef != ARCTOPK_EF21 || rp_gerr) &&
+                         p->n_small > 0 && p->n_large_batches == 0 && !(p->small_lds > big_rows * 4 + 16) &&
+                         p->small_lds <= 48 * 1024 && rp->dec_lds_bytes <= 64 * 1024;
+    if (!fusable) return arctopk_select_draw(p, sketch, ws, rowlist, slotmap, next, next_seed, next_V, stream);
+    if (!p || !sketch || !rowlist || !slotmap || ws < 1 || rp_ws < 1) return ARCTOPK_EINVAL;
+    if (next && (!next_V || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
+    VDrawJob job{};
+    if (next && next->n_vchunk) {
+        job.segs = next->d_vdraw;
+        job.chunks = next->d_vchunk;
+        job.V = next_V;
+        job.seed = next_seed;
+        job.n = next->n_vchunk;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const int e = p->dtype == ARCTOPK_BF16
+                      ? launch_select_ride<bf16_t>(p, sketch, ws, rowlist, slotmap, job, rp, rp_ws, rp_ef, rp_gerr,
+                                                   rp_out, st)
+                      : launch_select_ride<float>(p, sketch, ws, rowlist, slotmap, job, rp, rp_ws, rp_ef, rp_gerr,
+                                                  rp_out, st);
+    if (!e) *rode = 1;
+    return e;
+}
+}  // namespace arctopk
 
 extern "C" int arctopk_select(const arctopk_plan* p, const void* sketch, int32_t ws,
                               int32_t* rowlist, int32_t* slotmap, void* stream) {

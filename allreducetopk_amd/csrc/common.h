@@ -55,6 +55,12 @@
 #ifndef ARCTOPK_SHORT_DEC_CHUNK
 #define ARCTOPK_SHORT_DEC_CHUNK 4096   // elements per short-row (m < 256) decode chunk
 #endif
+#ifndef ARCTOPK_ENC_PKFMA
+#define ARCTOPK_ENC_PKFMA 0            // fp32 encode: packed FMAs over even / odd columns
+#endif
+#ifndef ARCTOPK_ENC_UNITS_G_ONLY
+#define ARCTOPK_ENC_UNITS_G_ONLY 4     // fp32 encode without E loads: 16-B units per lane per step
+#endif
 #ifndef ARCTOPK_ENC_INTERLEAVE
 #define ARCTOPK_ENC_INTERLEAVE 1       // encode row tiles interleaved (1) or contiguous ranges (0)
 #endif
@@ -379,6 +385,9 @@ struct arctopk_plan {
     int x_ef, x_ws;                     //   the EF mode and world size of that call
 };
 namespace arctopk {
+int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
+                const arctopk_plan* next, uint64_t next_seed, void* next_V, const arctopk_plan* rp,
+                int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream);
 int pack_signal(const arctopk_plan* p, const void* grad, void* err, int32_t ef, const int32_t* rowlist,
                 const int32_t* slotmap, void* packed, void* stream, void* done);
 }

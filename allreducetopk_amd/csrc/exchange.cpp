@@ -175,18 +175,21 @@ int ensure_event(void** ev, unsigned flags) {
 
 // The deferred decode of plan p's last exchange step, on `stream`: after that step's packed
 // all-reduce (a stream wait only when the host does not already see it complete).
+namespace {
+int wait_ar(arctopk_plan* p, hipStream_t st) {
+    if (p->x_deferred != 1) return 0;  // 2: no all-reduce on another stream
+    const hipError_t q = hipEventQuery((hipEvent_t)p->x_ev_ar);
+    if (q == hipErrorNotReady) return (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
+    return q == hipSuccess ? 0 : (int)q;
+}
+}  // namespace
+
 extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* const* marks) {
     if (!p) return ARCTOPK_EINVAL;
     if (!p->x_deferred) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const hipError_t q = hipEventQuery((hipEvent_t)p->x_ev_ar);
-    if (q == hipErrorNotReady) {
-        const hipError_t w = hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
-        if (w != hipSuccess) return (int)w;
-    } else if (q != hipSuccess) {
-        return (int)q;
-    }
-    int e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
+    int e = wait_ar(p, st);
+    if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
     if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
     if (!e) p->x_deferred = 0;
@@ -196,15 +199,20 @@ extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* cons
 extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, void* gerr, int32_t ef,
                                      int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
                                      uint64_t next_seed, arctopk_comm* sketch_comm, arctopk_comm* packed_comm,
-                                     void* stream, void* ar_stream, arctopk_plan* prev, void* const* prev_marks,
-                                     const void* V, void* const* marks) {
-    if (!p || !bucket || !p->b_sketch || !sketch_comm || !packed_comm) return ARCTOPK_EINVAL;
-    if (sketch_comm->nranks != packed_comm->nranks) return ARCTOPK_EINVAL;
+                                     void* stream, void* ar_stream, int32_t defer, arctopk_plan* ride,
+                                     void* const* ride_marks, arctopk_plan* const* finish,
+                                     void* const* const* finish_marks, int32_t nfinish, const void* V,
+                                     void* const* marks) {
+    if (!p || !bucket || !p->b_sketch || !sketch_comm != !packed_comm || nfinish < 0 || (nfinish && !finish))
+        return ARCTOPK_EINVAL;
+    if (sketch_comm && sketch_comm->nranks != packed_comm->nranks) return ARCTOPK_EINVAL;
     if (next && (!next->b_sketch || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
-    if (ar_stream && ar_stream == stream) return ARCTOPK_EINVAL;
-    const int ws = packed_comm->nranks;
+    // deferring with a collective needs the all-reduce stream (the decode waits for its event)
+    if (defer && packed_comm && (!ar_stream || ar_stream == stream)) return ARCTOPK_EINVAL;
+    if (ride && (ride == p || !ride->x_deferred)) return ARCTOPK_EINVAL;
+    const int ws = packed_comm ? packed_comm->nranks : 1;
     hipStream_t st = (hipStream_t)stream, as = (hipStream_t)ar_stream;
-    // this bucket's own previous decode, if a caller never finished it (the hook always does)
+    // this bucket's own deferred decode, if a caller never finished it (the hook always does)
     int e = arctopk_exchange_finish(p, stream, nullptr);
     if (!e) e = mark(marks, ARCTOPK_MARK_START, st);
     if (!V) V = p->b_V;
@@ -213,44 +221,69 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (!e) e = arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_ENCODE, st);
     // one all-reduce for every tensor's sketch (the reference: one per tensor, :33, :58, :88)
-    if (!e) e = arctopk_comm_allreduce(sketch_comm, p->b_sketch, p->info.sketch_len, p->dtype, stream);
+    if (!e && sketch_comm) e = arctopk_comm_allreduce(sketch_comm, p->b_sketch, p->info.sketch_len, p->dtype, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_SKETCH_AR, st);
-    if (!e)
+    if (e) return e;
+    // the select, with an earlier bucket's deferred decode riding in the same launch when
+    // both fit (the select's latency hides behind the decode's stream)
+    int rode = 0;
+    if (ride) {
+        if ((e = wait_ar(ride, st)) || (e = mark(ride_marks, ARCTOPK_MARK_PACKED_AR, st))) return e;
+        e = arctopk::select_ride(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
+                                 next ? next->b_V : nullptr, ride, ride->x_ws, ride->x_ef, ride->x_gerr,
+                                 ride->x_bucket, &rode, stream);
+        if (!e && rode) {
+            ride->x_deferred = 0;
+            e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
+        }
+        if (!e && !rode) {  // a separate decode launch after the select
+            e = arctopk_decode(ride, ride->b_packed, ride->b_slotmap, ride->x_ws, ride->x_ef, ride->x_gerr,
+                               ride->x_bucket, stream);
+            if (!e) ride->x_deferred = 0;
+            if (!e) e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
+        }
+    } else {
         e = arctopk_select_draw(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
                                 next ? next->b_V : nullptr, stream);
+    }
     if (!e) e = mark(marks, ARCTOPK_MARK_SELECT, st);
     if (e) return e;
-    if (!as) {  // inline: the previous bucket's decode, then this bucket's exchange, all on `stream`
+    const bool signal = defer && packed_comm;
+    if (signal) {
+        // the pack kernel completes x_ev_packed itself (no marker packet on the caller's
+        // stream, where one idles the GPU several us); the all-reduce stream waits for it
+        if ((e = ensure_event(&p->x_ev_packed, 0)) ||
+            (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
+            return e;
+        e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
+                                 p->x_ev_packed);
+    } else {
         e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
-        if (!e) e = mark(marks, ARCTOPK_MARK_PACK, st);
-        if (!e && prev && prev != p) e = arctopk_exchange_finish(prev, stream, prev_marks);
-        // the index-free all-reduce of the packed values (:280)
-        if (!e) e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
-        if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
-        if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream);
-        if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
-        return e;
     }
-    // overlapped: the pack kernel completes x_ev_packed itself (no marker packet on the
-    // caller's stream, where one idles the GPU ~12 us); the all-reduce stream waits for it
-    if ((e = ensure_event(&p->x_ev_packed, 0)) ||
-        (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
-        return e;
-    e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream, p->x_ev_packed);
     if (!e) e = mark(marks, ARCTOPK_MARK_PACK, st);
     if (e) return e;
-    hipError_t he = hipStreamWaitEvent(as, (hipEvent_t)p->x_ev_packed, 0);
-    if (he != hipSuccess) return (int)he;
-    e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, as);
+    if (signal) {  // the index-free all-reduce of the packed values (:280) on its own stream
+        hipError_t he = hipStreamWaitEvent(as, (hipEvent_t)p->x_ev_packed, 0);
+        if (he != hipSuccess) return (int)he;
+        if ((e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, as))) return e;
+        he = hipEventRecord((hipEvent_t)p->x_ev_ar, as);
+        if (he != hipSuccess) return (int)he;
+    }
+    // earlier buckets' deferred decodes the caller wants done now (in its order)
+    for (int32_t i = 0; i < nfinish && !e; ++i)
+        if (finish[i] && finish[i] != p) e = arctopk_exchange_finish(finish[i], stream, finish_marks ? finish_marks[i] : nullptr);
     if (e) return e;
-    he = hipEventRecord((hipEvent_t)p->x_ev_ar, as);
-    if (he != hipSuccess) return (int)he;
-    p->x_deferred = 1;
-    p->x_bucket = bucket;
-    p->x_gerr = gerr;
-    p->x_ef = ef;
-    p->x_ws = ws;
-    // the previous bucket's decode (its all-reduce ran beside this bucket's encode)
-    if (prev && prev != p) e = arctopk_exchange_finish(prev, stream, prev_marks);
+    if (defer) {
+        p->x_deferred = signal ? 1 : 2;
+        p->x_bucket = bucket;
+        p->x_gerr = gerr;
+        p->x_ef = ef;
+        p->x_ws = ws;
+        return 0;
+    }
+    if (packed_comm) e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
+    if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
+    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream);
+    if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
     return e;
 }

@@ -175,6 +175,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-events", action="store_true")
+    ap.add_argument("--no-forced-exchange", action="store_true",
+                    help="at N = 1, skip the extra timing of the forced-exchange path")
     ap.add_argument("--force-exchange", action="store_true",
                     help="at N = 1, run the N > 1 code path: the native exchange step with its "
                          "all-reduces on one-rank RCCL communicators and the exchange stream")
@@ -259,6 +261,27 @@ def main():
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     host_times = dict(_G.HOST_TIMES) if _G.HOST_TIMES is not None else None
+
+    # At N = 1 the hook's own path has no collectives; the N > 1 code path (one-rank RCCL
+    # communicators, packed all-reduce on the exchange stream, deferred decodes) is timed
+    # beside it in the same run, so the N = 1 point of a scaling run can be read on either.
+    forced = None
+    if (world == 1 and args.hook == "arc" and not args.host_staged and not args.force_exchange
+            and not args.no_forced_exchange and args.backend == "nccl"):
+        st.force_exchange = True
+        st.init_exchange_comms(dev)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        fe = time.perf_counter() - t1
+        forced = {"value": round(args.steps * bytes_per_step / fe / 1e9, 2),
+                  "ms_per_bucket": round(fe / args.steps / nb * 1e3, 4), "steps": args.steps,
+                  "hook_path": "exchange (one-rank RCCL communicators)"}
+        st.force_exchange = False
 
     phase_ms = {}
     light = {}
@@ -356,6 +379,7 @@ def main():
                                      "all-reduce + decode on the exchange stream, overlapping the "
                                      "next bucket")},
         "per_gpu_value": round(value / world, 2),
+        "forced_exchange": forced,
         "ms_per_bucket": round(ms_per_step / nb, 4),
         "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
         "roofline": roof,

@@ -195,29 +195,32 @@ int arctopk_comm_size(const arctopk_comm* comm);
 int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t dtype, void* stream);
 
 /*
- * One bucket call of the hook with its collectives, in one host call (world size =
- * the communicators' size; at size 1 the all-reduces are identities but still issued).
- * Overlapped (ar_stream given):
- *   stream    : [draw] -> encode -> all_reduce(sketch, sketch_comm) -> select (+ next V) -> pack
- *               -> arctopk_exchange_finish(prev): the previous step's decode
- *   ar_stream : all_reduce(packed, packed_comm), after the pack kernel (which completes the
- *               event the stream waits for: no marker packet on `stream`)
- *   This step's own decode is deferred to arctopk_exchange_finish(plan, ...) -- the next step's
- *   `prev`, or an explicit call -- so the caller's stream encodes the next bucket while these
- *   packed values are on the wire, and the decode never competes with an encode for HBM.
- * Inline (ar_stream NULL): pack -> finish(prev) -> all_reduce(packed) -> decode, on `stream`
- *   (the last bucket of a backward: nothing is left in flight).
- * `prev_marks` are the markers of prev's step (its PACKED_AR / DECODE are recorded by the
- * finish).  `V`: the projections to encode with (NULL: the plan's bound projection buffer,
- * drawn there for `seed` when draw != 0).
+ * One bucket call of the hook, collectives included, in one host call.  World size = the
+ * communicators' size (both NULL: world size 1, no collectives issued).  On `stream`:
+ *   [draw] -> encode -> all_reduce(sketch, sketch_comm) -> select (+ next V)
+ *          -> pack -> the `finish` steps' deferred decodes -> [all_reduce(packed) -> decode]
+ * defer = 1: this step's decode is deferred to arctopk_exchange_finish(plan, ...) (or to a
+ *   later step's `ride` / `finish`); with communicators its packed all-reduce runs on
+ *   `ar_stream` after the pack kernel, which completes the event that stream waits for (no
+ *   marker packet on `stream`), so the caller's stream encodes the next bucket while these
+ *   packed values are on the wire.  defer = 0: all-reduce and decode inline on `stream`.
+ * ride: an earlier step's deferred decode, run inside this step's select launch when the select
+ *   is one launch of 256-thread single-block selects (the select's latency then hides behind the
+ *   decode's HBM stream), else right after the select; ride_marks are that step's markers.
+ * finish[0 .. nfinish): earlier deferred steps decoded after this pack, in order.
+ * `V`: the projections to encode with (NULL: the plan's bound projection buffer, drawn there
+ * for `seed` when draw != 0).  `marks`: see ARCTOPK_MARK_*.
  * Replaces: the whole of group_topk_hook's compressed path (:254-290) given the seed.
  */
 int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
                           int32_t err_in, int32_t draw, uint64_t seed, const arctopk_plan* next,
                           uint64_t next_seed, arctopk_comm* sketch_comm, arctopk_comm* packed_comm,
-                          void* stream, void* ar_stream, arctopk_plan* prev, void* const* prev_marks,
-                          const void* V, void* const* marks);
-/* The deferred decode of `plan`'s last overlapped exchange step, on `stream` (no-op if none). */
+                          void* stream, void* ar_stream, int32_t defer, arctopk_plan* ride,
+                          void* const* ride_marks, arctopk_plan* const* finish,
+                          void* const* const* finish_marks, int32_t nfinish, const void* V,
+                          void* const* marks);
+/* The deferred decode of `plan`'s last deferred exchange step, on `stream` (no-op if none):
+ * after that step's packed all-reduce. */
 int arctopk_exchange_finish(arctopk_plan* plan, void* stream, void* const* marks);
 
 /*
