@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     const int64_t rs = t.rstride;
     if constexpr (kDot2) {
         if (t.mode == ENC_ROW_VEC) {
-            constexpr int U = 2;  // 16-B units (8 bf16) per lane per step, two buffers
+            constexpr int U = ARCTOPK_ENC_UNITS_BF16;  // 16-B units (8 bf16) per lane per step, two buffers
             constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
             constexpr bool COMBINE = LOAD_E;  // x = rnd(g +- e); else x = g (already bf16)
             const int mu = cl >> 3;           // units of this tile row (cl is a multiple of 8)
@@ -1746,7 +1746,29 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     DIAG_STAMP(g_st_refine, 1);
 }
 
+// A deferred decode (an earlier bucket's, arctopk_exchange_step's `ride`) riding in a launch of
+// the current bucket's select: its chunks run as extra 256-thread blocks after the select's own
+// (latency-bound) blocks, so the select's latency hides behind the decode's HBM stream.
 template <typename T>
+struct DecodeRide {
+    const SegDev* segs;
+    const Chunk* chunks;
+    const T* packed;
+    const int32_t* slotmap;
+    T* gE;
+    T* out;
+    Scale sc;
+    int32_t n;  // chunks (blocks); 0: none
+};
+template <typename T, int EF>
+__device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                             const T* __restrict__ packed,
+                                             const int32_t* __restrict__ slotmap, Scale sc,
+                                             T* __restrict__ gE, T* __restrict__ out,
+                                             float* __restrict__ dlds);
+
+// grid: [write ranges (nflat)] [small selects] [ride decode chunks (dr.n)] [V draw (job.n)]
+template <typename T, int EF>
 __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, int nflat,
                                                              const uint32_t* __restrict__ keys, MWorkspace* ws,
                                                              const uint32_t* __restrict__ ckey,
@@ -1754,9 +1776,16 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
                                                              const int32_t* __restrict__ small_ids,
                                                              const T* __restrict__ sketch, int R, Scale sc,
                                                              int32_t* __restrict__ rowlist,
-                                                             int32_t* __restrict__ slotmap, VDrawJob job) {
+                                                             int32_t* __restrict__ slotmap, DecodeRide<T> dr,
+                                                             VDrawJob job) {
     if (maybe_draw_v<T>(job, kFuseNT)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    const int rb = (int)blockIdx.x - ((int)gridDim.x - job.n - dr.n);
+    if (rb >= 0) {  // the ride's decode chunks
+        decode_chunk<T, EF>(dr.segs, dr.chunks[rb], dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
+                            reinterpret_cast<float*>(dyn));
+        return;
+    }
     if ((int)blockIdx.x >= nflat) {  // the small segments' single-block selects
         select_small_seg<T, kFuseNT>(segs, small_ids[blockIdx.x - nflat], sketch, R, sc, rowlist, slotmap, dyn);
         return;
@@ -2484,18 +2513,6 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
 // single-block select launch of the current bucket: the select blocks are latency-bound
 // (a few KiB each), the decode chunks stream the bucket, so the select is hidden behind the
 // decode's HBM time instead of idling the GPU between encode and pack.
-template <typename T>
-struct DecodeRide {
-    const SegDev* segs;
-    const Chunk* chunks;
-    const T* packed;
-    const int32_t* slotmap;
-    T* gE;
-    T* out;
-    Scale sc;
-    int32_t n;  // chunks (blocks); 0: none
-};
-
 template <typename T, int EF>
 __global__ void __launch_bounds__(kST) k_select_small_dec(const SegDev* __restrict__ segs,
                                                           const int32_t* __restrict__ seg_ids, int nsel,
@@ -2653,10 +2670,52 @@ int launch_energy(const arctopk_plan* p, const void* sketch, int32_t ws, uint32_
     return (int)hipGetLastError();
 }
 
+// a deferred decode offered to ride in the select's last launch (see DecodeRide)
+struct RideArgs {
+    const arctopk_plan* rp;
+    int32_t ws, ef;
+    void* gerr;
+    void* out;
+};
+
+template <typename T>
+DecodeRide<T> make_ride(const RideArgs* ra) {
+    DecodeRide<T> dr{};
+    if (!ra) return dr;
+    const arctopk_plan* rp = ra->rp;
+    dr.segs = rp->d_segs;
+    dr.chunks = rp->d_dec;
+    dr.packed = static_cast<const T*>(rp->b_packed);
+    dr.slotmap = rp->b_slotmap;
+    dr.gE = static_cast<T*>(ra->gerr);
+    dr.out = static_cast<T*>(ra->out);
+    dr.sc = make_scale(ra->ws);
+    dr.n = rp->n_dec;
+    return dr;
+}
+
+template <typename T, int EF>
+int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int nsm, const uint32_t* ckey, const T* sketch,
+                       int32_t ws, int32_t* rowlist, int32_t* slotmap, DecodeRide<T> dr, VDrawJob bj, size_t shm,
+                       hipStream_t st) {
+    if (shm > 48 * 1024) {
+        static const hipError_t ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_arc_write_fused<T, EF>),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        if (ok != hipSuccess) return (int)ok;
+    }
+    launch_job_kernel(&k_arc_write_fused<T, EF>, dim3(nflat + nsm + dr.n + bj.n), dim3(kFuseNT), shm, st,
+                      (const MBatch*)(p->d_large_batches + bi), nflat, (const uint32_t*)p->d_keys, p->d_mws, ckey,
+                      (const SegDev*)p->d_segs, (const int32_t*)p->d_small, sketch, (int)p->r, make_scale(ws),
+                      rowlist, slotmap, dr, bj);
+    return (int)hipGetLastError();
+}
+
+// ride: a deferred decode that may run in the last select launch (*rode = true if it did)
 template <typename T>
 int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_t* rowlist, int32_t* slotmap,
-                  VDrawJob job, bool* drawn, hipStream_t st) {
+                  VDrawJob job, bool* drawn, hipStream_t st, const RideArgs* ride = nullptr, bool* rode = nullptr) {
     *drawn = false;
+    if (rode) *rode = false;
     const T* sketch = static_cast<const T*>(sketch_);
 #ifndef ARCTOPK_DIAG_NOSMALL
 #define ARCTOPK_DIAG_NOSMALL 0  // diagnostic builds only: skip the single-block select
@@ -2735,20 +2794,21 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         // write blocks finish: ResNet-18's third DDP bucket measured 250 -> 241 GB/s fused)
         if (fuse_ok && maxn <= kFuseMaxRows && nflat + nsm + bj.n <= kFuseMaxBlocks &&
             (nsm == 0 || p->small_lds <= 4096 * 4 + 16)) {
-            const size_t shm = std::max<size_t>((size_t)kFuseCap * 4, nsm ? (size_t)p->small_lds : 0);
-            if (bi == 0)
-                launch_job_kernel(&k_arc_write_fused<T>, dim3(nflat + nsm + bj.n), dim3(kFuseNT), shm, st,
-                                  (const MBatch*)(p->d_large_batches + bi), nflat, (const uint32_t*)p->d_keys,
-                                  p->d_mws, (const uint32_t*)ckey, (const SegDev*)p->d_segs,
-                                  (const int32_t*)p->d_small, sketch, (int)p->r, make_scale(ws), rowlist, slotmap,
-                                  bj);
-            else
-                hipLaunchKernelGGL(k_arc_write_fused<T>, dim3(nflat + nsm + bj.n), dim3(kFuseNT), shm, st,
-                                   p->d_large_batches + bi, nflat, p->d_keys, p->d_mws, ckey, p->d_segs, p->d_small,
-                                   sketch, p->r, make_scale(ws), rowlist, slotmap, bj);
-            if (bi == 0) *drawn = true;
-            e = (int)hipGetLastError();
+            size_t shm = std::max<size_t>((size_t)kFuseCap * 4, nsm ? (size_t)p->small_lds : 0);
+            // the deferred decode rides in the last batch's launch (its blocks come after the
+            // write blocks, so they do not change which of those are resident at once)
+            const bool take = ride && bi == p->n_large_batches - 1 && ride->rp->n_dec > 0 &&
+                              ride->rp->dtype == p->dtype && ride->rp->dec_lds_bytes <= 64 * 1024;
+            const DecodeRide<T> dr = make_ride<T>(take ? ride : nullptr);
+            if (take) shm = std::max<size_t>(shm, (size_t)ride->rp->dec_lds_bytes);
+            e = take && ride->ef == ARCTOPK_EF21
+                    ? launch_write_fused<T, ARCTOPK_EF21>(p, bi, nflat, nsm, ckey, sketch, ws, rowlist, slotmap, dr,
+                                                          bj, shm, st)
+                    : launch_write_fused<T, ARCTOPK_EF_NONE>(p, bi, nflat, nsm, ckey, sketch, ws, rowlist, slotmap,
+                                                             dr, bj, shm, st);
             if (e) return e;
+            if (bi == 0) *drawn = true;
+            if (take && rode) *rode = true;
             continue;
         }
         static const hipError_t lds_ok = hipFuncSetAttribute(
@@ -2922,10 +2982,33 @@ int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* 
                 int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream) {
     *rode = 0;
     constexpr int64_t big_rows = ARCTOPK_SEL_BIG_ROWS;
-    const bool fusable = rp && rp->dtype == p->dtype && rp->device == p->device && rp->n_dec > 0 &&
-                         rp->b_packed && rp->b_slotmap && rp_out && (rp_ef != ARCTOPK_EF21 || rp_gerr) &&
-                         p->n_small > 0 && p->n_large_batches == 0 && !(p->small_lds > big_rows * 4 + 16) &&
-                         p->small_lds <= 48 * 1024 && rp->dec_lds_bytes <= 64 * 1024;
+    const bool rideable = rp && rp->dtype == p->dtype && rp->device == p->device && rp->n_dec > 0 &&
+                          rp->b_packed && rp->b_slotmap && rp_out && (rp_ef != ARCTOPK_EF21 || rp_gerr) &&
+                          rp->dec_lds_bytes <= 64 * 1024;
+    const bool fusable = rideable && p->n_small > 0 && p->n_large_batches == 0 &&
+                         !(p->small_lds > big_rows * 4 + 16) && p->small_lds <= 48 * 1024;
+    if (rideable && p->n_large_batches > 0) {  // multi-block select: ride in its fused write launch
+        if (!p || !sketch || !rowlist || !slotmap || ws < 1 || rp_ws < 1) return ARCTOPK_EINVAL;
+        if (next && (!next_V || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
+        VDrawJob job{};
+        if (next && next->n_vchunk) {
+            job.segs = next->d_vdraw;
+            job.chunks = next->d_vchunk;
+            job.V = next_V;
+            job.seed = next_seed;
+            job.n = next->n_vchunk;
+        }
+        const RideArgs ra{rp, rp_ws, rp_ef, rp_gerr, rp_out};
+        bool drawn = false, took = false;
+        hipStream_t st = (hipStream_t)stream;
+        const int e = p->dtype == ARCTOPK_BF16
+                          ? launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, &ra, &took)
+                          : launch_select<float>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, &ra, &took);
+        if (e) return e;
+        *rode = took ? 1 : 0;
+        if (job.n && !drawn) return arctopk_draw_projections(next, next_seed, next_V, stream);
+        return 0;
+    }
     if (!fusable) return arctopk_select_draw(p, sketch, ws, rowlist, slotmap, next, next_seed, next_V, stream);
     if (!p || !sketch || !rowlist || !slotmap || ws < 1 || rp_ws < 1) return ARCTOPK_EINVAL;
     if (next && (!next_V || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;

@@ -61,6 +61,9 @@
 #ifndef ARCTOPK_ENC_UNITS_G_ONLY
 #define ARCTOPK_ENC_UNITS_G_ONLY 4     // fp32 encode without E loads: 16-B units per lane per step
 #endif
+#ifndef ARCTOPK_ENC_UNITS_BF16
+#define ARCTOPK_ENC_UNITS_BF16 4       // bf16 encode rows: 16-B units per lane per step
+#endif
 #ifndef ARCTOPK_ENC_INTERLEAVE
 #define ARCTOPK_ENC_INTERLEAVE 1       // encode row tiles interleaved (1) or contiguous ranges (0)
 #endif

@@ -10,7 +10,7 @@ i=0
 while read -r args; do
   [ -z "$args" ] && continue
   i=$((i+1))
-  timeout -k 10 240 python bench.py $args --steps 20 --warmup 3 --no-cpu-baseline \
+  timeout -k 10 240 python bench.py $args --steps 20 --warmup 3 --no-cpu-baseline --no-forced-exchange \
       > gpurun_out/wl/w$i.log 2>&1 || { echo "bench [$args] failed"; tail -20 gpurun_out/wl/w$i.log; exit 1; }
   tail -1 gpurun_out/wl/w$i.log >> gpurun_out/wl/all.jsonl
   echo "[$args] done"
