@@ -24,6 +24,9 @@
 #ifndef ARCTOPK_SEL_BIG_ROWS
 #define ARCTOPK_SEL_BIG_ROWS 4096      // single-block select: 1024 threads above this many rows
 #endif
+#ifndef ARCTOPK_SMALL_SEL_ROWS_MIXED
+#define ARCTOPK_SMALL_SEL_ROWS_MIXED 4096  // single-block selects beside multi-block items: at most this many rows
+#endif
 #ifndef ARCTOPK_KEYS_THREADS
 #define ARCTOPK_KEYS_THREADS 1024      // multi-block select key pass: block size (256 or 1024)
 #endif

@@ -97,6 +97,13 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
 
     std::vector<SegDev> dsegs(segs.size());
     std::vector<int32_t> small_ids, large_ids, split_ids;
+    // Single-block selects up to kSmallSelRows rows -- but in a bucket that has multi-block
+    // items anyway, only the ones that fit 256-thread blocks: the rest join the multi-block
+    // batch, so the batch's write launch can host the small selects (and a deferred decode)
+    // and the separate refine launch is not needed
+    bool any_large = false;
+    for (const arctopk_segment& s : segs) any_large = any_large || s.n > kSmallSelRows;
+    const int64_t small_cap = any_large ? (int64_t)ARCTOPK_SMALL_SEL_ROWS_MIXED : (int64_t)kSmallSelRows;
     int64_t small_rows = 0;
     std::vector<EncTile> enc;
     std::vector<Chunk> pack, dec;
@@ -134,7 +141,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         g.magic32 = s.m > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)s.m - 1) / (uint64_t)s.m) : 0u;
         g.nparts = 1;
         g.part_off = 0;
-        if (s.n <= kSmallSelRows) {
+        if (s.n <= small_cap) {
             small_ids.push_back((int32_t)i);
             small_rows = std::max<int64_t>(small_rows, s.n);
         } else {
