@@ -204,9 +204,10 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   `ar_stream` after the pack kernel, which completes the event that stream waits for (no
  *   marker packet on `stream`), so the caller's stream encodes the next bucket while these
  *   packed values are on the wire.  defer = 0: all-reduce and decode inline on `stream`.
- * ride: an earlier step's deferred decode, run inside this step's select launch when the select
- *   is one launch of 256-thread single-block selects (the select's latency then hides behind the
- *   decode's HBM stream), else right after the select; ride_marks are that step's markers.
+ * ride: an earlier step's deferred decode, run inside this step's select launch (extra blocks of
+ *   the single-block select launch, or of the multi-block select's last, fused write launch: the
+ *   select's latency then hides behind the decode's HBM stream), else right after the select;
+ *   ride_marks are that step's markers.
  * finish[0 .. nfinish): earlier deferred steps decoded after this pack, in order.
  * `V`: the projections to encode with (NULL: the plan's bound projection buffer, drawn there
  * for `seed` when draw != 0).  `marks`: see ARCTOPK_MARK_*.

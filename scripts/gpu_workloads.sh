@@ -28,6 +28,9 @@ done <<LIST
 --workload headline --ef ef14 --hook topk
 --workload headline --ef ef14 --hook randk
 --workload headline --ef ef14 --dtype bf16
+--workload headline --ef ef14 --force-exchange
+--workload resnet18_ddp --ef ef14 --force-exchange
+--workload llama_embed --ef ef21 --force-exchange
 ${EXTRA_WL}
 LIST
 python scripts/wl_table.py gpurun_out/wl/all.jsonl
