@@ -1504,11 +1504,16 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __r
 // rounds, counts the candidates of the ranges before its own, and writes its range.  The
 // selection is the same exact top-k (same T, same lowest-range-first T-equal allowances).
 constexpr int kFuseCap = 8192;              // staged candidates per block (32 KiB of LDS)
-constexpr int64_t kFuseMaxRows = 262144;    // host rule: largest item of a fused batch
+constexpr int64_t kFuseMaxRows = ARCTOPK_FUSE_MAX_ROWS;  // host rule: largest item of a fused batch
 constexpr int kFuseNT = 256;
 constexpr int kFuseMaxBlocks = 512;         // host rule: two blocks per CU (LDS allows three)
+constexpr int kFuseMaxSpan = ARCTOPK_FUSE_MAX_SPAN;     // host rule: ranges per write block
 
-__device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int r, const uint32_t* __restrict__ keys,
+// ranges [r, r + qn) of item t: one span of consecutive ranges per block (several when the
+// batch has more ranges than kFuseMaxBlocks, so every write block is still resident at once
+// and the refine is paid once per span)
+__device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int r, int qn,
+                                                      const uint32_t* __restrict__ keys,
                                                       MWorkspace* ws, const uint32_t* __restrict__ ckey,
                                                       int32_t* __restrict__ out_idx, int32_t* __restrict__ out_slot,
                                                       uint32_t* __restrict__ stage /* LDS, kFuseCap */) {
@@ -1522,9 +1527,9 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     const int nr = it.nranges;
     const uint32_t* src = ckey + it.cand_off;
     const int64_t r0 = (int64_t)r * it.range;
-    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+    const int64_t r1 = min<int64_t>(it.n, r0 + (int64_t)qn * it.range);
     DIAG_STAMP(g_st_refine, 0);
-    // one round trip: the first-pass state, the per-range counts and this range's first tile
+    // one round trip: the first-pass state, the per-range counts and this span's first tile
     MState s = ws->st[t];
     uint32_t cc[PR], cg[PR], kor = 0u, kand = ~0u;
 #pragma unroll
@@ -1664,8 +1669,8 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     }
     DIAG_STAMP(g_st_refine, 3);
     const uint32_t T = s.prefix;
-    // candidates before this range (> T, == T) and this range's == T
-    const uint32_t cb = roff[r], ce = r + 1 < nr ? roff[r + 1] : nc32;
+    // candidates before this span (> T, == T) and this span's == T
+    const uint32_t cb = roff[r], ce = r + qn < nr ? roff[r + qn] : nc32;
     uint32_t gb = 0, eb = 0, eo = 0;
     if (all_eq) {  // no candidate above T; every one ties with it
         if (tid == 0) {
@@ -1767,9 +1772,9 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
                                              T* __restrict__ gE, T* __restrict__ out,
                                              float* __restrict__ dlds);
 
-// grid: [write ranges (nflat)] [small selects] [ride decode chunks (dr.n)] [V draw (job.n)]
+// grid: [write spans (nflat)] [small selects] [ride decode chunks (dr.n)] [V draw (job.n)]
 template <typename T, int EF>
-__global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, int nflat,
+__global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, int nflat, int span,
                                                              const uint32_t* __restrict__ keys, MWorkspace* ws,
                                                              const uint32_t* __restrict__ ckey,
                                                              const SegDev* __restrict__ segs,
@@ -1791,12 +1796,15 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
         return;
     }
     const MBatch& b = *bp;
-    int t = 0, r = (int)blockIdx.x;  // flat grid: the ranges of the batch's items back to back
-    while (t + 1 < b.cnt && r >= b.it[t].nranges) {
-        r -= b.it[t].nranges;
+    int t = 0, r = (int)blockIdx.x;  // flat grid: the spans of the batch's items back to back
+    while (t + 1 < b.cnt) {
+        const int ns = (b.it[t].nranges + span - 1) / span;
+        if (r < ns) break;
+        r -= ns;
         ++t;
     }
-    arc_write_fused_range(b.it[t], t, r, keys, ws, ckey, rowlist, slotmap, dyn);
+    const int r0 = r * span;
+    arc_write_fused_range(b.it[t], t, r0, min(span, b.it[t].nranges - r0), keys, ws, ckey, rowlist, slotmap, dyn);
 }
 
 struct KeysGrid {
@@ -1956,6 +1964,10 @@ __device__ __forceinline__ float4 pack4(const T* __restrict__ G, T* __restrict__
 #define ARCTOPK_PACK_FULL_QUADS 1  // tuning switch (A/B builds): 0 = rewrite only quads with a selected row
 #endif
 constexpr bool kPackFullQuads = ARCTOPK_PACK_FULL_QUADS != 0;
+#ifndef ARCTOPK_PACK_PAIRS
+#define ARCTOPK_PACK_PAIRS 1  // tuning switch (A/B builds): 0 = scalar gathers for even short rows
+#endif
+constexpr bool kPackPairs = ARCTOPK_PACK_PAIRS != 0;
 
 // Pack of a row range of an m in {1, 2} fp32 segment (Chunk mode 1): lane per 16-B quad of
 // the segment (4 / 2 rows), slot map read alongside; selected rows go to packed[slot * m],
@@ -2102,6 +2114,52 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
         __syncthreads();
         const uint32_t cnt = (uint32_t)(nr * m);
         const int64_t dbase = s.packed_off + ch.row0 * m;
+        if constexpr (sizeof(T) == 4 && kPackPairs) {
+            if ((m & 1) == 0 && (s.offset & 1) == 0) {
+                // even m (3x3 / 5x5 conv rows, 72 / 200 B): 8-B units.  Every unit lies in one
+                // row and both ends are 8-B aligned, so a wave's loads cover ~512 contiguous
+                // bytes per row run instead of four stride-4 scalar passes over the same lines
+                const uint32_t cnt2 = cnt >> 1;
+                const float* Gf = reinterpret_cast<const float*>(G);
+                float* Ef = reinterpret_cast<float*>(E);
+                float* df = reinterpret_cast<float*>(dst);
+                constexpr int Q = 8;
+                for (uint32_t q0 = threadIdx.x; q0 < cnt2; q0 += 256 * Q) {
+                    int64_t src[Q];
+                    float2 va[Q], vb[Q];
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        const uint32_t e = min(q0 + u * 256, cnt2 - 1) << 1;
+                        const uint32_t r = div32(e, s.magic32);
+                        src[u] = s.offset + (int64_t)rs[r] * m + (e - r * (uint32_t)m);
+                    }
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        if constexpr (EF == ARCTOPK_EF_NONE) va[u] = *reinterpret_cast<const float2*>(Gf + src[u]);
+                        else if constexpr (EF == ARCTOPK_EF14) va[u] = *reinterpret_cast<const float2*>(Ef + src[u]);
+                        else {
+                            va[u] = *reinterpret_cast<const float2*>(Gf + src[u]);
+                            vb[u] = *reinterpret_cast<const float2*>(Ef + src[u]);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        const uint32_t q = q0 + u * 256;
+                        if (q < cnt2) {
+                            float2 v = va[u];
+                            if constexpr (EF == ARCTOPK_EF14) {
+                                *reinterpret_cast<float2*>(Ef + src[u]) = make_float2(0.f, 0.f);
+                            } else if constexpr (EF == ARCTOPK_EF21) {
+                                v = make_float2(va[u].x - vb[u].x, va[u].y - vb[u].y);
+                                *reinterpret_cast<float2*>(Ef + src[u]) = make_float2(vb[u].x + v.x, vb[u].y + v.y);
+                            }
+                            *reinterpret_cast<float2*>(df + 2 * (int64_t)q) = v;
+                        }
+                    }
+                }
+                return;
+            }
+        }
         const int64_t pre = (4 - (dbase & 3)) & 3;
         auto one = [&](uint32_t e) -> float {
             const uint32_t r = div32(e, s.magic32);
@@ -2695,7 +2753,7 @@ DecodeRide<T> make_ride(const RideArgs* ra) {
 }
 
 template <typename T, int EF>
-int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int nsm, const uint32_t* ckey, const T* sketch,
+int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int span, int nsm, const uint32_t* ckey, const T* sketch,
                        int32_t ws, int32_t* rowlist, int32_t* slotmap, DecodeRide<T> dr, VDrawJob bj, size_t shm,
                        hipStream_t st) {
     if (shm > 48 * 1024) {
@@ -2704,7 +2762,7 @@ int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int nsm, const 
         if (ok != hipSuccess) return (int)ok;
     }
     launch_job_kernel(&k_arc_write_fused<T, EF>, dim3(nflat + nsm + dr.n + bj.n), dim3(kFuseNT), shm, st,
-                      (const MBatch*)(p->d_large_batches + bi), nflat, (const uint32_t*)p->d_keys, p->d_mws, ckey,
+                      (const MBatch*)(p->d_large_batches + bi), nflat, span, (const uint32_t*)p->d_keys, p->d_mws, ckey,
                       (const SegDev*)p->d_segs, (const int32_t*)p->d_small, sketch, (int)p->r, make_scale(ws),
                       rowlist, slotmap, dr, bj);
     return (int)hipGetLastError();
@@ -2784,15 +2842,20 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         // items of at most kFuseMaxRows rows: the refine runs inside the write blocks (one
         // launch fewer)
         constexpr bool fuse_ok = ARCTOPK_FUSED_WRITE != 0;  // build-time A/B switch
+        // ... and only while every write block is resident at once: each one carries a refine,
+        // so a second round of blocks costs more than the refine launch it saves (28 x [512,
+        // 512, 3, 3] as 896 one-range blocks: select 63 -> 74 us).  Blocks take spans of
+        // consecutive ranges instead, as many as keep the grid within kFuseMaxBlocks.
+        int nranges = 0;
+        for (int i = 0; i < b.cnt; ++i) nranges += b.it[i].nranges;
+        const int room = kFuseMaxBlocks - nsm - bj.n;
+        const int span = room > 0 ? std::max(1, (nranges + room - 1) / room) : kFuseMaxSpan + 1;
         int nflat = 0;
-        for (int i = 0; i < b.cnt; ++i) nflat += b.it[i].nranges;
-        // ... and only while every write block is resident at once: each one now carries a
-        // refine, so a second round of blocks costs more than the refine launch it saves
-        // (28 x [512, 512, 3, 3]: 896 blocks, select 63 -> 74 us)
+        for (int i = 0; i < b.cnt; ++i) nflat += (b.it[i].nranges + span - 1) / span;
         // The small selects sharing the launch run as 256-thread blocks: only when none has
         // more than 4,096 rows (1,024-thread blocks select 8 K-row segments faster than these
         // write blocks finish: ResNet-18's third DDP bucket measured 250 -> 241 GB/s fused)
-        if (fuse_ok && maxn <= kFuseMaxRows && nflat + nsm + bj.n <= kFuseMaxBlocks &&
+        if (fuse_ok && maxn <= kFuseMaxRows && span <= kFuseMaxSpan && nflat + nsm + bj.n <= kFuseMaxBlocks &&
             (nsm == 0 || p->small_lds <= 4096 * 4 + 16)) {
             size_t shm = std::max<size_t>((size_t)kFuseCap * 4, nsm ? (size_t)p->small_lds : 0);
             // the deferred decode rides in the last batch's launch (its blocks come after the
@@ -2802,9 +2865,9 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
             const DecodeRide<T> dr = make_ride<T>(take ? ride : nullptr);
             if (take) shm = std::max<size_t>(shm, (size_t)ride->rp->dec_lds_bytes);
             e = take && ride->ef == ARCTOPK_EF21
-                    ? launch_write_fused<T, ARCTOPK_EF21>(p, bi, nflat, nsm, ckey, sketch, ws, rowlist, slotmap, dr,
+                    ? launch_write_fused<T, ARCTOPK_EF21>(p, bi, nflat, span, nsm, ckey, sketch, ws, rowlist, slotmap, dr,
                                                           bj, shm, st)
-                    : launch_write_fused<T, ARCTOPK_EF_NONE>(p, bi, nflat, nsm, ckey, sketch, ws, rowlist, slotmap,
+                    : launch_write_fused<T, ARCTOPK_EF_NONE>(p, bi, nflat, span, nsm, ckey, sketch, ws, rowlist, slotmap,
                                                              dr, bj, shm, st);
             if (e) return e;
             if (bi == 0) *drawn = true;

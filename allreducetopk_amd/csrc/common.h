@@ -36,6 +36,12 @@
 #ifndef ARCTOPK_KEYS_MIN_ROWS
 #define ARCTOPK_KEYS_MIN_ROWS 4096     // ... rows per block at least
 #endif
+#ifndef ARCTOPK_FUSE_MAX_ROWS
+#define ARCTOPK_FUSE_MAX_ROWS 1048576  // largest item whose refine runs in the write blocks
+#endif
+#ifndef ARCTOPK_FUSE_MAX_SPAN
+#define ARCTOPK_FUSE_MAX_SPAN 8        // most ranges per fused write block
+#endif
 #ifndef ARCTOPK_FUSED_WRITE
 #define ARCTOPK_FUSED_WRITE 1          // refine folded into the write blocks where it fits
 #endif

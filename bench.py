@@ -383,6 +383,7 @@ def main():
         "ms_per_bucket": round(ms_per_step / nb, 4),
         "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
         "roofline": roof,
+        "algorithmic_bytes_per_call": {k: int(v) for k, v in alg.items()},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -197,14 +197,28 @@ def test_llama_layer_mix_ef21():
     assert run.checked == 4
 
 
-@pytest.mark.parametrize("ef", ["ef14", "ef21"])
-def test_resnet50_mix_arc(ef):
-    """configs[3] through ARC-TopK: 1x1 convs (m = 2, sketch twice the tensor), 3x3 convs
-    (m = 18) and 1-D BatchNorm tensors in one bucket."""
+@pytest.mark.parametrize("ef,nb,force_exchange", [("ef14", 1, False), ("ef21", 1, False),
+                                                   ("ef14", 2, False), ("ef21", 2, True)])
+def test_resnet50_mix_arc(ef, nb, force_exchange):
+    """configs[3] through ARC-TopK: 1x1 convs (m = 2, sketch twice the tensor; 524,288 and
+    1,048,576-row segments), 3x3 convs (m = 18) and 1-D BatchNorm tensors in one bucket.  With
+    two buckets per backward the first bucket's deferred decode rides in the second bucket's
+    fused write launch (spans of ranges per block)."""
     n = bucket_numel(RESNET50)
-    run = ArcRun(ef, seed=21)
+    run = ArcRun(ef, seed=21, force_exchange=force_exchange)
     for it in range(3):
-        run.step({0: (RESNET50, _randn(n, 1100 + it))})
+        run.step({b: (RESNET50, _randn(n, 1100 + 10 * it + b)) for b in range(nb)})
+
+
+def test_conv3x3_stack_ef14():
+    """28 x [512, 512, 3, 3] (m = 18, 131,072 rows each, 896 ranges of the multi-block
+    select): the fused write launch with two ranges per block."""
+    shapes = WORKLOADS["resnet18_conv"][1]
+    n = bucket_numel(shapes)
+    run = ArcRun("ef14", seed=41)
+    for it in range(2):
+        run.step({0: (shapes, _randn(n, 1300 + it))})
+    assert run.checked == 2
 
 
 @pytest.mark.parametrize("ef", ["ef14", "ef21"])
