@@ -37,10 +37,12 @@
 #define ARCTOPK_KEYS_MIN_ROWS 4096     // ... rows per block at least
 #endif
 #ifndef ARCTOPK_FUSE_MAX_ROWS
-#define ARCTOPK_FUSE_MAX_ROWS 1048576  // largest item whose refine runs in the write blocks
+#define ARCTOPK_FUSE_MAX_ROWS 262144   // largest item whose refine runs in the write blocks
 #endif
 #ifndef ARCTOPK_FUSE_MAX_SPAN
-#define ARCTOPK_FUSE_MAX_SPAN 8        // most ranges per fused write block
+#define ARCTOPK_FUSE_MAX_SPAN 1        // most ranges per fused write block (A/B: 8 measured
+                                       // slower on 28 x [512,512,3,3] 738 -> 695 GB/s and on
+                                       // the ResNet-50 mix with 1 M-row items 358 -> 256)
 #endif
 #ifndef ARCTOPK_FUSED_WRITE
 #define ARCTOPK_FUSED_WRITE 1          // refine folded into the write blocks where it fits
