@@ -134,7 +134,37 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
     if (t.mode == ENC_RAW) {
         const int64_t base = s.offset + t.row0;
         T* out = sketch + s.sketch_off + t.row0;
-        for (int64_t i = tid; i < t.nrows; i += 256) {
+        int64_t done = 0;
+        if constexpr (sizeof(T) == 4) {
+            if ((base & 3) == 0 && ((s.sketch_off + t.row0) & 3) == 0) {
+                // 16-B quads, all of a thread's loads issued before its stores (the scalar loop
+                // below is one dependent round trip per element: a store to E may not move above
+                // the next load from E)
+                constexpr int Q = 4;
+                constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
+                const int cnt4 = (int)(t.nrows >> 2);
+                for (int q0 = tid; q0 < cnt4; q0 += 256 * Q) {
+                    float4 gv[Q], ev[Q];
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        const int q = min(q0 + u * 256, cnt4 - 1);
+                        gv[u] = ldq<T, true>(G + base, q);
+                        if constexpr (LOAD_E) ev[u] = ldq<T, true>(E + base, q);
+                    }
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        const int q = q0 + u * 256;
+                        if (q < cnt4) {
+                            const float4 x = ef_combine4<T, EF, ERR_IN>(gv[u], ev[u]);
+                            if constexpr (WRITE_E) stq<T, true>(E + base, q, x);
+                            stq<T, false>(out, q, x);
+                        }
+                    }
+                }
+                done = (int64_t)cnt4 << 2;
+            }
+        }
+        for (int64_t i = done + tid; i < t.nrows; i += 256) {
             const float x = ef_apply1<T, EF, ERR_IN>(G + base, E + base, i);
             if constexpr (WRITE_E) st1<T, true>(E + base + i, x);
             st1<T>(out + i, x);
@@ -2364,6 +2394,88 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
                         stq<T, kNtDecode>(out + el, 0, make_float4(o[0], o[1], o[2], o[3]));
                     } else {
                         for (int j = 0; j < 4 && el + j < seg_end; ++j) st1<T>(out + el + j, o[j]);
+                    }
+                }
+            }
+            return;
+        }
+        if (ch.mode == 2) {  // 4 <= m < 256 fp32: lane per 16-B output quad, no LDS, no barrier
+            // The chunk's elements [e0, e1) of the segment; quads are 16-B aligned in memory,
+            // so the chunk's first / last quad may hold elements of a neighbouring chunk:
+            // those are masked out (and written element by element).  A quad spans at most two
+            // rows (m >= 4): slot and column of its first element, the wrap decided per element.
+            const int64_t e0 = ch.row0 * m, e1 = min<int64_t>(s.n, ch.row0 + ch.nrows) * m;
+            const int64_t qa = (s.offset + e0) >> 2, qb = (s.offset + e1 + 3) >> 2;
+            const int nq = (int)(qb - qa);
+            const int32_t* smg = slotmap + s.row_off;
+            const int64_t nrow_last = s.n - 1;
+            constexpr int UQ = 4;
+            for (int q0 = threadIdx.x; q0 < nq; q0 += 256 * UQ) {
+                float pv[UQ][4], gv[UQ][4];
+                int32_t sl0[UQ], sl1[UQ], col[UQ];
+#pragma unroll
+                for (int u = 0; u < UQ; ++u) {
+                    const int q = min(q0 + u * 256, nq - 1);
+                    const int64_t a = ((qa + q) << 2) - s.offset;  // segment element of quad slot 0
+                    const int64_t af = max(a, e0);
+                    const uint32_t r = fdiv((uint32_t)af, s.mdiv);
+                    const int c = (int)(af - (int64_t)r * m) - (int)(af - a);  // column of slot 0 (may be < 0 at the head)
+                    col[u] = c;
+                    sl0[u] = smg[r];
+                    sl1[u] = smg[min<int64_t>((int64_t)r + 1, nrow_last)];
+                    if constexpr (EF == ARCTOPK_EF21) {
+                        if (a >= e0 && a + 4 <= e1) {
+                            const float4 g = ldq<T, kNtDecode>(gE + s.offset + a, 0);
+                            gv[u][0] = g.x; gv[u][1] = g.y; gv[u][2] = g.z; gv[u][3] = g.w;
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                gv[u][j] = (a + j >= e0 && a + j < e1) ? to_f(gE[s.offset + a + j]) : 0.f;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UQ; ++u) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int cj = col[u] + j;
+                        const bool wrap = cj >= m;
+                        const int32_t slot = wrap ? sl1[u] : sl0[u];
+                        const int cc = wrap ? cj - m : cj;
+                        pv[u][j] = (slot >= 0 && cj >= 0) ? to_f(pk[(int64_t)slot * m + cc]) : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UQ; ++u) {
+                    const int q = q0 + u * 256;
+                    if (q >= nq) break;
+                    const int64_t a = ((qa + q) << 2) - s.offset;
+                    float o[4];
+                    bool selj[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int cj = col[u] + j;
+                        selj[j] = (cj >= m ? sl1[u] : sl0[u]) >= 0;
+                        float v = selj[j] ? mean1(pv[u][j]) : 0.f;
+                        if constexpr (EF == ARCTOPK_EF21) v = selj[j] ? rnd<T>(gv[u][j] + v) : gv[u][j] + 0.f;
+                        o[j] = v;
+                    }
+                    if (a >= e0 && a + 4 <= e1) {
+                        stq<T, kNtDecode>(out + s.offset + a, 0, make_float4(o[0], o[1], o[2], o[3]));
+                        if constexpr (EF == ARCTOPK_EF21) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (selj[j]) st1<T>(gE + s.offset + a + j, o[j]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            if (a + j >= e0 && a + j < e1) {
+                                st1<T>(out + s.offset + a + j, o[j]);
+                                if constexpr (EF == ARCTOPK_EF21)
+                                    if (selj[j]) st1<T>(gE + s.offset + a + j, o[j]);
+                            }
+                        }
                     }
                 }
             }

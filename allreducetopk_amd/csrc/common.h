@@ -44,6 +44,12 @@
                                        // slower on 28 x [512,512,3,3] 738 -> 695 GB/s and on
                                        // the ResNet-50 mix with 1 M-row items 358 -> 256)
 #endif
+#ifndef ARCTOPK_QUAD_DEC
+#define ARCTOPK_QUAD_DEC 1             // short-row (4 <= m < 256) fp32 decode: lane per output quad
+#endif                                 // (0: the chunk composed in an LDS tile)
+#ifndef ARCTOPK_QUAD_DEC_CHUNK
+#define ARCTOPK_QUAD_DEC_CHUNK 8192    // ... elements per chunk
+#endif
 #ifndef ARCTOPK_FUSED_WRITE
 #define ARCTOPK_FUSED_WRITE 1          // refine folded into the write blocks where it fits
 #endif
@@ -65,6 +71,13 @@
 #endif
 #ifndef ARCTOPK_SHORT_DEC_CHUNK
 #define ARCTOPK_SHORT_DEC_CHUNK 4096   // elements per short-row (m < 256) decode chunk
+#endif
+#ifndef ARCTOPK_ENC_MIN_TILE
+#define ARCTOPK_ENC_MIN_TILE 2048      // fewest elements per wave-per-row encode tile
+                                       // (A/B: ResNet-18 DDP buckets 292 -> 304 GB/s vs 8192)
+#endif
+#ifndef ARCTOPK_ENC_ROWS_MULT
+#define ARCTOPK_ENC_ROWS_MULT 1        // rows per wave-per-row encode tile rounded up to a multiple
 #endif
 #ifndef ARCTOPK_ENC_PKFMA
 #define ARCTOPK_ENC_PKFMA 0            // fp32 encode: packed FMAs over even / odd columns
@@ -336,7 +349,8 @@ struct VDrawJob {      // a projection draw riding in the trailing blocks of ano
 
 struct Chunk {         // pack: selected-row range (mode 0) or row range (mode 1); decode: row range
     int32_t seg;
-    int32_t mode;      // 1: m in {1, 2}, fp32, 16-B aligned: quad streams over every row
+    int32_t mode;      // 1: m in {1, 2}, fp32, 16-B aligned: quad streams over every row;
+                       // decode 2: 4 <= m < 256 fp32, lane per output quad
     int64_t row0;
     int64_t nrows;
 };

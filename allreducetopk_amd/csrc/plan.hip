@@ -118,7 +118,9 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         if (s.kind != ARCTOPK_SEG_RAW && !(s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536))
             row_work += s.n * s.m;
     const int64_t target = kEncTargetBlocks;
-    const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(8192, row_work / target));
+    // (small buckets: tiles down to ARCTOPK_ENC_MIN_TILE elements -- at least one row per wave --
+    // so a bucket of a few rows spreads them over waves instead of walking them in sequence)
+    const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(ARCTOPK_ENC_MIN_TILE, row_work / target));
     // chunk sizes (build-time A/B switches, common.h): short rows (m < 256) and the m <= 2
     // streams get smaller chunks, more blocks in flight (ResNet-50 1x1 mix, 2048-element
     // stream pack chunks: 346 -> 356 GB/s; 4096-element decode chunks: +3 %)
@@ -174,7 +176,10 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 split_ids.push_back((int32_t)i);
                 split_rows_max = std::max<int64_t>(split_rows_max, s.n);
             }
-            const int64_t per = std::max<int64_t>(4, tile_elems / std::min<int64_t>(clen, s.m));
+            // rows per tile: a multiple of ARCTOPK_ENC_ROWS_MULT (4: every wave of the block the
+            // same number of rows)
+            constexpr int64_t rm = ARCTOPK_ENC_ROWS_MULT;
+            const int64_t per = std::max<int64_t>(4, (tile_elems / std::min<int64_t>(clen, s.m) + rm - 1) / rm * rm);
             const int64_t ntiles = (s.n + per - 1) / per;
             for (int part = 0; part < nparts; ++part) {
                 const int64_t c0 = part * clen;
@@ -214,7 +219,12 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 pack.push_back(Chunk{(int32_t)i, 0, j, std::min(per, s.k_rows - j)});
         }
         // ---- decode chunks: all rows
-        {
+        if (small_tile && dtype == ARCTOPK_F32 && ARCTOPK_QUAD_DEC) {
+            // mode 2: lane per 16-B output quad, rows of whole chunks (no LDS tile)
+            const int64_t per = std::max<int64_t>(1, (int64_t)ARCTOPK_QUAD_DEC_CHUNK / s.m);
+            for (int64_t row = 0; row < s.n; row += per)
+                dec.push_back(Chunk{(int32_t)i, 2, row, std::min(per, s.n - row)});
+        } else {
             int64_t per = std::max<int64_t>(min_rows, (s.m < 256 ? short_dec_elems : dec_elems) / s.m);
             if (stream_small) per = (per + 3) / 4 * 4;  // mode 1: whole quads per chunk
             if (small_tile)  // the chunk tile lives in LDS: <= 64 KiB

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
 TAG=$(echo "${BENCH_ARGS}" | tr -c 'a-zA-Z0-9_' '_' | sed 's/__*/_/g')
 for rep in 1 2; do
-  for lib in product ${VARIANTS}; do
+  for lib in ${AB_LIBS:-product} ${VARIANTS}; do
     if [ "$lib" = product ]; then L=""; else L="allreducetopk_amd/lib/var/libarctopk_$lib.so"; fi
     LOG=gpurun_out/ab/${lib}${TAG}.log
     ARCTOPK_LIB=$L timeout -k 10 200 python bench.py --steps 50 --no-cpu-baseline --no-forced-exchange ${BENCH_ARGS} > $LOG 2>&1 || { tail -5 $LOG; exit 1; }

@@ -2,6 +2,7 @@
 plus per-kernel averages over the whole trace."""
 import collections
 import csv
+import os
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
@@ -13,7 +14,8 @@ for r in rows:
 for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:14]:
     print(f"  {k:60s} n={len(v):5d} avg={sum(v) / len(v):8.2f} us")
 enc = [i for i, r in enumerate(rows) if "k_encode" in r["Kernel_Name"]]
-start = enc[-2] if len(enc) > 1 else enc[-1]
+back = int(os.environ.get("KSEQ_BACK", "2"))  # encodes back from the end (one step: buckets + 1)
+start = enc[-back] if len(enc) >= back else enc[0]
 print("  -- one call:")
 t0 = int(rows[start]["Start_Timestamp"])
 for r in rows[start:start + 40]:
