@@ -397,11 +397,12 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         float acc[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) acc[j] = 0.f;
-#if ARCTOPK_ENC_PKFMA
+        // packed FMAs (v_pk_fma_f32) on the G-only stream (A/B: noef headline encode 57.7 -> 53.1
+        // us; with E loads the EF14 encode measured 140 -> 146 us, so those keep scalar FMAs)
+        constexpr bool kPk = ARCTOPK_ENC_PKFMA == 1 || (ARCTOPK_ENC_PKFMA == 2 && !LOAD_E);
         f2_t acc2[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) acc2[j] = f2_t{0.f, 0.f};
-#endif
 
         auto issue = [&](float4 (&gx)[U][PQ], float4 (&ex)[U][PQ], int64_t r_, int st_) {
             const T* gp = G + s.offset + r_ * m + c0;
@@ -429,44 +430,44 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int h = 0; h < PQ; ++h)
                     if (!ok) x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-#if ARCTOPK_ENC_PKFMA
-                // packed FMA (v_pk_fma_f32): even / odd columns accumulate separately, two
-                // products per instruction; the halves are added at the row end
+                if constexpr (kPk) {
+                    // packed FMA (v_pk_fma_f32): even / odd columns accumulate separately, two
+                    // products per instruction; the halves are added at the row end
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    f2_t a = acc2[j];
+                    for (int j = 0; j < R; ++j) {
+                        f2_t a = acc2[j];
 #pragma unroll
-                    for (int h = 0; h < PQ; ++h) {
-                        const float4 v = vt4[j * m4 + c * PQ + h];
-                        a = __builtin_elementwise_fma(f2_t{x[h].x, x[h].y}, f2_t{v.x, v.y}, a);
-                        a = __builtin_elementwise_fma(f2_t{x[h].z, x[h].w}, f2_t{v.z, v.w}, a);
+                        for (int h = 0; h < PQ; ++h) {
+                            const float4 v = vt4[j * m4 + c * PQ + h];
+                            a = __builtin_elementwise_fma(f2_t{x[h].x, x[h].y}, f2_t{v.x, v.y}, a);
+                            a = __builtin_elementwise_fma(f2_t{x[h].z, x[h].w}, f2_t{v.z, v.w}, a);
+                        }
+                        acc2[j] = a;
                     }
-                    acc2[j] = a;
-                }
-#else
+                } else {
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    float a = acc[j];
+                    for (int j = 0; j < R; ++j) {
+                        float a = acc[j];
 #pragma unroll
-                    for (int h = 0; h < PQ; ++h) {
-                        const float4 v = vt4[j * m4 + c * PQ + h];
-                        a = fmaf(x[h].x, v.x, a);
-                        a = fmaf(x[h].y, v.y, a);
-                        a = fmaf(x[h].z, v.z, a);
-                        a = fmaf(x[h].w, v.w, a);
+                        for (int h = 0; h < PQ; ++h) {
+                            const float4 v = vt4[j * m4 + c * PQ + h];
+                            a = fmaf(x[h].x, v.x, a);
+                            a = fmaf(x[h].y, v.y, a);
+                            a = fmaf(x[h].z, v.z, a);
+                            a = fmaf(x[h].w, v.w, a);
+                        }
+                        acc[j] = a;
                     }
-                    acc[j] = a;
                 }
-#endif
             }
             if (st_ == steps - 1) {
-#if ARCTOPK_ENC_PKFMA
+                if constexpr (kPk) {
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                    acc[j] = acc2[j].x + acc2[j].y;
-                    acc2[j] = f2_t{0.f, 0.f};
+                    for (int j = 0; j < R; ++j) {
+                        acc[j] = acc2[j].x + acc2[j].y;
+                        acc2[j] = f2_t{0.f, 0.f};
+                    }
                 }
-#endif
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
                 // every lane holds all R sums; lanes 0..R-1 store one each.  (The compiler

@@ -80,8 +80,8 @@
 #define ARCTOPK_ENC_ROWS_MULT 1        // rows per wave-per-row encode tile rounded up to a multiple
 #endif
 #ifndef ARCTOPK_ENC_PKFMA
-#define ARCTOPK_ENC_PKFMA 0            // fp32 encode: packed FMAs over even / odd columns
-#endif
+#define ARCTOPK_ENC_PKFMA 2            // fp32 encode: packed FMAs over even / odd columns (1: always,
+#endif                                 // 2: on the G-only stream (noef, first EF14 call), 0: never)
 #ifndef ARCTOPK_ENC_UNITS_G_ONLY
 #define ARCTOPK_ENC_UNITS_G_ONLY 4     // fp32 encode without E loads: 16-B units per lane per step
 #endif
