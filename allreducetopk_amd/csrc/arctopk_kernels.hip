@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
         constexpr int PQ = kQuadsPer16<T>;  // quads per 16-B unit
         constexpr bool LOAD_E = (EF == ARCTOPK_EF21) || (EF == ARCTOPK_EF14 && ERR_IN);
         // units per lane per step: a stream of G alone keeps more of them in flight
-        constexpr int U = (LOAD_E ? 4 : ARCTOPK_ENC_UNITS_G_ONLY) / PQ;
+        constexpr int U = (LOAD_E ? ARCTOPK_ENC_UNITS_GE : ARCTOPK_ENC_UNITS_G_ONLY) / PQ;
         const int m4 = cl >> 2;   // quads of this tile row
         const int mu = m4 / PQ;   // 16-B units (the plan makes m4 a multiple of PQ)
         const int steps = (mu + 64 * U - 1) / (64 * U);
@@ -410,8 +410,8 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
             for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: no exec-masked blocks
                 const int c = min(st_ * 64 * U + u * 64 + lane, mu - 1);
-                ld16<T, true>(gp, c, gx[u]);
-                if constexpr (LOAD_E) ld16<T, true>(ep, c, ex[u]);
+                ld16<T, kEncNtLoad>(gp, c, gx[u]);
+                if constexpr (LOAD_E) ld16<T, kEncNtLoad>(ep, c, ex[u]);
             }
         };
         auto consume = [&](float4 (&gx)[U][PQ], float4 (&ex)[U][PQ], int64_t r_, int st_) {
@@ -425,7 +425,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int h = 0; h < PQ; ++h) x[h] = ef_combine4<T, EF, ERR_IN>(gx[u][h], ex[u][h]);
                 if constexpr (WRITE_E) {
-                    if (ok) st16<T, true>(ep, c, x);
+                    if (ok) st16<T, kEncNtStore>(ep, c, x);
                 }
 #pragma unroll
                 for (int h = 0; h < PQ; ++h)
@@ -2779,9 +2779,10 @@ template <typename T, int R>
 int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
                     hipStream_t st) {
     if (p->n_enc > 0) {
-        dim3 grid(p->n_enc), block(256);
+        const bool use_e = p->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
+        dim3 grid(use_e ? p->n_enc_e : p->n_enc), block(256);
         const size_t lds = (size_t)p->enc_lds_bytes;
-        const EncTile* tiles = p->d_enc;
+        const EncTile* tiles = use_e ? p->d_enc_e : p->d_enc;
         float* pb = p->d_part;
         if (ef == ARCTOPK_EF_NONE)
             hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);

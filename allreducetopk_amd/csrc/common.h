@@ -72,6 +72,12 @@
 #ifndef ARCTOPK_SHORT_DEC_CHUNK
 #define ARCTOPK_SHORT_DEC_CHUNK 4096   // elements per short-row (m < 256) decode chunk
 #endif
+#ifndef ARCTOPK_ENC_TARGET_BLOCKS_E
+#define ARCTOPK_ENC_TARGET_BLOCKS_E 4096  // ... for the fp32 kernels that also stream E (large tensors)
+#endif
+#ifndef ARCTOPK_ENC_E_MIN_ROWS
+#define ARCTOPK_ENC_E_MIN_ROWS 16384   // ... for tensors of at least this many rows
+#endif
 #ifndef ARCTOPK_ENC_MIN_TILE
 #define ARCTOPK_ENC_MIN_TILE 2048      // fewest elements per wave-per-row encode tile
                                        // (A/B: ResNet-18 DDP buckets 292 -> 304 GB/s vs 8192)
@@ -84,6 +90,15 @@
 #endif                                 // 2: on the G-only stream (noef, first EF14 call), 0: never)
 #ifndef ARCTOPK_ENC_UNITS_G_ONLY
 #define ARCTOPK_ENC_UNITS_G_ONLY 4     // fp32 encode without E loads: 16-B units per lane per step
+#endif
+#ifndef ARCTOPK_ENC_UNITS_GE
+#define ARCTOPK_ENC_UNITS_GE 4         // fp32 encode with E loads: 16-B units of G (and of E) per lane per step
+#endif
+#ifndef ARCTOPK_ENC_NT_LOAD
+#define ARCTOPK_ENC_NT_LOAD 1          // fp32 encode rows: nontemporal G / E loads
+#endif
+#ifndef ARCTOPK_ENC_NT_STORE
+#define ARCTOPK_ENC_NT_STORE 1         // fp32 encode rows: nontemporal E stores
 #endif
 #ifndef ARCTOPK_ENC_UNITS_BF16
 #define ARCTOPK_ENC_UNITS_BF16 4       // bf16 encode rows: 16-B units per lane per step
@@ -309,6 +324,8 @@ template <typename T, bool NT = false> __device__ __forceinline__ void st1(T* p,
 #endif
 constexpr bool kNtPack = ARCTOPK_NT_PACK != 0;
 constexpr bool kNtDecode = ARCTOPK_NT_DECODE != 0;
+constexpr bool kEncNtLoad = ARCTOPK_ENC_NT_LOAD != 0;
+constexpr bool kEncNtStore = ARCTOPK_ENC_NT_STORE != 0;
 constexpr int kSmallTileRows = 1024;  // rows of a small-m pack/decode chunk (LDS slot table)
 
 // encode tile modes
@@ -370,6 +387,8 @@ struct arctopk_plan {
     arctopk::SegDev* d_segs;
     arctopk::EncTile* d_enc;      // encode tiles (k_encode)
     int n_enc;
+    arctopk::EncTile* d_enc_e;    // encode tiles of the fp32 kernels that also stream E (0: use d_enc)
+    int n_enc_e;
     int enc_lds_bytes;            // dynamic LDS of the encode launch
     float* d_part;                // partial sketches of column-split segments
     int32_t* d_split;             // ids of column-split segments

@@ -121,6 +121,14 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     // (small buckets: tiles down to ARCTOPK_ENC_MIN_TILE elements -- at least one row per wave --
     // so a bucket of a few rows spreads them over waves instead of walking them in sequence)
     const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(ARCTOPK_ENC_MIN_TILE, row_work / target));
+    // a second table for the fp32 kernels that also stream E (EF14 after the first call, EF21):
+    // tensors of at least ARCTOPK_ENC_E_MIN_ROWS rows (embeddings) get tiles sized for twice the
+    // block target (A/B: Llama-1B embedding bucket 1,072 -> 1,137 GB/s, RoBERTa 994 -> 1,008;
+    // for every tensor it cost the headline 1 % and the G-only and bf16 kernels 2-3 %)
+    const int64_t tile_elems_e = std::min<int64_t>(
+        65536, std::max<int64_t>(ARCTOPK_ENC_MIN_TILE, row_work / (int64_t)ARCTOPK_ENC_TARGET_BLOCKS_E));
+    std::vector<EncTile> enc_e;
+    bool any_e = false;
     // chunk sizes (build-time A/B switches, common.h): short rows (m < 256) and the m <= 2
     // streams get smaller chunks, more blocks in flight (ResNet-50 1x1 mix, 2048-element
     // stream pack chunks: 346 -> 356 GB/s; 4096-element decode chunks: +3 %)
@@ -153,14 +161,16 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         if (s.kind == ARCTOPK_SEG_RAW) {
             const int64_t per = 4096;
             for (int64_t e = 0; e < s.n; e += per)
-                enc.push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e), 0, 1, -1, 1});
+                for (std::vector<EncTile>* dst : {&enc, &enc_e})
+                    dst->push_back(EncTile{(int32_t)i, ENC_RAW, e, std::min(per, s.n - e), 0, 1, -1, 1});
         } else if (s.m < kSmallM && (kTileRows * s.m + s.m * r) * 4 <= 65536) {
             // rows per tile: ~kSmallTileBytes of the tensor (multiples of 256 rows), so the
             // smallest m (1x1 convs, m = 2) does not run thousands of 2 KiB blocks
             const int64_t tr = std::max<int64_t>(kTileRows, kSmallTileBytes / (4 * s.m) / kTileRows * kTileRows);
             for (int64_t row = 0; row < s.n; row += tr)
-                enc.push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(tr, s.n - row),
-                                      0, (int32_t)s.m, -1, 1});
+                for (std::vector<EncTile>* dst : {&enc, &enc_e})
+                    dst->push_back(EncTile{(int32_t)i, ENC_TILE, row, std::min<int64_t>(tr, s.n - row),
+                                           0, (int32_t)s.m, -1, 1});
             lds = std::max<int>(lds, (int)(std::min(tr, s.n) * s.m * 4 + ((s.m * r + 3) & ~3) * 4));
         } else {
             const int mode = g.vec ? ENC_ROW_VEC : ENC_ROW_SCALAR;
@@ -179,12 +189,16 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             // rows per tile: a multiple of ARCTOPK_ENC_ROWS_MULT (4: every wave of the block the
             // same number of rows)
             constexpr int64_t rm = ARCTOPK_ENC_ROWS_MULT;
-            const int64_t per = std::max<int64_t>(4, (tile_elems / std::min<int64_t>(clen, s.m) + rm - 1) / rm * rm);
-            const int64_t ntiles = (s.n + per - 1) / per;
+            for (int tab = 0; tab < 2; ++tab)
             for (int part = 0; part < nparts; ++part) {
+                const bool big = s.n >= (int64_t)ARCTOPK_ENC_E_MIN_ROWS;
+                any_e = any_e || (tab && big);
+                const int64_t te = tab && big ? tile_elems_e : tile_elems;
+                const int64_t per = std::max<int64_t>(4, (te / std::min<int64_t>(clen, s.m) + rm - 1) / rm * rm);
+                const int64_t ntiles = (s.n + per - 1) / per;
                 const int64_t c0 = part * clen;
                 const int64_t cl = std::min<int64_t>(clen, s.m - c0);
-                std::vector<EncTile>& dst = enc;
+                std::vector<EncTile>& dst = tab ? enc_e : enc;
                 for (int64_t ti = 0; ti < ntiles; ++ti) {
                     if (interleave)  // rows ti, ti + ntiles, ...: consecutive blocks, adjacent rows
                         dst.push_back(EncTile{(int32_t)i, mode, ti, (s.n - ti + ntiles - 1) / ntiles,
@@ -249,6 +263,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     p->h_segs = new arctopk_segment[segs.size()];
     std::copy(segs.begin(), segs.end(), p->h_segs);
     p->n_enc = (int)enc.size();
+    p->n_enc_e = dtype == ARCTOPK_F32 && any_e ? (int)enc_e.size() : 0;
     p->n_pack = (int)pack.size();
     p->n_dec = (int)dec.size();
     pack_begin.push_back((int32_t)pack.size());
@@ -271,6 +286,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     } while (0)
     ALLOC_COPY(p->d_segs, dsegs);
     ALLOC_COPY(p->d_enc, enc);
+    if (p->n_enc_e) ALLOC_COPY(p->d_enc_e, enc_e);
     ALLOC_COPY(p->d_pack, pack);
     ALLOC_COPY(p->d_dec, dec);
     ALLOC_COPY(p->d_small, small_ids);
@@ -359,6 +375,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     (void)hipSetDevice(p->device);
     if (p->d_segs) (void)hipFree(p->d_segs);
     if (p->d_enc) (void)hipFree(p->d_enc);
+    if (p->d_enc_e) (void)hipFree(p->d_enc_e);
     if (p->d_pack) (void)hipFree(p->d_pack);
     if (p->d_dec) (void)hipFree(p->d_dec);
     if (p->d_keys) (void)hipFree(p->d_keys);
