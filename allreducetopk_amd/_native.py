@@ -25,7 +25,11 @@ BF16 = 1
 DTYPE_CODE = {torch.float32: F32, torch.bfloat16: BF16}  # bucket dtype -> ARCTOPK_F32 / _BF16
 
 STATUS = {1001: "invalid argument", 1002: "ND tensor numel not divisible by 2*t^2",
-          1003: "unsupported dtype", 1004: "empty tensor", 1005: "RCCL library not loadable"}
+          1003: "unsupported dtype", 1004: "empty tensor", 1005: "RCCL library not loadable",
+          1006: "communicator timed out (a collective or the communicator's creation outlived the "
+                "process group's timeout; every RCCL communicator of the library was aborted)",
+          1007: "communicator aborted"}
+ETIMEOUT, EABORTED = 1006, 1007
 ECOMM = 1100  # + ncclResult_t
 NMARKS = 8    # ARCTOPK_MARK_*: phase markers of a step
 MARKS = {"start": 0, "draw": 1, "encode": 2, "sketch_allreduce": 3, "select": 4, "pack": 5,
@@ -64,7 +68,12 @@ _SIGS = {
                                c_uint64, c_void_p, c_uint64, c_void_p, c_void_p]),
     "arctopk_comm_unique_id": (c_int32, [c_char_p, c_void_p]),
     "arctopk_comm_init_rccl": (c_int32, [c_char_p, c_char_p, c_int32, c_int32, c_int32, POINTER(c_void_p)]),
+    "arctopk_comm_init_rccl_timeout": (c_int32, [c_char_p, c_char_p, c_int32, c_int32, c_int32, c_int64,
+                                                 POINTER(c_void_p)]),
+    "arctopk_comm_status": (c_int32, [c_void_p]),
+    "arctopk_comm_abort": (c_int32, [c_void_p]),
     "arctopk_comm_init_callback": (c_int32, [ALLREDUCE_FN, c_void_p, c_int32, c_int32, POINTER(c_void_p)]),
+    "arctopk_comm_init_wire": (c_int32, [c_int32, c_double, c_double, c_int32, c_int32, POINTER(c_void_p)]),
     "arctopk_comm_destroy": (c_int32, [c_void_p]),
     "arctopk_comm_size": (c_int32, [c_void_p]),
     "arctopk_comm_allreduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p]),

@@ -27,7 +27,7 @@ INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libarctopk.so")
 SOURCES = ["plan.hip", "arctopk_kernels.hip", "sparse_kernels.hip", "mselect.hip", "vdraw.hip",
-           "projection.cpp", "step.cpp", "exchange.cpp"]
+           "projection.cpp", "step.cpp", "exchange.cpp", "wire.hip"]
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
          "-Wno-unused-function"]

@@ -343,9 +343,19 @@ class GroupTopKState(HookState):
         # Deferred decodes: a step's decode runs inside a later call (in
         # that call's select launch, whose latency it hides; or, with collectives, once the
         # packed all-reduce on the exchange stream is done), and the backward's last bucket
-        # finishes them all.  FIFO of (plan, its Future, its markers, bucket tensor, stream).
-        self.defer_decode = True
+        # finishes them all.  The Future of a deferred step completes only when its decode is
+        # enqueued (a later hook call), so deferral needs a caller that waits on no bucket's
+        # Future before the backward's last hook call -- DDP's Reducer (finalize, after every
+        # bucket).  None (default): defer for DDP's own buckets (dist.GradBucket, or a state
+        # registered by register_comm_hook_for_ddp_model); True: always (callers that wait like
+        # DDP: bench.py); False: never (every Future complete on return).
+        # FIFO of (plan, its Future, its markers, bucket tensor, stream, residuals kept alive).
+        self.defer_decode = None
         self._x_pend: List[tuple] = []
+        # measurement only: emulated-wire communicators (exchange.Comm.wire parameters, e.g.
+        # dict(ranks=8, busbw_gbs=350)) instead of real ones; with force_exchange at world
+        # size 1 the step then runs beside the local cost of an N-rank ring
+        self.emulate_wire = None
         # Sketch all-reduces on a communicator of their own ("separate") or on the packed
         # values' communicator ("shared": a sketch then queues behind the previous bucket's
         # packed all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
@@ -436,23 +446,45 @@ class GroupTopKState(HookState):
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")
         device = torch.device(device)
-        sk, pk = X.make_comms(group, device, self.sketch_comm)
+        wire = self.emulate_wire
+        if wire is not None and group.size() != 1:
+            raise RuntimeError("emulate_wire models the wire on one GPU: world size must be 1")
+        sk, pk = X.make_comms(group, device, self.sketch_comm, wire=wire)
         self._comms = (group, device, sk, pk)
+
+    def reset_exchange_comms(self) -> None:
+        """Drop the exchange communicators (after finishing deferred decodes); the next
+        compressed call makes new ones (e.g. after switching emulate_wire)."""
+        self.flush_exchange()
+        self._comms = None
+
+    def _raise_if_comm_failed(self) -> None:
+        """RuntimeError when a communicator of the exchange failed (watchdog timeout, RCCL
+        error, abort): the reference's collectives raise from the hook in that case."""
+        if self._comms is not None:
+            for c in (self._comms[2], self._comms[3]):
+                c.raise_if_failed()
 
     def flush_exchange(self, upto=None) -> None:
         """Enqueue deferred decodes in call order (each on the stream of its call) and
         complete their Futures: all of them, or up to and including `upto`'s.  The hook does
         this itself in later calls; a Python wait()/value() on such a Future does it too."""
         while self._x_pend:
-            plan, fut, marks, t, sid = self._x_pend.pop(0)
+            plan, fut, marks, t, sid, _keep = self._x_pend.pop(0)
             N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
             fut.set_result(t)
             if fut is upto:
                 break
+        self._raise_if_comm_failed()
 
     def state_dict(self) -> dict:
         self.flush_exchange()  # the deferred decode writes gE (EF21)
         return super().state_dict()
+
+    def load_state_dict(self, sd: dict, device=None) -> None:
+        # a pending decode writes into the residuals being replaced (ADVICE r03)
+        self.flush_exchange()
+        super().load_state_dict(sd, device)
 
     def _exchange_comms(self, group, dev):
         if self._comms is None:
@@ -887,10 +919,11 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         # ONE native call per bucket (arctopk_exchange_step): the kernels, the collectives at
         # world size > 1 (or with force_exchange: the N > 1 code path over one-rank
         # communicators), and earlier buckets' deferred decodes
-        comms = world_size > 1 or state.force_exchange
+        comms = world_size > 1 or state.force_exchange or state.emulate_wire is not None
         sk = pk = None
         if comms:
             sk, pk = state._exchange_comms(group, dev)
+            state._raise_if_comm_failed()
             if plan.comm_registered is not pk:
                 sk.register(plan.sketch)
                 pk.register(plan.packed)
@@ -904,9 +937,14 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             vptr = V.data_ptr()
         # deferred except for the last bucket of a backward (nothing follows it), which then
         # finishes every earlier deferred decode: nothing is left in flight when it returns
-        defer = state.defer_decode and state.async_exchange and not bucket.is_last()
+        dd = state.defer_decode
+        if dd is None:  # DDP's own buckets (or a DDP-registered state): Futures waited at finalize
+            dd = isinstance(bucket, dist.GradBucket) or getattr(state, "_ddp_registered", False)
+        defer = dd and state.async_exchange and not bucket.is_last()
         pend = state._x_pend
-        if any(e_[0] is plan for e_ in pend):  # (a caller that skipped buckets: finish first)
+        # finish first: a caller that skipped buckets, or one whose stream changed since a
+        # pending step (its decode is enqueued on that step's own stream)
+        if any(e_[0] is plan or e_[4] != sid for e_ in pend):
             state.flush_exchange()
         # the decode riding in this call's select launch: the previous bucket's without
         # collectives, the one before it with them (its all-reduce has had a whole call to
@@ -951,7 +989,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         if defer:
             fut = ExchangeFuture()
             fut._arctopk_state = state
-            pend.append((plan, fut, marks, input_tensor, sid))
+            pend.append((plan, fut, marks, input_tensor, sid, (err, gerr)))
         else:
             fut = torch.futures.Future()
             fut.set_result(input_tensor)

@@ -8,7 +8,9 @@ Per bucket call (all on the caller's stream, no host synchronisation):
     TopK : topk_select  exact element top-k of |x| per tensor (radix select),
                         ascending int32 indices + gathered values
     RandK: indices      torch.randperm(numel, device)[:k] after the shared reseed
-                        (parity mode: the reference's own draw), or a keyed device
+                        (index_source="torch": the reference's own draw on a GPU), the
+                        same draw on the CPU generator (index_source="host": the reference
+                        run on CPU, as the golden vectors were made), or a keyed device
                         permutation (index_source="hash", perf mode); then gather
     residual        EF14: E[idx] = 0 | EF21: E[idx] += values
     RandK: all_reduce(values)              -> decode: zero + scatter(values / ws)
@@ -67,8 +69,8 @@ class SparseState(HookState):
         self.error_dict: Dict[int, torch.Tensor] = {}
         self.global_error_dict: Dict[int, torch.Tensor] = {}
         self.random_seed = random_seed
-        if index_source not in ("torch", "hash"):
-            raise ValueError("index_source must be 'torch' or 'hash'")
+        if index_source not in ("torch", "host", "hash"):
+            raise ValueError("index_source must be 'torch', 'host' or 'hash'")
         self.index_source = index_source
         self._workspace = None
         self._ws_bytes: Dict[tuple, int] = {}
@@ -191,6 +193,14 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
         if state.index_source == "torch":  # the reference's own draw (:20), per tensor in order
             for t, k, ko in zip(tensors, ks, k_off):
                 indices[ko:ko + k].copy_(torch.randperm(t.numel(), device=device)[:k])
+        elif state.index_source == "host":
+            # parity mode: the reference run on CPU (sparse_hook_c4.py:20 with CPU tensors, after
+            # the reseed at :269-274) draws from the CPU generator; the same draws, in tensor
+            # order (so the generator is left where the reference leaves it), copied to the GPU
+            host = torch.empty(sum_k, dtype=torch.int32)
+            for t, k, ko in zip(tensors, ks, k_off):
+                host[ko:ko + k].copy_(torch.randperm(t.numel())[:k])
+            indices.copy_(host)
         else:
             N.check(L.arctopk_randk_indices(nt, a_n, a_k, a_ko, int(seed), indices.data_ptr(),
                                             stream), "arctopk_randk_indices")

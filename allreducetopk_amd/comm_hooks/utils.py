@@ -158,6 +158,7 @@ def register_comm_hook_for_ddp_model(model, process_group, args, optimizer=None)
                 # the exchange's communicators, now, on every rank (collective)
                 dev = next((p.device for p in model.parameters() if p.is_cuda), None)
                 hook_state.init_exchange_comms(dev)
+        hook_state._ddp_registered = True  # DDP waits on the Futures at finalize: decodes may defer
         model.register_comm_hook(hook_state, group_topk_hook)
     elif args.compressor == "noop":
         from torch.distributed.algorithms.ddp_comm_hooks.debugging_hooks import noop_hook

@@ -3044,20 +3044,31 @@ int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* 
     return (int)hipGetLastError();
 }
 
+// `done` as in pack_launch (the decode after an inline all-reduce, watched by exchange.cpp)
+template <typename T, int EF>
+void decode_launch(dim3 grid, size_t lds, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
+                   const T* packed, const int32_t* slotmap, Scale sc, T* gerr, T* out) {
+    if (done)
+        hipExtLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, nullptr, done, 0, segs, ch, packed,
+                              slotmap, sc, gerr, out);
+    else
+        hipLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, segs, ch, packed, slotmap, sc, gerr, out);
+}
+
 template <typename T>
 int launch_decode(const arctopk_plan* p, int c0, int c1, const void* packed_, const int32_t* slotmap,
-                  int32_t ws, int32_t ef, void* gerr_, void* out_, hipStream_t st) {
+                  int32_t ws, int32_t ef, void* gerr_, void* out_, hipStream_t st, hipEvent_t done = nullptr) {
     const T* packed = static_cast<const T*>(packed_);
     T* gerr = static_cast<T*>(gerr_);
     T* out = static_cast<T*>(out_);
-    dim3 grid(c1 - c0), block(256);
+    dim3 grid(c1 - c0);
     const Chunk* ch = p->d_dec + c0;
     const Scale sc = make_scale(ws);
     const size_t lds = (size_t)p->dec_lds_bytes;
     if (ef == ARCTOPK_EF21)
-        hipLaunchKernelGGL((k_decode<T, ARCTOPK_EF21>), grid, block, lds, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, packed, slotmap, sc, gerr, out);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        hipLaunchKernelGGL((k_decode<T, ARCTOPK_EF_NONE>), grid, block, lds, st, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, packed, slotmap, sc, gerr, out);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -3271,6 +3282,22 @@ extern "C" int arctopk_decode(const arctopk_plan* p, const void* packed, const i
     if (!p) return ARCTOPK_EINVAL;
     return arctopk_decode_segments(p, 0, p->nseg, packed, slotmap, ws, ef, gerr, out, stream);
 }
+
+namespace arctopk {
+// arctopk_decode whose kernel completes `done` (exchange.cpp)
+int decode_signal(const arctopk_plan* p, const void* packed, const int32_t* slotmap, int32_t ws, int32_t ef,
+                  void* gerr, void* out, void* stream, void* done) {
+    if (!p || !packed || !slotmap || !out || ws < 1 || !done) return ARCTOPK_EINVAL;
+    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF21 && !gerr) return ARCTOPK_EINVAL;
+    const int c0 = p->h_dec_begin[0], c1 = p->h_dec_begin[p->nseg];
+    hipStream_t st = (hipStream_t)stream;
+    if (c1 == c0) return (int)hipEventRecord((hipEvent_t)done, st);
+    if (p->dtype == ARCTOPK_BF16)
+        return launch_decode<bf16_t>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
+    return launch_decode<float>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
+}
+}  // namespace arctopk
 
 extern "C" int arctopk_ef_apply(void* x_, void* E_, int64_t n, int32_t ef, int32_t err_in,
                                 int32_t dtype, void* stream) {

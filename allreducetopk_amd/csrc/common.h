@@ -430,6 +430,7 @@ struct arctopk_plan {
     void* x_bucket;                     //   the bucket,
     void* x_gerr;                       //   the global residual (EF21),
     int x_ef, x_ws;                     //   the EF mode and world size of that call
+    void* x_ev_dec;                     // completed by an inline decode after a collective
 };
 namespace arctopk {
 int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
@@ -437,4 +438,17 @@ int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* 
                 int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream);
 int pack_signal(const arctopk_plan* p, const void* grad, void* err, int32_t ef, const int32_t* rowlist,
                 const int32_t* slotmap, void* packed, void* stream, void* done);
+// arctopk_decode whose kernel completes `done`
+int decode_signal(const arctopk_plan* p, const void* packed, const int32_t* slotmap, int32_t ws, int32_t ef,
+                  void* gerr, void* out, void* stream, void* done);
+// the watchdog stops looking at a plan's events (arctopk_plan_destroy)
+void exchange_forget(arctopk_plan* p);
+// the emulated wire communicator (wire.hip): one all-reduce's local cost on an R-rank ring
+struct WireParams {
+    int32_t ranks;      // ranks of the emulated ring
+    double busbw_gbs;   // bus bandwidth it is paced to
+    double latency_us;  // fixed cost per all-reduce
+    int32_t blocks;     // workgroups (the collective's CU footprint)
+};
+int wire_allreduce(const WireParams& w, void* buf, int64_t bytes, hipStream_t st);
 }

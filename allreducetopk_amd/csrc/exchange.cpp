@@ -21,10 +21,16 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "common.h"
 
@@ -34,10 +40,14 @@ struct Rccl {
     void* handle = nullptr;
     ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+    ncclResult_t (*get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                hipStream_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
+    bool nonblocking() const { return comm_init_rank_config && comm_abort && get_async_error; }
 };
 
 std::mutex g_rccl_mu;
@@ -60,7 +70,11 @@ int rccl_load(const char* path, const Rccl** out) {
     r.handle = h;
     r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
     r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    r.comm_init_rank_config =
+        reinterpret_cast<decltype(r.comm_init_rank_config)>(dlsym(h, "ncclCommInitRankConfig"));
     r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.comm_abort = reinterpret_cast<decltype(r.comm_abort)>(dlsym(h, "ncclCommAbort"));
+    r.get_async_error = reinterpret_cast<decltype(r.get_async_error)>(dlsym(h, "ncclCommGetAsyncError"));
     r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
     r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
     if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce) {
@@ -76,18 +90,175 @@ int rccl_load(const char* path, const Rccl** out) {
 // RCCL status -> ABI status (ARCTOPK_ECOMM + ncclResult_t)
 int rccl_status(ncclResult_t r) { return r == ncclSuccess ? 0 : ARCTOPK_ECOMM + (int)r; }
 
+int64_t now_ms() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// the caller's current device, restored on every return path
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
 }  // namespace
 
 struct arctopk_comm {
-    int kind;  // 0: RCCL, 1: callback
-    int nranks;
-    int rank;
-    int device;
-    ncclComm_t nccl;
-    const Rccl* rccl;
-    arctopk_allreduce_fn fn;
-    void* ctx;
+    enum Kind { RCCL = 0, CALLBACK = 1, WIRE = 2 };
+    int kind = RCCL;
+    int nranks = 1;
+    int rank = 0;
+    int device = -1;
+    ncclComm_t nccl = nullptr;           // RCCL: null once aborted
+    const Rccl* rccl = nullptr;
+    bool nonblocking = false;
+    arctopk_allreduce_fn fn = nullptr;   // callback
+    void* ctx = nullptr;
+    int64_t timeout_ms = 0;              // RCCL: watchdog deadline (0: no watchdog)
+    std::atomic<int> err{0};             // sticky failure status
+    std::mutex mu;                       // RCCL calls of the caller vs the watchdog's abort
+    arctopk::WireParams wire{};          // WIRE
 };
+
+namespace {
+
+// Abort one RCCL communicator (caller holds c->mu), leaving `status` sticky.
+void abort_locked(arctopk_comm* c, int status) {
+    int expected = 0;
+    c->err.compare_exchange_strong(expected, status);
+    if (c->kind == arctopk_comm::RCCL && c->nccl) {
+        if (c->rccl->comm_abort) (void)c->rccl->comm_abort(c->nccl);
+        else (void)c->rccl->comm_destroy(c->nccl);  // (no abort entry point: best effort)
+        c->nccl = nullptr;
+    }
+}
+
+// Watchdog: the library's RCCL communicators created with a timeout, and the completion
+// events of the collectives the exchange step enqueued on them (each keyed by its event,
+// re-armed when the event is recorded again).  Polls every kPollMs.
+class Watchdog {
+  public:
+    static Watchdog& get() {
+        static Watchdog w;
+        return w;
+    }
+    void add(arctopk_comm* c) {
+        std::lock_guard<std::mutex> lk(mu_);
+        comms_.push_back(c);
+        if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    }
+    void remove(arctopk_comm* c) {
+        std::lock_guard<std::mutex> lk(mu_);
+        comms_.erase(std::remove(comms_.begin(), comms_.end(), c), comms_.end());
+        items_.erase(std::remove_if(items_.begin(), items_.end(), [c](const Item& i) { return i.c == c; }),
+                     items_.end());
+    }
+    // the collective of `c` ordered before event `ev` (just recorded) must complete in time
+    void watch(arctopk_comm* c, void* ev) {
+        if (!c || c->kind != arctopk_comm::RCCL || c->timeout_ms <= 0 || !ev) return;
+        const int64_t t = now_ms();
+        std::lock_guard<std::mutex> lk(mu_);
+        for (Item& i : items_)
+            if (i.ev == ev) {
+                i.c = c;
+                i.t = t;
+                return;
+            }
+        items_.push_back(Item{c, ev, t});
+    }
+    void forget_event(void* ev) {
+        if (!ev) return;
+        std::lock_guard<std::mutex> lk(mu_);
+        items_.erase(std::remove_if(items_.begin(), items_.end(), [ev](const Item& i) { return i.ev == ev; }),
+                     items_.end());
+    }
+    // abort every RCCL communicator of the library (a failed peer breaks all of them)
+    void fail_all(int status) {
+        std::lock_guard<std::mutex> lk(mu_);
+        fail_all_locked(status);
+    }
+    ~Watchdog() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        if (th_.joinable()) th_.join();
+    }
+
+  private:
+    struct Item {
+        arctopk_comm* c;
+        void* ev;
+        int64_t t;
+    };
+    static constexpr int kPollMs = 20;
+    void fail_all_locked(int status) {
+        for (arctopk_comm* c : comms_) {
+            std::lock_guard<std::mutex> lc(c->mu);
+            abort_locked(c, status);
+        }
+        items_.clear();
+    }
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        while (!stop_) {
+            cv_.wait_for(lk, std::chrono::milliseconds(kPollMs));
+            if (stop_) break;
+            int fail = 0;
+            for (arctopk_comm* c : comms_) {
+                std::lock_guard<std::mutex> lc(c->mu);
+                if (c->err.load() || !c->nccl) continue;
+                ncclResult_t st = ncclSuccess;
+                if (c->rccl->get_async_error && c->rccl->get_async_error(c->nccl, &st) == ncclSuccess &&
+                    st != ncclSuccess && st != ncclInProgress) {
+                    fail = rccl_status(st);
+                    break;
+                }
+            }
+            const int64_t t = now_ms();
+            for (size_t i = 0; !fail && i < items_.size();) {
+                const hipError_t q = hipEventQuery((hipEvent_t)items_[i].ev);
+                if (q == hipErrorNotReady) {
+                    if (t - items_[i].t > items_[i].c->timeout_ms) fail = ARCTOPK_ETIMEOUT;
+                    ++i;
+                } else {  // complete (or no longer a valid record): nothing to watch
+                    items_[i] = items_.back();
+                    items_.pop_back();
+                }
+            }
+            if (fail) fail_all_locked(fail);
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<arctopk_comm*> comms_;
+    std::vector<Item> items_;
+    std::thread th_;
+    bool stop_ = false;
+};
+
+// a communicator's sticky failure, if any (checked before any work is enqueued on it)
+inline int comm_failed(const arctopk_comm* c) { return c ? c->err.load() : 0; }
+
+}  // namespace
+
+namespace arctopk {
+void exchange_forget(arctopk_plan* p) {
+    if (!p) return;
+    Watchdog::get().forget_event(p->x_ev_packed);
+    Watchdog::get().forget_event(p->x_ev_ar);
+    Watchdog::get().forget_event(p->x_ev_dec);
+}
+}  // namespace arctopk
 
 extern "C" int arctopk_comm_unique_id(const char* rccl_path, void* id_out) {
     if (!id_out) return ARCTOPK_EINVAL;
@@ -101,28 +272,73 @@ extern "C" int arctopk_comm_unique_id(const char* rccl_path, void* id_out) {
     return 0;
 }
 
-extern "C" int arctopk_comm_init_rccl(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
-                                      int32_t device, arctopk_comm** out) {
-    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return ARCTOPK_EINVAL;
+extern "C" int arctopk_comm_init_rccl_timeout(const char* rccl_path, const void* id, int32_t nranks,
+                                              int32_t rank, int32_t device, int64_t timeout_ms,
+                                              arctopk_comm** out) {
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks || timeout_ms < 0) return ARCTOPK_EINVAL;
     *out = nullptr;
     const Rccl* r = nullptr;
     int e = rccl_load(rccl_path, &r);
     if (e) return e;
-    hipError_t he = hipSetDevice(device);
-    if (he != hipSuccess) return (int)he;
+    DeviceGuard dg(device);
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != device) return (int)hipErrorInvalidDevice;
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
     ncclComm_t c = nullptr;
-    e = rccl_status(r->comm_init_rank(&c, nranks, uid, rank));
-    if (e) return e;
+    const bool nb = timeout_ms > 0 && r->nonblocking();
+    if (nb) {
+        // non-blocking creation, polled against the deadline: a rank that never joins makes
+        // this fail with ARCTOPK_ETIMEOUT instead of blocking forever
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t st = r->comm_init_rank_config(&c, nranks, uid, rank, &cfg);
+        const int64_t t0 = now_ms();
+        while (st == ncclInProgress || (st == ncclSuccess && c)) {
+            ncclResult_t a = ncclSuccess;
+            if (r->get_async_error(c, &a) != ncclSuccess) {
+                st = ncclInternalError;
+                break;
+            }
+            if (a != ncclInProgress) {
+                st = a;
+                break;
+            }
+            if (now_ms() - t0 > timeout_ms) {
+                (void)r->comm_abort(c);
+                return ARCTOPK_ETIMEOUT;
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        if (st != ncclSuccess) {
+            if (c) (void)r->comm_abort(c);
+            return rccl_status(st);
+        }
+    } else {
+        e = rccl_status(r->comm_init_rank(&c, nranks, uid, rank));
+        if (e) return e;
+    }
     arctopk_comm* m = new (std::nothrow) arctopk_comm;
     if (!m) {
-        r->comm_destroy(c);
+        (void)(r->comm_abort ? r->comm_abort(c) : r->comm_destroy(c));
         return ARCTOPK_EINVAL;
     }
-    *m = arctopk_comm{0, nranks, rank, device, c, r, nullptr, nullptr};
+    m->kind = arctopk_comm::RCCL;
+    m->nranks = nranks;
+    m->rank = rank;
+    m->device = device;
+    m->nccl = c;
+    m->rccl = r;
+    m->nonblocking = nb;
+    m->timeout_ms = nb ? timeout_ms : 0;
+    if (m->timeout_ms > 0) Watchdog::get().add(m);
     *out = m;
     return 0;
+}
+
+extern "C" int arctopk_comm_init_rccl(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
+                                      int32_t device, arctopk_comm** out) {
+    return arctopk_comm_init_rccl_timeout(rccl_path, id, nranks, rank, device, 0, out);
 }
 
 extern "C" int arctopk_comm_init_callback(arctopk_allreduce_fn fn, void* ctx, int32_t nranks, int32_t rank,
@@ -130,15 +346,50 @@ extern "C" int arctopk_comm_init_callback(arctopk_allreduce_fn fn, void* ctx, in
     if (!fn || !out || nranks < 1 || rank < 0 || rank >= nranks) return ARCTOPK_EINVAL;
     arctopk_comm* m = new (std::nothrow) arctopk_comm;
     if (!m) return ARCTOPK_EINVAL;
-    *m = arctopk_comm{1, nranks, rank, -1, nullptr, nullptr, fn, ctx};
+    m->kind = arctopk_comm::CALLBACK;
+    m->nranks = nranks;
+    m->rank = rank;
+    m->fn = fn;
+    m->ctx = ctx;
     *out = m;
+    return 0;
+}
+
+extern "C" int arctopk_comm_init_wire(int32_t emul_ranks, double busbw_gbs, double latency_us, int32_t blocks,
+                                      int32_t device, arctopk_comm** out) {
+    if (!out || emul_ranks < 1 || !(busbw_gbs > 0.0) || latency_us < 0.0 || blocks < 1 || blocks > 1024)
+        return ARCTOPK_EINVAL;
+    arctopk_comm* m = new (std::nothrow) arctopk_comm;
+    if (!m) return ARCTOPK_EINVAL;
+    m->kind = arctopk_comm::WIRE;
+    m->nranks = 1;  // results of a one-rank all-reduce; the wire's cost of emul_ranks
+    m->device = device;
+    m->wire = arctopk::WireParams{emul_ranks, busbw_gbs, latency_us, blocks};
+    *out = m;
+    return 0;
+}
+
+extern "C" int arctopk_comm_status(const arctopk_comm* c) { return c ? c->err.load() : ARCTOPK_EINVAL; }
+
+extern "C" int arctopk_comm_abort(arctopk_comm* c) {
+    if (!c) return ARCTOPK_EINVAL;
+    std::lock_guard<std::mutex> lc(c->mu);
+    abort_locked(c, ARCTOPK_EABORTED);
     return 0;
 }
 
 extern "C" int arctopk_comm_destroy(arctopk_comm* c) {
     if (!c) return 0;
     int e = 0;
-    if (c->kind == 0 && c->nccl) e = rccl_status(c->rccl->comm_destroy(c->nccl));
+    if (c->kind == arctopk_comm::RCCL) {
+        if (c->timeout_ms > 0) Watchdog::get().remove(c);
+        std::lock_guard<std::mutex> lc(c->mu);
+        if (c->nccl) {
+            const ncclResult_t r = c->rccl->comm_destroy(c->nccl);
+            e = (r == ncclInProgress) ? 0 : rccl_status(r);
+            c->nccl = nullptr;
+        }
+    }
     delete c;
     return e;
 }
@@ -149,10 +400,44 @@ extern "C" int arctopk_comm_size(const arctopk_comm* c) { return c ? c->nranks :
 extern "C" int arctopk_comm_allreduce(arctopk_comm* c, void* buf, int64_t count, int32_t dtype, void* stream) {
     if (!c || (!buf && count) || count < 0) return ARCTOPK_EINVAL;
     if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EDTYPE;
+    if (int f = comm_failed(c)) return f;
     if (count == 0) return 0;
-    if (c->kind == 1) return c->fn(c->ctx, buf, count, dtype, stream);
-    return rccl_status(c->rccl->all_reduce(buf, buf, (size_t)count, dtype == ARCTOPK_BF16 ? ncclBfloat16 : ncclFloat32,
-                                           ncclSum, c->nccl, (hipStream_t)stream));
+    if (c->kind == arctopk_comm::CALLBACK) return c->fn(c->ctx, buf, count, dtype, stream);
+    if (c->kind == arctopk_comm::WIRE)
+        return arctopk::wire_allreduce(c->wire, buf, count * (dtype == ARCTOPK_BF16 ? 2 : 4), (hipStream_t)stream);
+    std::unique_lock<std::mutex> lc(c->mu);
+    if (!c->nccl) return c->err.load() ? c->err.load() : ARCTOPK_EABORTED;
+    ncclResult_t r = c->rccl->all_reduce(buf, buf, (size_t)count, dtype == ARCTOPK_BF16 ? ncclBfloat16 : ncclFloat32,
+                                         ncclSum, c->nccl, (hipStream_t)stream);
+    if (r == ncclInProgress && c->nonblocking) {
+        // non-blocking communicator: the call returns while RCCL still sets up (its first
+        // collective connects the ranks); wait for that on the host, against the deadline
+        const int64_t t0 = now_ms();
+        for (;;) {
+            ncclResult_t a = ncclSuccess;
+            if (c->rccl->get_async_error(c->nccl, &a) != ncclSuccess) a = ncclInternalError;
+            if (a != ncclInProgress) {
+                r = a;
+                break;
+            }
+            if (now_ms() - t0 > c->timeout_ms) {
+                lc.unlock();
+                Watchdog::get().fail_all(ARCTOPK_ETIMEOUT);
+                return ARCTOPK_ETIMEOUT;
+            }
+            lc.unlock();
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            lc.lock();
+            if (!c->nccl) return c->err.load() ? c->err.load() : ARCTOPK_EABORTED;
+        }
+    }
+    if (r != ncclSuccess) {
+        const int st = rccl_status(r);
+        lc.unlock();
+        if (c->timeout_ms > 0) Watchdog::get().fail_all(st);
+        return st;
+    }
+    return 0;
 }
 
 namespace {
@@ -210,6 +495,9 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // deferring with a collective needs the all-reduce stream (the decode waits for its event)
     if (defer && packed_comm && (!ar_stream || ar_stream == stream)) return ARCTOPK_EINVAL;
     if (ride && (ride == p || !ride->x_deferred)) return ARCTOPK_EINVAL;
+    // a communicator that failed (watchdog timeout, RCCL error, abort) takes no more work
+    if (int f = comm_failed(sketch_comm)) return f;
+    if (int f = comm_failed(packed_comm)) return f;
     const int ws = packed_comm ? packed_comm->nranks : 1;
     hipStream_t st = (hipStream_t)stream, as = (hipStream_t)ar_stream;
     // this bucket's own deferred decode, if a caller never finished it (the hook always does)
@@ -248,33 +536,36 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_SELECT, st);
     if (e) return e;
-    const bool signal = defer && packed_comm;
-    if (signal) {
-        // the pack kernel completes x_ev_packed itself (no marker packet on the caller's
-        // stream, where one idles the GPU several us); the all-reduce stream waits for it
+    // with collectives the pack kernel completes x_ev_packed itself (no marker packet on the
+    // caller's stream, where one idles the GPU several us): the all-reduce stream waits for it,
+    // and the watchdog sees the sketch all-reduce before it complete
+    const bool async_ar = defer && packed_comm;
+    if (packed_comm) {
         if ((e = ensure_event(&p->x_ev_packed, 0)) ||
             (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
             return e;
         e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
                                  p->x_ev_packed);
+        if (!e) Watchdog::get().watch(sketch_comm, p->x_ev_packed);
     } else {
         e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_PACK, st);
     if (e) return e;
-    if (signal) {  // the index-free all-reduce of the packed values (:280) on its own stream
+    if (async_ar) {  // the index-free all-reduce of the packed values (:280) on its own stream
         hipError_t he = hipStreamWaitEvent(as, (hipEvent_t)p->x_ev_packed, 0);
         if (he != hipSuccess) return (int)he;
         if ((e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, as))) return e;
         he = hipEventRecord((hipEvent_t)p->x_ev_ar, as);
         if (he != hipSuccess) return (int)he;
+        Watchdog::get().watch(packed_comm, p->x_ev_ar);
     }
     // earlier buckets' deferred decodes the caller wants done now (in its order)
     for (int32_t i = 0; i < nfinish && !e; ++i)
         if (finish[i] && finish[i] != p) e = arctopk_exchange_finish(finish[i], stream, finish_marks ? finish_marks[i] : nullptr);
     if (e) return e;
     if (defer) {
-        p->x_deferred = signal ? 1 : 2;
+        p->x_deferred = async_ar ? 1 : 2;
         p->x_bucket = bucket;
         p->x_gerr = gerr;
         p->x_ef = ef;
@@ -283,7 +574,14 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     }
     if (packed_comm) e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
-    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream);
+    if (e) return e;
+    if (packed_comm) {  // the decode kernel completes x_ev_dec: the inline all-reduce is watched too
+        if ((e = ensure_event(&p->x_ev_dec, hipEventDisableTiming | hipEventReleaseToDevice))) return e;
+        e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream, p->x_ev_dec);
+        if (!e) Watchdog::get().watch(packed_comm, p->x_ev_dec);
+    } else {
+        e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream);
+    }
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
     return e;
 }

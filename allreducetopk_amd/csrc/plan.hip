@@ -385,8 +385,10 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_part) (void)hipFree(p->d_part);
     delete[] p->h_segs;
     delete[] p->h_pack_begin;
+    arctopk::exchange_forget(p);  // before its events go
     if (p->x_ev_packed) (void)hipEventDestroy((hipEvent_t)p->x_ev_packed);
     if (p->x_ev_ar) (void)hipEventDestroy((hipEvent_t)p->x_ev_ar);
+    if (p->x_ev_dec) (void)hipEventDestroy((hipEvent_t)p->x_ev_dec);
     delete[] p->h_large_batches;
     if (p->d_large_batches) (void)hipFree(p->d_large_batches);
     if (p->d_mws) (void)hipFree(p->d_mws);

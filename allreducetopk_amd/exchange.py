@@ -11,16 +11,27 @@ comm_hooks/group_topk_hook_no_reshape.py:58, :280) are issued by the native exch
   into ``torch.distributed.all_reduce`` on the group, so the very same native
   orchestration runs in those tests.
 
-Creating an RCCL communicator is collective over the group's ranks (it blocks until all
+Creating an RCCL communicator is collective over the group's ranks (it waits until all
 of them have called it); the hook creates its communicators at its first compressed call,
 which every rank reaches at the same point of the same backward, or
 ``GroupTopKState.init_exchange_comms()`` does it earlier (register_comm_hook_for_ddp_model
 calls it on every rank).
+
+Failure behaviour (the reference's collectives run on ProcessGroupNCCL under
+``init_process_group(timeout=...)``, cifar10/run_cifar10.py:55-58, whose watchdog turns a hung
+or failed collective into an error): the RCCL communicators are created non-blocking with the
+process group's timeout (a rank that never joins: ``RuntimeError`` after the timeout instead of
+a hang), and the library's watchdog aborts them when a collective stays pending past the
+timeout or RCCL reports an asynchronous error; the hook then raises ``RuntimeError`` at its
+next call (or at ``flush_exchange``).  The callback communicators inherit the torch backend's
+own timeout (gloo raises from ``dist.all_reduce``; the hook re-raises that exception).
+
+``Comm.wire`` is a measurement-only stand-in (world size 1, results unchanged) whose
+all-reduce costs the local GPU what an N-rank ring all-reduce would.
 """
 from __future__ import annotations
 
 import ctypes
-import itertools
 import logging
 import os
 from typing import Dict, Optional
@@ -33,7 +44,33 @@ from allreducetopk_amd import _native as N
 logger = logging.getLogger(__name__)
 
 _DTYPE = {N.F32: torch.float32, N.BF16: torch.bfloat16}
-_serial = itertools.count()
+DEFAULT_TIMEOUT_S = 600.0  # ProcessGroupNCCL's default when a group's own cannot be read
+
+
+def group_timeout_s(group) -> float:
+    """The timeout of `group` (init_process_group / new_group(timeout=...)); ARCTOPK_COMM_TIMEOUT_S
+    overrides it."""
+    env = os.environ.get("ARCTOPK_COMM_TIMEOUT_S")
+    if env:
+        return float(env)
+    for dev in ("cuda", "cpu"):
+        try:
+            return float(group._get_backend(torch.device(dev)).options._timeout.total_seconds())
+        except Exception:  # noqa: BLE001 -- backend without options / not registered for dev
+            continue
+    t = getattr(dist.distributed_c10d, "default_pg_nccl_timeout", None) or \
+        getattr(dist.distributed_c10d, "default_pg_timeout", None)
+    return float(t.total_seconds()) if t is not None else DEFAULT_TIMEOUT_S
+
+
+def _store_key(store, tag: str, ranks) -> str:
+    """A key every rank of the group derives alike for its n-th communicator of `tag`: each rank
+    counts itself in at the store, and the creation of generation g completes only once all
+    ranks have joined it, so every count of g precedes every count of g + 1 (a
+    process-local counter diverges when processes create different numbers of communicators)."""
+    base = f"arctopk_comm/{tag}/{'-'.join(map(str, ranks))}"
+    gen = (int(store.add(base + "/count", 1)) - 1) // len(ranks)
+    return f"{base}/{gen}"
 
 
 def rccl_path() -> str:
@@ -65,14 +102,15 @@ class Comm:
 
     # ---- RCCL ---------------------------------------------------------------------
     @classmethod
-    def rccl(cls, group, device: torch.device, tag: str) -> "Comm":
-        """An RCCL communicator over `group`'s ranks (collective over them)."""
+    def rccl(cls, group, device: torch.device, tag: str, timeout_s: Optional[float] = None) -> "Comm":
+        """An RCCL communicator over `group`'s ranks (collective over them), created non-blocking
+        and watched against `timeout_s` (default: the group's timeout)."""
         L = N.lib()
         path = rccl_path().encode()
         ranks = dist.get_process_group_ranks(group)
         me = dist.get_rank(group)
-        key = f"arctopk_comm/{tag}/{'-'.join(map(str, ranks))}/{next(_serial)}"
         store = dist.distributed_c10d._get_default_store()
+        key = _store_key(store, tag, ranks)
         if me == 0:
             uid = ctypes.create_string_buffer(128)
             N.check(L.arctopk_comm_unique_id(path, uid), "arctopk_comm_unique_id")
@@ -80,10 +118,42 @@ class Comm:
             raw = uid.raw
         else:
             raw = bytes(store.get(key))
+        timeout_s = group_timeout_s(group) if timeout_s is None else float(timeout_s)
         h = ctypes.c_void_p()
-        N.check(L.arctopk_comm_init_rccl(path, raw, len(ranks), me, device.index or 0, ctypes.byref(h)),
-                f"arctopk_comm_init_rccl({tag}, {len(ranks)} ranks)")
-        return cls(h.value, group, "rccl")
+        N.check(L.arctopk_comm_init_rccl_timeout(path, raw, len(ranks), me, device.index or 0,
+                                                 max(1, int(timeout_s * 1000)), ctypes.byref(h)),
+                f"arctopk_comm_init_rccl({tag}, {len(ranks)} ranks, timeout {timeout_s:g} s)")
+        c = cls(h.value, group, "rccl")
+        c.timeout_s = timeout_s
+        return c
+
+    # ---- emulated wire (measurement only) ---------------------------------------------
+    @classmethod
+    def wire(cls, device: torch.device, ranks: int = 8, busbw_gbs: float = 350.0,
+             latency_us: float = 15.0, blocks: int = 32) -> "Comm":
+        """World size 1 (buffers unchanged) at the local cost of a `ranks`-rank ring all-reduce
+        paced to `busbw_gbs` (arctopk_comm_init_wire)."""
+        h = ctypes.c_void_p()
+        N.check(N.lib().arctopk_comm_init_wire(int(ranks), float(busbw_gbs), float(latency_us), int(blocks),
+                                               torch.device(device).index or 0, ctypes.byref(h)),
+                "arctopk_comm_init_wire")
+        c = cls(h.value, None, "wire")
+        c.wire_params = dict(ranks=int(ranks), busbw_gbs=float(busbw_gbs), latency_us=float(latency_us),
+                             blocks=int(blocks))
+        return c
+
+    def status(self) -> int:
+        """0, or the communicator's sticky failure (watchdog timeout, RCCL error, abort)."""
+        return int(N.lib().arctopk_comm_status(self.handle)) if self.handle else 0
+
+    def raise_if_failed(self, what: str = "ARC-TopK exchange") -> None:
+        st = self.status()
+        if st:
+            N.check(st, f"{what} ({self.kind} communicator over {self.size} ranks)")
+
+    def abort(self) -> None:
+        if self.handle:
+            N.lib().arctopk_comm_abort(self.handle)
 
     # ---- callback (any torch.distributed backend) ----------------------------------
     @classmethod
@@ -146,11 +216,17 @@ class Comm:
             self.handle = None
 
 
-def make_comms(group, device: torch.device, mode: str):
+def make_comms(group, device: torch.device, mode: str, wire: Optional[dict] = None):
     """(sketch communicator, packed-values communicator) over `group`.
 
     mode "separate": two communicators, so a bucket's sketch all-reduce never queues behind
-    the previous bucket's packed all-reduce; "shared": one."""
+    the previous bucket's packed all-reduce; "shared": one.
+    `wire`: emulated-wire parameters (Comm.wire) instead of real communicators."""
+    if wire is not None:
+        packed = Comm.wire(device, **wire)
+        sketch = Comm.wire(device, **wire) if mode == "separate" else packed
+        logger.info("ARC-TopK exchange: emulated wire %s (%s sketch)", packed.wire_params, mode)
+        return sketch, packed
     backend = dist.get_backend(group)
     if "nccl" in str(backend):
         packed = Comm.rccl(group, device, "packed")

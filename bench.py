@@ -226,6 +226,7 @@ def main():
                             use_error_feedback=args.ef, seed=1234)
         st.host_staged = args.host_staged
         st.force_exchange = args.force_exchange
+        st.defer_decode = True  # step() waits every Future after the last bucket, as DDP's finalize
         if world > 1 or args.force_exchange:
             st.init_exchange_comms(dev)  # collective, before any step (as the registry does)
         hook = group_topk_hook

@@ -42,6 +42,10 @@ extern "C" {
 #define ARCTOPK_EDTYPE 1003     /* unsupported element type */
 #define ARCTOPK_EEMPTY 1004     /* empty tensor: torch.topk(k=1) on 0 elements raises */
 #define ARCTOPK_ENOCOMM 1005    /* the RCCL library could not be loaded / lacks entry points */
+#define ARCTOPK_ETIMEOUT 1006   /* a communicator's collective (or its creation) outlived the
+                                   process group's timeout; the communicator was aborted */
+#define ARCTOPK_EABORTED 1007   /* the communicator was aborted (by arctopk_comm_abort, or after
+                                   an error of another communicator of this process) */
 #define ARCTOPK_ECOMM 1100      /* RCCL error: ARCTOPK_ECOMM + ncclResult_t */
 
 /* error-feedback modes (ref GroupTopKState.use_error_feedback, :149, :224-250) */
@@ -187,8 +191,36 @@ typedef int (*arctopk_allreduce_fn)(void* ctx, void* buf, int64_t count, int32_t
 int arctopk_comm_unique_id(const char* rccl_path, void* id_out);
 int arctopk_comm_init_rccl(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
                            int32_t device, arctopk_comm** out);
+/*
+ * Failure detection (the reference's collectives run on ProcessGroupNCCL, whose watchdog turns
+ * a hung or failed collective into an error after the group's timeout: cifar10/run_cifar10.py:
+ * 55-58).  arctopk_comm_init_rccl_timeout creates the communicator non-blocking
+ * (ncclCommInitRankConfig, blocking = 0) and gives up after `timeout_ms` (aborting it:
+ * ARCTOPK_ETIMEOUT) when a rank never joins.  With timeout_ms > 0 a watchdog thread of the
+ * library then polls ncclCommGetAsyncError and the completion of every collective the
+ * exchange step issued on the communicator; an asynchronous RCCL error, or a collective still
+ * pending `timeout_ms` after it was enqueued, aborts EVERY RCCL communicator of the library
+ * (the GPU kernels of an aborted communicator exit) and leaves the error sticky:
+ * arctopk_comm_status returns it, and every later exchange step on the communicator returns
+ * it instead of enqueueing work.  arctopk_comm_init_rccl = timeout 0: blocking creation, no
+ * watchdog.  The device current on the calling thread is left unchanged.
+ */
+int arctopk_comm_init_rccl_timeout(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
+                                   int32_t device, int64_t timeout_ms, arctopk_comm** out);
+int arctopk_comm_status(const arctopk_comm* comm);
+int arctopk_comm_abort(arctopk_comm* comm);
 int arctopk_comm_init_callback(arctopk_allreduce_fn fn, void* ctx, int32_t nranks, int32_t rank,
                                arctopk_comm** out);
+/*
+ * Measurement only: an "emulated wire" communicator of world size 1 (results are those of a
+ * one-rank all-reduce: the buffer is left unchanged) whose all-reduce costs what an
+ * `emul_ranks`-rank ring all-reduce costs the local GPU: a kernel of `blocks` workgroups
+ * (RCCL's CU footprint) that reads and rewrites 2 (R - 1) / R of the buffer's bytes in HBM,
+ * paced to take at least latency_us + 2 (R - 1) / R * bytes / busbw_gbs.  Lets one GPU measure
+ * the exchange step beside an N-rank wire.
+ */
+int arctopk_comm_init_wire(int32_t emul_ranks, double busbw_gbs, double latency_us, int32_t blocks,
+                           int32_t device, arctopk_comm** out);
 int arctopk_comm_destroy(arctopk_comm* comm);
 int arctopk_comm_size(const arctopk_comm* comm);
 /* in-place SUM all-reduce of `count` elements (ARCTOPK_F32 / ARCTOPK_BF16), stream-ordered */

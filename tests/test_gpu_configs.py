@@ -64,6 +64,7 @@ class ArcRun:
         self.st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                                  use_error_feedback=ef, seed=seed)
         self.st.force_exchange = force_exchange
+        self.st.defer_decode = True  # every bucket's Future is waited after the last one, as DDP does
         self.ost = A.OracleState(r=4, compress_ratio=0.2, start_compress_iter=0,
                                  use_error_feedback=ef, seed=seed)
         self.E, self.gE = {}, {}

@@ -128,7 +128,7 @@ def test_topk_select_degenerate_large(case):
 
 
 @pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
-@pytest.mark.parametrize("source", ["torch", "hash"])
+@pytest.mark.parametrize("source", ["torch", "host", "hash"])
 def test_randk_hook_vs_oracle(ef, source):
     st = sparse_hook.SparseState(None, compress_ratio=0.2, start_compress_iter=0,
                                  sparse_type="tensor", random=True, use_error_feedback=ef,
@@ -148,6 +148,9 @@ def test_randk_hook_vs_oracle(ef, source):
         if source == "torch":  # the device draw the hook made (deterministic per seed)
             torch.manual_seed(seed)
             idx = [torch.randperm(n, device=DEV)[:k].cpu() for n, k in zip(numels, ks)]
+        elif source == "host":  # the reference's CPU draw
+            torch.manual_seed(seed)
+            idx = [torch.randperm(n)[:k] for n, k in zip(numels, ks)]
         else:
             kof = [sum(ks[:i]) for i in range(len(ks))]
             buf = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
@@ -177,6 +180,32 @@ def test_topk_golden_on_gpu(name):
                          sparse_type="tensor", random=False, use_error_feedback=m["ef"],
                          random_seed=m["seed"])
     st.error_decay = m.get("error_decay", 1.0)  # EF21 residual scaling (set by hand, as a driver would)
+    shapes = [tuple(s) for s in m["shapes"]]
+    for it in range(m["iters"]):
+        out = mod.sparse_hook_sync(st, SyntheticBucket(g.t(0, it, "G").to(DEV), shapes)).wait()
+        torch.cuda.synchronize()
+        assert_bitwise(out, g.t(0, it, "out"), f"{name} it{it} out")
+        if g.has(0, it, "E"):
+            assert_bitwise(st.error_dict[0], g.t(0, it, "E"), f"{name} it{it} E")
+        if g.has(0, it, "gE"):
+            assert_bitwise(st.global_error_dict[0], g.t(0, it, "gE"), f"{name} it{it} gE")
+        assert st.comm_bits_this_round == int(g.np(0, it, "bits"))
+
+
+@pytest.mark.parametrize("name", [n for n in case_names("randk_") if n.endswith("ws1")])
+def test_randk_golden_on_gpu(name):
+    """The reference's RandK fixtures (its CPU torch.randperm draws after the global reseed,
+    sparse_hook_c4.py:20, :269-274) through the HIP hook with index_source="host": outputs,
+    residuals and bits bit for bit."""
+    g = Golden(name)
+    m = g.meta
+    assert m["random"]
+    mod = sparse_hook_c4 if m["hook"] == "sparse_c4" else sparse_hook
+    st = mod.SparseState(None, compress_ratio=m["ratio"], start_compress_iter=m["start"],
+                         sparse_type="tensor", random=True, use_error_feedback=m["ef"],
+                         random_seed=m["seed"])
+    st.index_source = "host"
+    st.error_decay = m.get("error_decay", 1.0)
     shapes = [tuple(s) for s in m["shapes"]]
     for it in range(m["iters"]):
         out = mod.sparse_hook_sync(st, SyntheticBucket(g.t(0, it, "G").to(DEV), shapes)).wait()
