@@ -922,8 +922,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         comms = world_size > 1 or state.force_exchange or state.emulate_wire is not None
         sk = pk = None
         if comms:
-            sk, pk = state._exchange_comms(group, dev)
-            state._raise_if_comm_failed()
+            sk, pk = state._exchange_comms(group, dev)  # (a failed communicator: the step returns its status)
             if plan.comm_registered is not pk:
                 sk.register(plan.sketch)
                 pk.register(plan.packed)

@@ -1490,7 +1490,10 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
         ws->take_eq[t][r] = (uint32_t)take;
         ws->sel_before[t][r] = sel_before;
     }
-    if (tid == 0) ws->st[t] = s;  // the write pass reads the threshold (prefix)
+    if (tid == 0) {
+        ws->st[t] = s;  // the write pass reads the threshold (prefix)
+        arc_win_update(ws, it.win, s.prefix);  // the next call's first-digit window
+    }
 }
 
 // The refine of a batch's large segments and, in the same launch, the single-block selects
@@ -1700,6 +1703,7 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     }
     DIAG_STAMP(g_st_refine, 3);
     const uint32_t T = s.prefix;
+    if (r == 0 && tid == 0) arc_win_update(ws, it.win, T);  // the next call's first-digit window
     // candidates before this span (> T, == T) and this span's == T
     const uint32_t cb = roff[r], ce = r + qn < nr ? roff[r + qn] : nc32;
     uint32_t gb = 0, eb = 0, eo = 0;
@@ -1789,6 +1793,7 @@ template <typename T>
 struct DecodeRide {
     const SegDev* segs;
     const Chunk* chunks;
+    const int32_t* dfirst;  // the chunk table (mode 3)
     const T* packed;
     const int32_t* slotmap;
     T* gE;
@@ -1798,6 +1803,7 @@ struct DecodeRide {
 };
 template <typename T, int EF>
 __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                             const int32_t* __restrict__ dfc,
                                              const T* __restrict__ packed,
                                              const int32_t* __restrict__ slotmap, Scale sc,
                                              T* __restrict__ gE, T* __restrict__ out,
@@ -1818,7 +1824,7 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     const int rb = (int)blockIdx.x - ((int)gridDim.x - job.n - dr.n);
     if (rb >= 0) {  // the ride's decode chunks
-        decode_chunk<T, EF>(dr.segs, dr.chunks[rb], dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
+        decode_chunk<T, EF>(dr.segs, dr.chunks[rb], dr.dfirst + rb, dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
                             reinterpret_cast<float*>(dyn));
         return;
     }
@@ -1866,6 +1872,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
     const int bx = (int)blockIdx.x - kg.first[t];
     const uint32_t nblk = (uint32_t)(kg.first[t + 1] - kg.first[t]);
     const SegDev s = segs[ids[first + t]];
+    const ArcWin w = arc_win(ws, first + t < kMWin ? first + t : -1);  // (plan: MItem::win)
 #ifdef ARCTOPK_STAMPS
     if (threadIdx.x == 0) g_st_keys[blockIdx.x * 8 + 4] = (unsigned long long)t;
 #endif
@@ -1890,7 +1897,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
                     const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
                     kout[rr] = key;
 #if ARCTOPK_DIAG_KEYS < 2
-                    atomicAdd(&h[key >> kArcShift], 1u);
+                    atomicAdd(&h[arc_digit(key, w)], 1u);
 #endif
                 }
             }
@@ -1906,7 +1913,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
             if (rr < s.n) {
                 const uint32_t key = energy_key(e[u]);
                 kout[rr] = key;
-                atomicAdd(&h[key >> kArcShift], 1u);
+                atomicAdd(&h[arc_digit(key, w)], 1u);
             }
         }
     }
@@ -1957,7 +1964,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
         DIAG_STAMP(g_st_keys, 3);
         return;
     }
-    ms_arc_first_digit<KT>(ws, t, s.k_rows, h);
+    ms_arc_first_digit<KT>(ws, t, s.k_rows, w, h);
     DIAG_STAMP(g_st_keys, 3);
 }
 
@@ -1999,6 +2006,10 @@ constexpr bool kPackFullQuads = ARCTOPK_PACK_FULL_QUADS != 0;
 #define ARCTOPK_PACK_PAIRS 1  // tuning switch (A/B builds): 0 = scalar gathers for even short rows
 #endif
 constexpr bool kPackPairs = ARCTOPK_PACK_PAIRS != 0;
+#ifndef ARCTOPK_PACK_QUADS
+#define ARCTOPK_PACK_QUADS 1  // tuning switch (A/B builds): 0 = 8-B pairs for even short rows
+#endif
+constexpr bool kPackQuads = ARCTOPK_PACK_QUADS != 0;
 
 // Pack of a row range of an m in {1, 2} fp32 segment (Chunk mode 1): lane per 16-B quad of
 // the segment (4 / 2 rows), slot map read alongside; selected rows go to packed[slot * m],
@@ -2087,7 +2098,7 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                                               const T* __restrict__ G, T* __restrict__ E,
                                               const int32_t* __restrict__ rowlist,
                                               const int32_t* __restrict__ slotmap,
-                                              T* __restrict__ packed) {
+                                              T* __restrict__ packed, int32_t* __restrict__ dfirst) {
     const Chunk ch = chunks[blockIdx.x];
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
@@ -2141,10 +2152,108 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
     if (m >= 4 && m < 256) {  // small-m: row list staged in LDS, 32-bit mulhi division
         __shared__ int32_t rs[kSmallTileRows];
         const int nr = (int)ch.nrows;
+        const int32_t before = (threadIdx.x == 0 && ch.row0 > 0) ? rl[-1] : -1;  // the previous slot's row
         for (int r = threadIdx.x; r < nr; r += 256) rs[r] = rl[r];
         __syncthreads();
+        if (s.dchunk_rows > 0) {
+            // the decode's chunk table (mode 3): chunk l of the segment starts at row l * CR, and
+            // its first selected row is slot j for every boundary l * CR in (row(j - 1), row(j)];
+            // boundaries past the last selected row get k (the segment's end, then the next
+            // segment's first chunk: the same bucket-wide value the next segment would write)
+            const int64_t CR = s.dchunk_rows;
+            const int64_t nch = (s.n + CR - 1) / CR;
+            for (int jl = threadIdx.x; jl < nr; jl += 256) {
+                const int64_t j = ch.row0 + jl;
+                const int64_t rj = rs[jl];
+                const int64_t rp = jl > 0 ? rs[jl - 1] : before;
+                for (int64_t l = (rp + CR) / CR; l <= rj / CR; ++l)
+                    dfirst[s.dchunk0 + l] = (int32_t)(s.sel_off + j);
+                if (j == s.k_rows - 1)
+                    for (int64_t l = (rj + CR) / CR; l <= nch; ++l)
+                        dfirst[s.dchunk0 + l] = (int32_t)(s.sel_off + s.k_rows);
+            }
+        }
         const uint32_t cnt = (uint32_t)(nr * m);
         const int64_t dbase = s.packed_off + ch.row0 * m;
+        if constexpr (sizeof(T) == 4 && kPackQuads) {
+            if ((m & 1) == 0 && (s.offset & 1) == 0) {
+                // even m (3x3 / 5x5 conv rows, 72 / 200 B; rows start 8-B aligned): each row is
+                // read -- and EF14 / EF21 rewritten -- as the 16-B quads of the bucket that
+                // cover it (their first / last may hold half a neighbour row: loaded, never
+                // stored), so a 72-B row costs 5 quad loads and 5 stores instead of 9 + 9 of
+                // 8 B (the counter profile had this pack stalled at instruction issue); the
+                // packed values leave as 8-B pairs (a row's packed position is 8-B aligned).
+                const int nq = (m + 5) >> 2;  // quads a row spans at most
+                const uint32_t units = (uint32_t)(nr * nq);
+                const uint32_t qmagic = (uint32_t)(((1ull << 32) + (uint64_t)nq - 1) / (uint64_t)nq);
+                const int64_t seg_end = s.offset + s.n * m;
+                const float* Gf = reinterpret_cast<const float*>(G);
+                float* Ef = reinterpret_cast<float*>(E);
+                float* df = reinterpret_cast<float*>(dst);
+                constexpr int Q = 8;
+                for (uint32_t u0 = threadIdx.x; u0 < units; u0 += 256 * Q) {
+                    int64_t qa[Q];
+                    int lo[Q], hi[Q], jr[Q];  // in-row elements [lo, hi) of the quad; row of the chunk
+                    float4 va[Q], vb[Q];
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        const uint32_t un = min(u0 + u * 256, units - 1);
+                        const uint32_t j = div32(un, qmagic);
+                        const int q = (int)(un - j * (uint32_t)nq);
+                        const int64_t s0 = s.offset + (int64_t)rs[j] * m;
+                        qa[u] = (s0 & ~(int64_t)3) + 4 * q;
+                        lo[u] = (int)max<int64_t>(0, s0 - qa[u]);
+                        hi[u] = (int)min<int64_t>(4, s0 + m - qa[u]);
+                        jr[u] = (int)j;
+                    }
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        // whole quad when it lies inside the segment, else only the in-row half
+                        const bool whole = qa[u] + 4 <= seg_end && qa[u] >= s.offset;
+                        const int64_t h = qa[u] + (lo[u] ? 2 : 0);
+                        if constexpr (EF != ARCTOPK_EF14) {
+                            if (whole) va[u] = *reinterpret_cast<const float4*>(Gf + qa[u]);
+                            else if (hi[u] > lo[u]) {
+                                const float2 t2 = *reinterpret_cast<const float2*>(Gf + h);
+                                va[u] = lo[u] ? make_float4(0.f, 0.f, t2.x, t2.y) : make_float4(t2.x, t2.y, 0.f, 0.f);
+                            }
+                        }
+                        if constexpr (EF != ARCTOPK_EF_NONE) {
+                            if (whole) vb[u] = *reinterpret_cast<const float4*>(Ef + qa[u]);
+                            else if (hi[u] > lo[u]) {
+                                const float2 t2 = *reinterpret_cast<const float2*>(Ef + h);
+                                vb[u] = lo[u] ? make_float4(0.f, 0.f, t2.x, t2.y) : make_float4(t2.x, t2.y, 0.f, 0.f);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < Q; ++u) {
+                        if (u0 + u * 256 >= units || hi[u] <= lo[u]) continue;  // (a quad past the row)
+                        float4 v, en;
+                        if constexpr (EF == ARCTOPK_EF_NONE) {
+                            v = va[u];
+                        } else if constexpr (EF == ARCTOPK_EF14) {
+                            v = vb[u];
+                            en = make_float4(0.f, 0.f, 0.f, 0.f);
+                        } else {
+                            v = make_float4(va[u].x - vb[u].x, va[u].y - vb[u].y, va[u].z - vb[u].z, va[u].w - vb[u].w);
+                            en = add4(vb[u], v);
+                        }
+                        if constexpr (EF != ARCTOPK_EF_NONE) {
+                            if (lo[u] == 0 && hi[u] == 4) *reinterpret_cast<float4*>(Ef + qa[u]) = en;
+                            else if (lo[u]) *reinterpret_cast<float2*>(Ef + qa[u] + 2) = make_float2(en.z, en.w);
+                            else *reinterpret_cast<float2*>(Ef + qa[u]) = make_float2(en.x, en.y);
+                        }
+                        // packed position of the quad's first in-row element
+                        const int64_t s0 = s.offset + (int64_t)rs[jr[u]] * m;
+                        const int64_t pp = (int64_t)jr[u] * m + (qa[u] + lo[u] - s0);
+                        if (lo[u] == 0) *reinterpret_cast<float2*>(df + pp) = make_float2(v.x, v.y);
+                        if (hi[u] == 4) *reinterpret_cast<float2*>(df + pp + (lo[u] ? 0 : 2)) = make_float2(v.z, v.w);
+                    }
+                }
+                return;
+            }
+        }
         if constexpr (sizeof(T) == 4 && kPackPairs) {
             if ((m & 1) == 0 && (s.offset & 1) == 0) {
                 // even m (3x3 / 5x5 conv rows, 72 / 200 B): 8-B units.  Every unit lies in one
@@ -2338,6 +2447,7 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
 // deferred decode rides in (k_select_small_dec).  dlds: the small-m chunk tile (dynamic LDS).
 template <typename T, int EF>
 __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                             const int32_t* __restrict__ dfc,
                                              const T* __restrict__ packed,
                                              const int32_t* __restrict__ slotmap, Scale sc,
                                              T* __restrict__ gE, T* __restrict__ out,
@@ -2350,6 +2460,94 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
     const int64_t base = s.offset + ch.row0 * m;
     const int32_t* sm = slotmap + s.row_off + ch.row0;
     const T* pk = packed + s.packed_off;
+    if (ch.mode == 3) {
+        // Short rows (4 <= m < 256), chunk of nr rows starting on a quad boundary of the bucket.
+        // The pack wrote the bucket-wide index of the chunk's first selected row (dfc[0]) and
+        // of the next chunk's (dfc[1]): the chunk's packed rows are one contiguous range, so
+        // the slot map, that range and (EF21) gE are all loaded in ONE round trip, staged in
+        // LDS (map: row -> slot within the range), and the chunk is written as 16-B quads.
+        static_assert(ARCTOPK_SHORT3_CHUNK <= 4096, "register staging sized for 4096-element chunks");
+        constexpr int UR = 4, UP = 16, UG = 4;  // rows, packed values, quads per thread
+        const int nr = (int)ch.nrows, cnt = nr * m;
+        const int32_t g0 = dfc[0], g1 = dfc[1];
+        const int32_t f0 = g0 - (int32_t)s.sel_off;
+        const int nsel = max(0, min(g1 - g0, nr));
+        const int np = nsel * m;
+        const T* pkc = pk + (int64_t)f0 * m;
+        int32_t* lmap = reinterpret_cast<int32_t*>(dlds);
+        float* lpk = dlds + nr;
+        int32_t sv[UR];
+        float pv[UP];
+        [[maybe_unused]] float4 gq[UG];
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int r = (int)threadIdx.x + u * 256;
+            sv[u] = r < nr ? sm[r] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+            const int p = (int)threadIdx.x + u * 256;
+            pv[u] = p < np ? to_f(pkc[p]) : 0.f;
+        }
+        if constexpr (EF == ARCTOPK_EF21) {
+#pragma unroll
+            for (int u = 0; u < UG; ++u) {
+                const int e = 4 * ((int)threadIdx.x + u * 256);
+                if (e + 4 <= cnt) {
+                    gq[u] = ldq<T, kNtDecode>(gE + base + e, 0);
+                } else {
+                    float g4[4] = {0.f, 0.f, 0.f, 0.f};
+                    for (int j = 0; j < 4 && e + j < cnt; ++j) g4[j] = ld1<T>(gE + base + e + j);
+                    gq[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int r = (int)threadIdx.x + u * 256;
+            if (r < nr) lmap[r] = sv[u] >= 0 ? sv[u] - f0 : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+            const int p = (int)threadIdx.x + u * 256;
+            if (p < np) lpk[p] = pv[u];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < UG; ++u) {
+            const int e = 4 * ((int)threadIdx.x + u * 256);
+            if (e >= cnt) break;
+            float o[4];
+            bool sel[4], any = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ej = min(e + j, cnt - 1);
+                const uint32_t r = div32((uint32_t)ej, s.magic32);
+                const int c = ej - (int)r * m;
+                const int sl = lmap[r];
+                sel[j] = sl >= 0 && sl < nsel && e + j < cnt;
+                any = any || sel[j];
+                float v = sel[j] ? mean1(lpk[sl * m + c]) : 0.f;
+                if constexpr (EF == ARCTOPK_EF21) {
+                    const float g = j == 0 ? gq[u].x : j == 1 ? gq[u].y : j == 2 ? gq[u].z : gq[u].w;
+                    v = sel[j] ? rnd<T>(g + v) : g + 0.f;
+                }
+                o[j] = v;
+            }
+            if (e + 4 <= cnt) {
+                stq<T, kNtDecode>(out + base + e, 0, make_float4(o[0], o[1], o[2], o[3]));
+                if constexpr (EF == ARCTOPK_EF21)
+                    if (any) stq<T, false>(gE + base + e, 0, make_float4(o[0], o[1], o[2], o[3]));
+            } else {
+                for (int j = 0; j < 4 && e + j < cnt; ++j) {
+                    st1<T>(out + base + e + j, o[j]);
+                    if constexpr (EF == ARCTOPK_EF21)
+                        if (sel[j]) st1<T>(gE + base + e + j, o[j]);
+                }
+            }
+        }
+        return;
+    }
     if constexpr (sizeof(T) == 4) {
         if (ch.mode == 1) {  // m in {1, 2}, 16-B aligned: lane per output quad
             const int nq = (int)((ch.nrows * m + 3) >> 2);
@@ -2673,11 +2871,12 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
 template <typename T, int EF>
 __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                                                 const Chunk* __restrict__ chunks,
+                                                const int32_t* __restrict__ dfirst,
                                                 const T* __restrict__ packed,
                                                 const int32_t* __restrict__ slotmap, Scale sc,
                                                 T* __restrict__ gE, T* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float dlds[];  // small-m chunk tile
-    decode_chunk<T, EF>(segs, chunks[blockIdx.x], packed, slotmap, sc, gE, out, dlds);
+    decode_chunk<T, EF>(segs, chunks[blockIdx.x], dfirst + blockIdx.x, packed, slotmap, sc, gE, out, dlds);
 }
 
 // A deferred decode (an earlier bucket's, arctopk_exchange_step's `ride`) riding in the
@@ -2697,7 +2896,8 @@ __global__ void __launch_bounds__(kST) k_select_small_dec(const SegDev* __restri
         select_small_seg<T, kST>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, dyn);
         return;
     }
-    decode_chunk<T, EF>(dr.segs, dr.chunks[blockIdx.x - nsel], dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
+    decode_chunk<T, EF>(dr.segs, dr.chunks[blockIdx.x - nsel], dr.dfirst + (blockIdx.x - nsel), dr.packed,
+                        dr.slotmap, dr.sc, dr.gE, dr.out,
                         reinterpret_cast<float*>(dyn));
 }
 
@@ -2857,6 +3057,7 @@ DecodeRide<T> make_ride(const RideArgs* ra) {
     const arctopk_plan* rp = ra->rp;
     dr.segs = rp->d_segs;
     dr.chunks = rp->d_dec;
+    dr.dfirst = rp->d_dfirst;
     dr.packed = static_cast<const T*>(rp->b_packed);
     dr.slotmap = rp->b_slotmap;
     dr.gE = static_cast<T*>(ra->gerr);
@@ -3015,13 +3216,14 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
 // marker packet on this stream (a marker between two kernels idles the GPU ~12 us)
 template <typename T, int EF>
 void pack_launch(dim3 grid, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
-                 const T* grad, T* err, const int32_t* rowlist, const int32_t* slotmap, T* packed) {
+                 const T* grad, T* err, const int32_t* rowlist, const int32_t* slotmap, T* packed,
+                 int32_t* dfirst) {
     if (done)
         hipExtLaunchKernelGGL((k_pack<T, EF>), grid, dim3(256), 0, st, nullptr, done, 0, segs, ch, grad, err,
-                              rowlist, slotmap, packed);
+                              rowlist, slotmap, packed, dfirst);
     else
         hipLaunchKernelGGL((k_pack<T, EF>), grid, dim3(256), 0, st, segs, ch, grad, err, rowlist, slotmap,
-                           packed);
+                           packed, dfirst);
 }
 
 template <typename T>
@@ -3034,11 +3236,11 @@ int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* 
     dim3 grid(c1 - c0);
     const Chunk* ch = p->d_pack + c0;
     if (ef == ARCTOPK_EF_NONE)
-        pack_launch<T, ARCTOPK_EF_NONE>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
+        pack_launch<T, ARCTOPK_EF_NONE>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dfirst);
     else if (ef == ARCTOPK_EF14)
-        pack_launch<T, ARCTOPK_EF14>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
+        pack_launch<T, ARCTOPK_EF14>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dfirst);
     else if (ef == ARCTOPK_EF21)
-        pack_launch<T, ARCTOPK_EF21>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed);
+        pack_launch<T, ARCTOPK_EF21>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dfirst);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -3047,12 +3249,13 @@ int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* 
 // `done` as in pack_launch (the decode after an inline all-reduce, watched by exchange.cpp)
 template <typename T, int EF>
 void decode_launch(dim3 grid, size_t lds, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
-                   const T* packed, const int32_t* slotmap, Scale sc, T* gerr, T* out) {
+                   const int32_t* dfirst, const T* packed, const int32_t* slotmap, Scale sc, T* gerr, T* out) {
     if (done)
-        hipExtLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, nullptr, done, 0, segs, ch, packed,
-                              slotmap, sc, gerr, out);
+        hipExtLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, nullptr, done, 0, segs, ch, dfirst,
+                              packed, slotmap, sc, gerr, out);
     else
-        hipLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, segs, ch, packed, slotmap, sc, gerr, out);
+        hipLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, segs, ch, dfirst, packed, slotmap, sc,
+                           gerr, out);
 }
 
 template <typename T>
@@ -3066,9 +3269,11 @@ int launch_decode(const arctopk_plan* p, int c0, int c1, const void* packed_, co
     const Scale sc = make_scale(ws);
     const size_t lds = (size_t)p->dec_lds_bytes;
     if (ef == ARCTOPK_EF21)
-        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, p->d_dfirst + c0, packed, slotmap, sc, gerr,
+                                       out);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, packed, slotmap, sc, gerr, out);
+        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, p->d_dfirst + c0, packed, slotmap, sc,
+                                          gerr, out);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -3126,6 +3331,7 @@ int launch_select_ride(const arctopk_plan* p, const void* sketch_, int32_t ws, i
     DecodeRide<T> dr;
     dr.segs = rp->d_segs;
     dr.chunks = rp->d_dec;
+    dr.dfirst = rp->d_dfirst;
     dr.packed = static_cast<const T*>(rp->b_packed);
     dr.slotmap = rp->b_slotmap;
     dr.gE = static_cast<T*>(rp_gerr);

@@ -72,6 +72,12 @@
 #ifndef ARCTOPK_SHORT_DEC_CHUNK
 #define ARCTOPK_SHORT_DEC_CHUNK 4096   // elements per short-row (m < 256) decode chunk
 #endif
+#ifndef ARCTOPK_SHORT3_DEC
+#define ARCTOPK_SHORT3_DEC 1           // short-row decode (4 <= m < 256, quad-aligned tensors): mode 3
+#endif
+#ifndef ARCTOPK_SHORT3_CHUNK
+#define ARCTOPK_SHORT3_CHUNK 4096      // ... elements per chunk at most (LDS: 4 (m + 1) / m B each)
+#endif
 #ifndef ARCTOPK_ENC_TARGET_BLOCKS_E
 #define ARCTOPK_ENC_TARGET_BLOCKS_E 4096  // ... for the fp32 kernels that also stream E (large tensors)
 #endif
@@ -158,6 +164,8 @@ struct SegDev {
     uint32_t magic32;  // ceil(2^32 / m): exact quotient for x < 2^32 / m (in-tile indices)
     int32_t nparts;    // encode column parts (V slice of each fits in LDS); 1 = unsplit
     int64_t part_off;  // nparts > 1: partial sketches at part_buf[part_off + (p * n + row) * r]
+    int32_t dchunk0;      // decode mode 3 (short rows): global index of the segment's first decode
+    int32_t dchunk_rows;  // chunk, and rows per chunk (0: the segment has no mode-3 chunks)
 };
 
 __device__ __forceinline__ uint32_t div32(uint32_t x, uint32_t magic) { return __umulhi(x, magic); }
@@ -367,7 +375,10 @@ struct VDrawJob {      // a projection draw riding in the trailing blocks of ano
 struct Chunk {         // pack: selected-row range (mode 0) or row range (mode 1); decode: row range
     int32_t seg;
     int32_t mode;      // 1: m in {1, 2}, fp32, 16-B aligned: quad streams over every row;
-                       // decode 2: 4 <= m < 256 fp32, lane per output quad
+                       // decode 2: 4 <= m < 256 fp32, lane per output quad;
+                       // decode 3: 4 <= m < 256, quad-aligned chunks: the chunk's slot map and
+                       //   packed rows staged in LDS, the packed range read from the chunk
+                       //   table the pack wrote (d_dfirst), one round trip for the data
     int64_t row0;
     int64_t nrows;
 };
@@ -401,6 +412,9 @@ struct arctopk_plan {
     int32_t* h_pack_begin;        // [nseg + 1]: first pack chunk of each segment
     int32_t* h_dec_begin;         // [nseg + 1]: first decode chunk of each segment
     int dec_lds_bytes;            // dynamic LDS of the decode launch (small-m chunk tiles)
+    int32_t* d_dfirst;            // [n_dec + 1]: per decode chunk, the bucket-wide index (sel_off +
+                                  // slot) of its first selected row; written by the pack from the
+                                  // row list, read by mode-3 decode chunks (and the next entry)
     uint32_t* d_keys;             // select workspace: one key per row
     int32_t* d_small;             // segments selected by the fused one-block kernel
     int n_small;

@@ -36,6 +36,8 @@ struct MItem {
     int64_t cand_cap;  // candidate-list capacity
     int32_t range;     // keys per range (multiple of kMTile)
     int32_t nranges;   // ceil(n / range) <= kMMaxRanges
+    int32_t win;       // ARC: index of the item's first-digit window (MWorkspace::win_*), -1: none
+    int32_t pad_;
 };
 
 struct MBatch {
@@ -62,8 +64,14 @@ struct alignas(128) MCounter {
 };
 __host__ __device__ constexpr int hist_slot(int bin) { return ((bin & 127) << 5) | (bin >> 7); }
 
+constexpr int kMWin = 4096;        // ARC items with a first-digit window (per plan)
+
 struct MWorkspace {
     uint32_t hist[kMB][kMBins];  // indexed by hist_slot(bin)
+    // ARC first-digit windows, kept across calls (see arc_digit): item i's keys are binned by
+    // (key >> win_sh[i]) - win_base[i], clamped to the 4096 bins; win_sh 0 = no window yet
+    uint32_t win_sh[kMWin];
+    uint32_t win_base[kMWin];
     MState st[kMB];
     MCounter ncand[kMB];
     MCounter done[kMB];          // blocks of the running kernel that finished, per item
@@ -148,8 +156,58 @@ __device__ inline void ms_init_item(MWorkspace* ws, int t, int64_t k, uint32_t k
 // bin holding the k-th largest key, and start the item in candidate mode on that bin
 // (cand_cap = n for ARC items: every key of the bin fits).
 constexpr int kArcShift = 31 - 12;
+
+// ---- ARC first digit: the top 12 value bits, or a window around the last call's threshold ----
+// With the top 12 bits, a first-pass bin spans 1/16 of an octave of energy, and the bin holding
+// the k-th largest key of a 1 M-row item holds ~14 K keys (1x1-conv rows, compress ratio 0.2):
+// the compact and refine passes then move and radix-sort all of them.  After a call, the
+// refine centres the item's window on the exact threshold T it found: 4096 bins of
+// 2^kArcWinShift keys (1/512 octave, +-4 octaves around T), so the bin of the next call's
+// k-th key holds ~30x fewer keys.  Keys outside the window fall into the two edge bins; if the
+// k-th key lands there (the energies moved by > 16x), that bin is not a bit prefix and the
+// refine resolves all 32 bits of its keys -- slower, never wrong.
+constexpr uint32_t kArcWinShift = 14;
+struct ArcWin {
+    uint32_t sh, base;
+};
+__device__ inline ArcWin arc_win(const MWorkspace* ws, int idx) {
+    ArcWin w{(uint32_t)kArcShift, 0u};
+    if (idx >= 0) {
+        const uint32_t sh = ws->win_sh[idx];
+        if (sh) w = ArcWin{sh, ws->win_base[idx]};
+    }
+    return w;
+}
+__device__ __forceinline__ uint32_t arc_digit(uint32_t key, ArcWin w) {
+    const uint32_t h = key >> w.sh;
+    return h < w.base ? 0u : min(h - w.base, (uint32_t)kMBins - 1u);
+}
+// the bin d as a radix state: a bit prefix, or (edge bin of a window) no decided bits
+__device__ inline void arc_bin_state(ArcWin w, uint32_t d, uint32_t* prefix, uint32_t* mask, int32_t* bit) {
+    const bool lo_edge = d == 0 && w.base > 0;
+    const bool hi_edge = d == (uint32_t)kMBins - 1 && (0x7FFFFFFFu >> w.sh) > w.base + (uint32_t)kMBins - 1;
+    if (lo_edge || hi_edge) {
+        *prefix = 0u;
+        *mask = 0u;
+        *bit = 32;
+    } else {
+        *prefix = (d + w.base) << w.sh;
+        *mask = ~((1u << w.sh) - 1u);
+        *bit = (int32_t)w.sh;
+    }
+}
+// the window of the next call, centred on this call's threshold T
+__device__ inline void arc_win_update(MWorkspace* ws, int idx, uint32_t T) {
+    if (idx < 0) return;
+    constexpr uint32_t top = 0x7FFFFFFFu >> kArcWinShift;  // largest key >> shift
+    const uint32_t c = T >> kArcWinShift;
+    uint32_t base = c > (uint32_t)kMBins / 2 ? c - (uint32_t)kMBins / 2 : 0u;
+    if (base + (uint32_t)kMBins - 1 > top) base = top + 1 - (uint32_t)kMBins;
+    ws->win_base[idx] = base;
+    ws->win_sh[idx] = kArcWinShift;
+}
 template <int NT>
-__device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k, uint32_t* lds_h /* kMBins */) {
+__device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k, ArcWin w, uint32_t* lds_h /* kMBins */) {
     __shared__ uint32_t s_w[NT / 64], s_d, s_acc;
     constexpr int PER = kMBins / NT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -185,9 +243,7 @@ __device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k, uint
     __syncthreads();
     if (tid == 0) {
         MState& g = ws->st[t];
-        g.prefix = s_d << kArcShift;
-        g.mask = ~((1u << kArcShift) - 1u);
-        g.bit = kArcShift;
+        arc_bin_state(w, s_d, &g.prefix, &g.mask, &g.bit);
         g.kk = k - (int64_t)s_acc;
         g.cand = 1;
         g.p1 = g.prefix;

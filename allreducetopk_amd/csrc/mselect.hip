@@ -270,29 +270,28 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
     int t, r;
     if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
-    MState s;
+    const ArcWin w = arc_win(ws, it.win);
+    uint32_t d;  // the first-pass bin (keys above it are selected; its keys are the candidates)
     if constexpr (kArcLocalDigit) {
         __shared__ uint32_t lds_d[256 + 128];
-        uint32_t d, acc;
+        uint32_t acc;
         ms_arc_digit_local<256>(ws->hist[t], it.k, lds_d, &d, &acc);
-        s.p1 = d << kArcShift;
-        s.m1 = ~((1u << kArcShift) - 1u);
         if (r == 0 && threadIdx.x == 0) {  // the item's state for the refine (next launch)
             MState g;
-            g.prefix = s.p1;
-            g.mask = s.m1;
-            g.bit = kArcShift;
+            arc_bin_state(w, d, &g.prefix, &g.mask, &g.bit);
             g.cand = 1;
             g.kk = it.k - (int64_t)acc;
-            g.p1 = s.p1;
-            g.m1 = s.m1;
+            g.p1 = g.prefix;
+            g.m1 = g.mask;
             g.ncand = 0;
             ws->st[t] = g;
         }
     } else {
-        s = ws->st[t];
+        // the key pass's last block left the bin's radix state: recover d from a key of it
+        // (prefix bins only; with a window, ARCTOPK_ARC_LOCAL_DIGIT = 0 is not supported)
+        const MState s = ws->st[t];
+        d = arc_digit(s.p1, w);
     }
-    const uint32_t hi = s.p1 | ~s.m1;  // largest key of the bin
     const int64_t r0 = (int64_t)r * it.range;
     const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -309,8 +308,9 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
             const bool valid = wb + j * 64 + lane < r1;
-            gt += (valid && kv[j] > hi) ? 1u : 0u;
-            bm[j] = __ballot(valid && (kv[j] & s.m1) == s.p1);
+            const uint32_t dj = arc_digit(kv[j], w);
+            gt += (valid && dj > d) ? 1u : 0u;
+            bm[j] = __ballot(valid && dj == d);
             nin += popc64(bm[j]);
         }
         if (lane == 0) s_cnt[wave] = nin;
@@ -585,6 +585,8 @@ void ms_item_geometry(MItem& it) {
     // candidates: the k-th key's 12-bit bin; a few % of n on gradient-like data, all of
     // n on degenerate data (e.g. a zero tensor) -> full mode past the cap
     it.cand_cap = it.n <= 65536 ? it.n : std::max<int64_t>(65536, it.n / 8);
+    it.win = -1;  // ARC plans assign first-digit windows (plan.hip)
+    it.pad_ = 0;
 }
 
 int64_t ms_workspace_bytes(int64_t cap_total) {

@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <numeric>
 #include <vector>
 
 #include "common.h"
@@ -233,7 +234,19 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 pack.push_back(Chunk{(int32_t)i, 0, j, std::min(per, s.k_rows - j)});
         }
         // ---- decode chunks: all rows
-        if (small_tile && dtype == ARCTOPK_F32 && ARCTOPK_QUAD_DEC) {
+        g.dchunk0 = (int32_t)dec.size();
+        g.dchunk_rows = 0;
+        // mode 3 (short rows, quad-aligned data): chunks of <= ARCTOPK_SHORT3_CHUNK elements whose
+        // first elements are quad-aligned (rows per chunk a multiple of 4 / gcd(m, 4))
+        const int64_t q3 = 4 / std::gcd<int64_t>(s.m, 4);
+        if (small_tile && ARCTOPK_SHORT3_DEC && s.offset % 4 == 0 &&
+            (int64_t)ARCTOPK_SHORT3_CHUNK / s.m >= q3) {
+            const int64_t per = (int64_t)ARCTOPK_SHORT3_CHUNK / s.m / q3 * q3;
+            g.dchunk_rows = (int32_t)per;
+            for (int64_t row = 0; row < s.n; row += per)
+                dec.push_back(Chunk{(int32_t)i, 3, row, std::min(per, s.n - row)});
+            dec_lds = std::max<int64_t>(dec_lds, (std::min(per, s.n) * (s.m + 1)) * 4);
+        } else if (small_tile && dtype == ARCTOPK_F32 && ARCTOPK_QUAD_DEC) {
             // mode 2: lane per 16-B output quad, rows of whole chunks (no LDS tile)
             const int64_t per = std::max<int64_t>(1, (int64_t)ARCTOPK_QUAD_DEC_CHUNK / s.m);
             for (int64_t row = 0; row < s.n; row += per)
@@ -289,6 +302,9 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     if (p->n_enc_e) ALLOC_COPY(p->d_enc_e, enc_e);
     ALLOC_COPY(p->d_pack, pack);
     ALLOC_COPY(p->d_dec, dec);
+    e = hipMalloc((void**)&p->d_dfirst, (dec.size() + 1) * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(p->d_dfirst, 0, (dec.size() + 1) * sizeof(int32_t));
+    if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
     ALLOC_COPY(p->d_small, small_ids);
     ALLOC_COPY(p->d_large, large_ids);
     ALLOC_COPY(p->d_split, split_ids);
@@ -315,6 +331,8 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 it.slot_off = sg.row_off;
                 ms_item_geometry(it);
                 it.cand_cap = it.n;  // ARC: every key of the first-pass bin is a candidate
+                const int gi = bi * kMB + i;  // = the key pass's item index (first + t)
+                it.win = gi < kMWin ? gi : -1;
                 it.cand_off = cap;
                 cap += it.cand_cap;
             }
@@ -378,6 +396,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_enc_e) (void)hipFree(p->d_enc_e);
     if (p->d_pack) (void)hipFree(p->d_pack);
     if (p->d_dec) (void)hipFree(p->d_dec);
+    if (p->d_dfirst) (void)hipFree(p->d_dfirst);
     if (p->d_keys) (void)hipFree(p->d_keys);
     if (p->d_small) (void)hipFree(p->d_small);
     if (p->d_large) (void)hipFree(p->d_large);

@@ -87,12 +87,17 @@ def pmc_traffic(workload: str, ef: str, kernel: str):
     import glob
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_{workload}_{ef}.json")))
     if not paths:
-        return None, None
+        return None, None, None
     with open(paths[-1]) as fh:
-        ent = json.load(fh)["kernels"].get(kernel)
+        doc = json.load(fh)
+    ent = doc["kernels"].get(kernel)
     if not ent:
-        return None, None
-    return ent["bytes_per_launch"], os.path.relpath(paths[-1], REPO)
+        return None, None, None
+    # the profile's library vs the one running now (PMC files stamped with the source hash)
+    from allreducetopk_amd.build import embedded_hash
+    lib = doc.get("lib_hash")
+    match = None if lib is None else lib == embedded_hash()
+    return ent["bytes_per_launch"], os.path.relpath(paths[-1], REPO), match
 
 
 def _cpu_model() -> str:
@@ -184,6 +189,12 @@ def main():
                     help="nccl = RCCL (real runs); gloo lets N ranks share one GPU (rehearsal)")
     ap.add_argument("--host-staged", action="store_true",
                     help="D2H + H2D of the packed payload around the all-reduce (NIC model)")
+    ap.add_argument("--wire-busbw", type=float, nargs="*", default=[350.0],
+                    help="at N = 1: also time the exchange path beside an emulated WIRE_RANKS-rank ring "
+                         "all-reduce paced to each of these bus bandwidths (GB/s; none: skip)")
+    ap.add_argument("--wire-ranks", type=int, default=8)
+    ap.add_argument("--wire-blocks", type=int, default=32,
+                    help="workgroups of the emulated collective (its CU footprint)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -284,6 +295,32 @@ def main():
                   "hook_path": "exchange (one-rank RCCL communicators)"}
         st.force_exchange = False
 
+    # The same exchange path beside an emulated N-rank wire (exchange.Comm.wire): each all-reduce
+    # costs this GPU what a ring all-reduce over WIRE_RANKS GPUs would -- 2 (R-1)/R of the buffer
+    # read and rewritten in HBM by WIRE_BLOCKS workgroups, paced to the bus bandwidth -- so the
+    # codec's kernels run beside the collective's CU and HBM footprint.
+    wire = []
+    if (world == 1 and args.hook == "arc" and not args.host_staged and not args.force_exchange
+            and args.backend == "nccl"):
+        for bw in args.wire_busbw or []:
+            st.reset_exchange_comms()
+            st.emulate_wire = dict(ranks=args.wire_ranks, busbw_gbs=bw, latency_us=15.0, blocks=args.wire_blocks)
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            fe = time.perf_counter() - t1
+            v = args.steps * bytes_per_step / fe / 1e9
+            wire.append({"busbw_gbs": bw, "emulated_ranks": args.wire_ranks, "blocks": args.wire_blocks,
+                         "latency_us": 15.0, "per_gpu_value": round(v, 2),
+                         "implied_aggregate": round(args.wire_ranks * v, 2),
+                         "ms_per_bucket": round(fe / args.steps / nb * 1e3, 4)})
+        st.reset_exchange_comms()
+        st.emulate_wire = None
+
     phase_ms = {}
     light = {}
     sample_steps = 0
@@ -296,16 +333,28 @@ def main():
         # .. after the encode); the full per-phase breakdown on every 32nd call
         st.hook_events = hs = []
         st.hook_event_every = 2
-        st.phase_events = pe_list = []
+        st.phase_events = None
         pe = st.phase_event_every = 32
         sample_steps = max(args.steps, 16)
         for _ in range(sample_steps):
             step()
         torch.cuda.synchronize()
-        st.hook_events = st.phase_events = None
+        # the per-phase breakdown from calls whose decode runs inline (with deferred decodes a
+        # step's decode lands in a later call, so its markers would bracket other work)
+        st.hook_events = None
+        st.phase_events = pe_list = []
+        st.phase_event_every = 1
+        st.defer_decode = False
+        for _ in range(4):
+            step()
+        torch.cuda.synchronize()
+        st.defer_decode = True
+        st.phase_events = None
         if pe_list:
             order = [p for p in ["start", "draw", "encode", "sketch_allreduce", "select", "pack", "h2d",
                                  "packed_allreduce", "decode"] if p in pe_list[0]]
+            if world == 1 and not args.force_exchange:  # no collectives at world size 1
+                order = [p for p in order if p not in ("sketch_allreduce", "packed_allreduce")]
             for a, b in zip(order[:-1], order[1:]):
                 phase_ms[b] = statistics.median(ev[a].elapsed_time(ev[b]) for ev in pe_list)
             phase_ms["hook_device_total"] = statistics.median(
@@ -314,8 +363,7 @@ def main():
         hd = sorted((ev for ev in hs if "decode" in ev), key=lambda ev: ev["_call"])
         # consecutive decode markers with no full-phase sample (every 32nd call) between them
         per_call = [a_["decode"].elapsed_time(b_["decode"]) / (b_["_call"] - a_["_call"])
-                    for a_, b_ in zip(hd, hd[1:])
-                    if not any(c % pe == 0 for c in range(a_["_call"] + 1, b_["_call"] + 1))]
+                    for a_, b_ in zip(hd, hd[1:])]
         if he and per_call:
             light = {"samples": len(he), "hook_samples": len(per_call),
                      "encode": statistics.median(ev["draw"].elapsed_time(ev["encode"]) for ev in he),
@@ -358,8 +406,15 @@ def main():
                         "wall_us": round(wall_s * 1e6, 1),
                         "wall_frac": round(alg["total"] / wall_s / 1e9 / HBM_PEAK_GBS, 4),
                         "headline": "frac (read + write bytes over device time)"}
+        # the north star names the HBM-read roofline; the headline fraction here
+        # counts read + write bytes (every phase writes as much as it must), read_frac only reads
+        roof["headline_choice"] = ("frac = encode read+write bytes over its duration; hook.frac = the whole "
+                                   "codec's read+write bytes over its device time; hook.read_frac = its "
+                                   "read bytes only (the north star's 'HBM-read roofline' reading)")
+        roof["read_frac"] = roof["hook"]["read_frac"]
     if roof is not None:
-        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.workload + ("_bf16" if args.dtype == "bf16" else ""), args.ef, "k_encode")
+        roof["traffic"], roof["traffic_source"], roof["traffic_lib_match"] = pmc_traffic(
+            args.workload + ("_bf16" if args.dtype == "bf16" else ""), args.ef, "k_encode")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -381,8 +436,10 @@ def main():
                                      "next bucket")},
         "per_gpu_value": round(value / world, 2),
         "forced_exchange": forced,
+        "emulated_wire": wire or None,
         "ms_per_bucket": round(ms_per_step / nb, 4),
         "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
+        "phase_ms_note": "separate pass, every call marked, decodes inline (not deferred)" if phase_ms else None,
         "roofline": roof,
         "algorithmic_bytes_per_call": {k: int(v) for k, v in alg.items()},
         "cpu_baseline": None,

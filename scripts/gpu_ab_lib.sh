@@ -10,7 +10,7 @@ for rep in 1 2; do
   for lib in ${AB_LIBS:-product} ${VARIANTS}; do
     if [ "$lib" = product ]; then L=""; else L="allreducetopk_amd/lib/var/libarctopk_$lib.so"; fi
     LOG=gpurun_out/ab/${lib}${TAG}.log
-    ARCTOPK_LIB=$L timeout -k 10 200 python bench.py --steps 50 --no-cpu-baseline --no-forced-exchange ${BENCH_ARGS} > $LOG 2>&1 || { tail -5 $LOG; exit 1; }
+    ARCTOPK_LIB=$L timeout -k 10 200 python bench.py --steps 50 --no-cpu-baseline --no-forced-exchange --wire-busbw ${BENCH_ARGS} > $LOG 2>&1 || { tail -5 $LOG; exit 1; }
     tail -1 $LOG | python -c "import json,sys; d=json.loads(sys.stdin.read()); p=d['phase_ms']; print('${BENCH_ARGS}', '$lib', d['config']['hook_path'], d['value'], round(d['roofline']['avg_launch_us'],1), round(d['roofline']['hook']['device_us'],1), {k: round(v*1e3,1) for k,v in p.items()})" | tee -a gpurun_out/ab/summary.txt
   done
 done

@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4t
-timeout -k 10 400 python -u -m pytest tests/test_gpu_exchange_failures.py tests/test_gpu_sparse.py -m gpu -v -k "exchange_failures or randk or Rccl or rccl or wire or direct or aborted" --timeout 120 --timeout-method thread > gpurun_out/r4t/new.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_exchange_failures.py tests/test_gpu_sparse.py tests/test_gpu_arctopk.py -m gpu -v -k "exchange_failures or randk or rccl or wire or direct or aborted or window" --timeout 120 --timeout-method thread > gpurun_out/r4t/new.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR" gpurun_out/r4t/new.log | tail -30
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc

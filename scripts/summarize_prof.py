@@ -60,7 +60,10 @@ for ent in out.values():
     ent["read_bytes"] = round(ent["read_bytes"] / ent["launches"])
     ent["write_bytes"] = round(ent["write_bytes"] / ent["launches"])
     ent["bytes_per_launch"] = ent["read_bytes"] + ent["write_bytes"]
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from allreducetopk_amd.build import embedded_hash  # noqa: E402
 with open(os.path.join(root, "pmc_per_launch.json"), "w") as fh:
     json.dump({"note": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads) + WRITE_SIZE, "
                        "KiB -> bytes, averaged per launch; separate --pmc passes",
+               "lib_hash": embedded_hash(),  # the libarctopk.so source hash these counters were taken on
                "kernels": out}, fh, indent=1)

@@ -429,6 +429,38 @@ def test_select_crowded_first_bin(fill):
         assert torch.all(r_[1:] > r_[:-1])
 
 
+def test_select_first_digit_window_across_calls():
+    """The multi-block select bins the next call's keys in a window centred on the last
+    threshold (mselect.h, arc_digit): calls whose energies stay inside it, jump far above or
+    below it (the k-th key in an edge bin: a full 32-bit radix of that bin), collapse to ties,
+    or come back -- every call exact under the tie rule, on one plan (1 M-row 1x1-conv items,
+    131 K-row 3x3 items, a 40 K-row 2-D item, and 1-D tensors riding along)."""
+    shapes = [(2048, 1024, 1, 1), (512, 512, 3, 3), (40000, 8), (2048,), (512,)]
+    segs = A.segments(shapes, 0.2)
+    plan = BucketPlan(shapes, 4, 0.2, torch.float32, DEV)
+    stream = torch.cuda.current_stream().cuda_stream
+    gen = torch.Generator().manual_seed(11)
+    for call, scale in enumerate([1.0, 1.0, 1.5, 1e5, 1e5, 1e-7, 0.0, 1.0, 300.0]):
+        Ps = []
+        for s in segs:
+            w = s.n if s.kind == A.RAW else s.n * 4
+            P = (torch.randn(w, generator=gen) * scale).reshape(-1, 1 if s.kind == A.RAW else 4)
+            if call == 4:  # half the rows tied at one value inside the (moved) window
+                P[::2] = P[0]
+            Ps.append(P[:, 0].contiguous() if s.kind == A.RAW else P)
+        ref = torch.cat([p.flatten() for p in Ps])
+        plan.sketch[:ref.numel()].copy_(ref.to(DEV))
+        plan.select(1, stream)
+        torch.cuda.synchronize()
+        norms, _ = A.select(Ps, 1, segs)
+        for j, (r_, nrm, s) in enumerate(zip(_gpu_rows(plan), norms, plan.segments)):
+            assert check_rows_tie_aware(r_, nrm, int(s.k_rows), band=0.0) == 0, f"call {call} seg {j}"
+            assert torch.all(r_[1:] > r_[:-1]), f"call {call} seg {j}: rows not ascending"
+            sm = plan.slotmap[s.row_off:s.row_off + s.n].cpu()
+            assert torch.equal(sm[r_], torch.arange(int(s.k_rows), dtype=sm.dtype)), f"call {call} seg {j} slots"
+            assert int((sm >= 0).sum()) == int(s.k_rows)
+
+
 @pytest.mark.parametrize("name", [n for n in case_names("arc_") if "bf16" in n and n.endswith("ws1")])
 def test_bf16_golden_on_gpu(name):
     """bf16 buckets against reference-generated golden vectors.

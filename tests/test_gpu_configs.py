@@ -204,7 +204,7 @@ def test_resnet50_mix_arc(ef, nb, force_exchange):
     """configs[3] through ARC-TopK: 1x1 convs (m = 2, sketch twice the tensor; 524,288 and
     1,048,576-row segments), 3x3 convs (m = 18) and 1-D BatchNorm tensors in one bucket.  With
     two buckets per backward the first bucket's deferred decode rides in the second bucket's
-    fused write launch (spans of ranges per block)."""
+    last select launch (the write launch; the 1 M-row items take the refine launch before it)."""
     n = bucket_numel(RESNET50)
     run = ArcRun(ef, seed=21, force_exchange=force_exchange)
     for it in range(3):
@@ -213,7 +213,8 @@ def test_resnet50_mix_arc(ef, nb, force_exchange):
 
 def test_conv3x3_stack_ef14():
     """28 x [512, 512, 3, 3] (m = 18, 131,072 rows each, 896 ranges of the multi-block
-    select): the fused write launch with two ranges per block."""
+    select: more write blocks than stay resident at once, so the refine has a launch of its
+    own before the write launch) and the short-row (mode 3) decode."""
     shapes = WORKLOADS["resnet18_conv"][1]
     n = bucket_numel(shapes)
     run = ArcRun("ef14", seed=41)

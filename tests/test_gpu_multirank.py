@@ -280,6 +280,7 @@ def _ddp_check(model, st, ost, ws, rank, ef, steps, x, flips_ok=2):
             checked += 1
     assert st.iter == steps
     assert checked >= 2 * (steps - st.start_compress_iter - (ef == "ef21"))
+    print(f"rank{rank}: {flips} rows differ from the oracle's selection (band 2e-4)")
     assert flips <= flips_ok, f"{flips} rows differ from the oracle's selection (near-ties only)"
 
 
@@ -299,7 +300,7 @@ def test_hook_inside_ddp_rccl(force_exchange):
                           use_error_feedback="ef14", seed=3)
     st.force_exchange = force_exchange
     x = torch.randn(8, 3, 8, 8, device="cuda")
-    _ddp_check(model, st, A.OracleState(seed=3), 1, 0, "ef14", 4, x)
+    _ddp_check(model, st, A.OracleState(seed=3), 1, 0, "ef14", 4, x, flips_ok=0)
     if force_exchange:
         assert st._comms is not None and st._comms[3].kind == "rccl" and st._comms[3].size == 1
 
