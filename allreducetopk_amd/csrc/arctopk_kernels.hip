@@ -2007,7 +2007,8 @@ constexpr bool kPackFullQuads = ARCTOPK_PACK_FULL_QUADS != 0;
 #endif
 constexpr bool kPackPairs = ARCTOPK_PACK_PAIRS != 0;
 #ifndef ARCTOPK_PACK_QUADS
-#define ARCTOPK_PACK_QUADS 1  // tuning switch (A/B builds): 0 = 8-B pairs for even short rows
+#define ARCTOPK_PACK_QUADS 0  // tuning switch (A/B builds): 1 = 16-B quads for even short rows (measured
+                              // slower: 28 x [512,512,3,3] pack 60 -> 80 us)
 #endif
 constexpr bool kPackQuads = ARCTOPK_PACK_QUADS != 0;
 
@@ -3150,6 +3151,9 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
 #endif
         int e = ms_arc_compact(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, st);
         if (e) return e;
+#if ARCTOPK_DIAG_STOP == 2  // diagnostic builds only: stop after the compact pass
+        continue;
+#endif
         const int nsm = (bi == 0 && !ARCTOPK_DIAG_NOSMALL) ? p->n_small : 0;
         VDrawJob bj = job;
         if (bi != 0) bj.n = 0;

@@ -585,3 +585,32 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
     return e;
 }
+
+// Diagnostics (not in the public header): the first `bytes` of a plan's multi-block select
+// workspace (arctopk::MWorkspace: histograms, first-digit windows, item states, per-range
+// counts), copied to the host after the device is idle.
+extern "C" int arctopk_diag_mws(const arctopk_plan* p, void* host, int64_t bytes) {
+    if (!p || !host || bytes < 0) return ARCTOPK_EINVAL;
+    if (!p->d_mws) return ARCTOPK_EINVAL;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(host, p->d_mws, (size_t)bytes, hipMemcpyDeviceToHost);
+    return (int)e;
+}
+
+// Diagnostics (not in the public header): the plan's row-energy keys (select workspace), as
+// the last select left them.
+extern "C" int arctopk_diag_keys(const arctopk_plan* p, uint32_t* host, int64_t n) {
+    if (!p || !host || n < 0 || n > p->info.rows_total) return ARCTOPK_EINVAL;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(host, p->d_keys, (size_t)n * 4, hipMemcpyDeviceToHost);
+    return (int)e;
+}
+
+// Diagnostics (not in the public header): overwrite `bytes` of the plan's select workspace at
+// byte offset `off` (e.g. a first-digit window) from the host.
+extern "C" int arctopk_diag_set_mws(const arctopk_plan* p, int64_t off, const void* host, int64_t bytes) {
+    if (!p || !host || off < 0 || bytes < 0 || !p->d_mws) return ARCTOPK_EINVAL;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(reinterpret_cast<char*>(p->d_mws) + off, host, (size_t)bytes, hipMemcpyHostToDevice);
+    return (int)e;
+}

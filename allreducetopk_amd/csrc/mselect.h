@@ -179,8 +179,10 @@ __device__ inline ArcWin arc_win(const MWorkspace* ws, int idx) {
     return w;
 }
 __device__ __forceinline__ uint32_t arc_digit(uint32_t key, ArcWin w) {
-    const uint32_t h = key >> w.sh;
-    return h < w.base ? 0u : min(h - w.base, (uint32_t)kMBins - 1u);
+    // (max before the subtraction: written as `h < base ? 0 : min(h - base, 4095)`, the
+    // compiler of ROCm 7.2 dropped the comparison and kept the wrapping subtraction)
+    const uint32_t h = max(key >> w.sh, w.base);
+    return min(h - w.base, (uint32_t)kMBins - 1u);
 }
 // the bin d as a radix state: a bit prefix, or (edge bin of a window) no decided bits
 __device__ inline void arc_bin_state(ArcWin w, uint32_t d, uint32_t* prefix, uint32_t* mask, int32_t* bit) {
@@ -197,8 +199,11 @@ __device__ inline void arc_bin_state(ArcWin w, uint32_t d, uint32_t* prefix, uin
     }
 }
 // the window of the next call, centred on this call's threshold T
+#ifndef ARCTOPK_ARC_WINDOW
+#define ARCTOPK_ARC_WINDOW 1  // tuning switch (A/B builds): 0 = always the top 12 value bits
+#endif
 __device__ inline void arc_win_update(MWorkspace* ws, int idx, uint32_t T) {
-    if (idx < 0) return;
+    if (idx < 0 || !ARCTOPK_ARC_WINDOW) return;
     constexpr uint32_t top = 0x7FFFFFFFu >> kArcWinShift;  // largest key >> shift
     const uint32_t c = T >> kArcWinShift;
     uint32_t base = c > (uint32_t)kMBins / 2 ? c - (uint32_t)kMBins / 2 : 0u;

@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r4d
+ARCTOPK_LIB=allreducetopk_amd/lib/var/libarctopk_stop2.so timeout -k 10 120 python3 scripts/sel_window_dbg2.py 2>&1 | tee gpurun_out/r4d/selwin2.log

@@ -454,6 +454,12 @@ def test_select_first_digit_window_across_calls():
         torch.cuda.synchronize()
         norms, _ = A.select(Ps, 1, segs)
         for j, (r_, nrm, s) in enumerate(zip(_gpu_rows(plan), norms, plan.segments)):
+            sm = plan.slotmap[s.row_off:s.row_off + s.n].cpu()
+            kth = torch.topk(nrm.double(), int(s.k_rows)).values.min().item()
+            assert torch.unique(r_).numel() == int(s.k_rows), (
+                f"call {call} (scale {scale}) seg {j}: {torch.unique(r_).numel()} distinct rows of "
+                f"{int(s.k_rows)}, {int((sm >= 0).sum())} slots set, k-th energy {kth:.6e}, "
+                f"{int((nrm.double() > kth).sum())} above it, {int((nrm.double() == kth).sum())} equal")
             assert check_rows_tie_aware(r_, nrm, int(s.k_rows), band=0.0) == 0, f"call {call} seg {j}"
             assert torch.all(r_[1:] > r_[:-1]), f"call {call} seg {j}: rows not ascending"
             sm = plan.slotmap[s.row_off:s.row_off + s.n].cpu()
