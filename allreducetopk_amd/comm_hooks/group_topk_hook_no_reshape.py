@@ -963,6 +963,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         fin_plans = (N.c_void_p * max(1, nf))(*[e_[0].handle for e_ in fin])
         fin_marks = (N.c_void_p * max(1, nf))(*[N.ctypes.cast(e_[2], N.c_void_p).value if e_[2] is not None
                                                 else None for e_ in fin])
+        _ht("prep")
         st_ = L.arctopk_exchange_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
                                       int(err_in), int(draw), seed,
                                       nplan.handle if nplan is not None else None, nseed,
@@ -982,7 +983,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             nplan.v_drawn, nplan.v_stream = nseed, sid
         if vslot >= 0:
             plan.projection_consumed(vslot, torch.cuda.current_stream(dev))
-        _ht("exchange_step")
+        _ht("native_step")
         state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
         state.maybe_increase_iter(bucket)
         if defer:

@@ -1884,6 +1884,16 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
     int64_t row = (int64_t)bx * KT + threadIdx.x;
     const T* sk = sketch + s.sketch_off;
     uint32_t* kout = keys + s.row_off;
+    // The two edge bins are counted in registers: they can be hot (a first-digit window puts every
+    // key below it in bin 0, ~10 % of a 1x1-conv item; tied zero rows all land in bin 0), and
+    // LDS atomics of a wave on ONE word serialise (measured: a window cost the select 16 us)
+    uint32_t c_lo = 0, c_hi = 0;
+    auto count = [&](uint32_t key) {
+        const uint32_t dg = arc_digit(key, w);
+        if (dg == 0u) ++c_lo;
+        else if (dg == (uint32_t)kMBins - 1u) ++c_hi;
+        else atomicAdd(&h[dg], 1u);
+    };
     if (stride == 4 && (s.sketch_off & 3) == 0) {  // r = 4: one quad load per row, UK rows in flight
         constexpr int UK = 8;
         for (; row < s.n; row += UK * gs) {
@@ -1897,7 +1907,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
                     const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
                     kout[rr] = key;
 #if ARCTOPK_DIAG_KEYS < 2
-                    atomicAdd(&h[arc_digit(key, w)], 1u);
+                    count(key);
 #endif
                 }
             }
@@ -1913,9 +1923,18 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
             if (rr < s.n) {
                 const uint32_t key = energy_key(e[u]);
                 kout[rr] = key;
-                atomicAdd(&h[arc_digit(key, w)], 1u);
+                count(key);
             }
         }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        c_lo += __shfl_xor(c_lo, o, 64);
+        c_hi += __shfl_xor(c_hi, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c_lo) atomicAdd(&h[0], c_lo);
+        if (c_hi) atomicAdd(&h[kMBins - 1], c_hi);
     }
     __syncthreads();
     DIAG_STAMP(g_st_keys, 1);
