@@ -356,6 +356,12 @@ class GroupTopKState(HookState):
         # dict(ranks=8, busbw_gbs=350)) instead of real ones; with force_exchange at world
         # size 1 the step then runs beside the local cost of an N-rank ring
         self.emulate_wire = None
+        # CU partition of the exchange path: > 0 runs the packed
+        # all-reduces on a stream restricted to that many CUs and the codec's kernels on a
+        # stream restricted to the others (event-ordered with the caller's stream), so the
+        # collective's workgroups never wait for CUs held by an encode grid.  0: one pool.
+        self.exchange_cus = int(os.environ.get("ARCTOPK_XCU", "0"))
+        self._partition = None
         # Sketch all-reduces on a communicator of their own ("separate") or on the packed
         # values' communicator ("shared": a sketch then queues behind the previous bucket's
         # packed all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
@@ -469,13 +475,26 @@ class GroupTopKState(HookState):
         """Enqueue deferred decodes in call order (each on the stream of its call) and
         complete their Futures: all of them, or up to and including `upto`'s.  The hook does
         this itself in later calls; a Python wait()/value() on such a Future does it too."""
+        part, used = self._partition, False
         while self._x_pend:
             plan, fut, marks, t, sid, _keep = self._x_pend.pop(0)
             N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
+            used = used or (part is not None and sid == part.cs)
             fut.set_result(t)
             if fut is upto:
                 break
+        if used:  # decodes enqueued on the codec's CU partition: the caller's stream follows them
+            part.join(_current_raw_stream(part.dix))
         self._raise_if_comm_failed()
+
+    def _partition_for(self, dev) -> "_Partition":
+        dix = torch.device(dev).index or 0
+        p = self._partition
+        if p is None or p.dix != dix or p.cus != self.exchange_cus:
+            if self._x_pend:
+                self.flush_exchange()
+            p = self._partition = _Partition(dix, self.exchange_cus)
+        return p
 
     def state_dict(self) -> dict:
         self.flush_exchange()  # the deferred decode writes gE (EF21)
@@ -647,6 +666,45 @@ class ExchangeFuture(torch.futures.Future):
         if not self.done():
             self._arctopk_state.flush_exchange(upto=self)
         return super().value()
+
+
+class _Partition:
+    """The exchange path's CU partition (GroupTopKState.exchange_cus): the codec's stream `cs`
+    (every CU but the reserved ones) and the exchange stream `xs` (the reserved CUs),
+    arctopk_stream_create_partition.  A call enters with enter(caller) (cs follows the caller's
+    stream) and leaves with join(caller) (the caller's stream follows cs)."""
+
+    def __init__(self, dix: int, cus: int):
+        L = N.lib()
+        self.dix, self.cus = dix, cus
+        hs = []
+        for side in (0, 1):
+            h = N.ctypes.c_void_p()
+            N.check(L.arctopk_stream_create_partition(dix, cus, side, N.ctypes.byref(h)),
+                    "arctopk_stream_create_partition")
+            hs.append(h.value)
+        self.cs, self.xs = hs
+        dev = torch.device("cuda", dix)
+        self.ext = torch.cuda.ExternalStream(self.cs, device=dev)
+        self.xext = torch.cuda.ExternalStream(self.xs, device=dev)
+        self._in, self._out = N.DeviceEvent(), N.DeviceEvent()
+
+    def enter(self, caller: int) -> None:
+        self._in.record(caller)
+        self._in.wait(self.cs)
+
+    def join(self, caller: int) -> None:
+        self._out.record(self.cs)
+        self._out.wait(caller)
+
+    def __del__(self):
+        L = N._lib
+        for h in (getattr(self, "cs", None), getattr(self, "xs", None)):
+            if h and L is not None:
+                try:
+                    L.arctopk_stream_destroy(h)
+                except Exception:  # interpreter shutdown
+                    pass
 
 
 def _order_after_exchange(state, dev) -> None:
@@ -921,18 +979,25 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         # communicators), and earlier buckets' deferred decodes
         comms = world_size > 1 or state.force_exchange or state.emulate_wire is not None
         sk = pk = None
+        tstream = torch.cuda.current_stream(dev)
+        part = caller = None
         if comms:
             sk, pk = state._exchange_comms(group, dev)  # (a failed communicator: the step returns its status)
             if plan.comm_registered is not pk:
                 sk.register(plan.sketch)
                 pk.register(plan.packed)
                 plan.comm_registered = pk
+            if state.exchange_cus > 0 and state.async_exchange:
+                # the codec's kernels on the unreserved CUs, ordered after the caller's stream
+                part = state._partition_for(dev)
+                caller, sid, tstream = sid, part.cs, part.ext
+                part.enter(caller)
         vslot, vptr, draw, nplan, nseed = -1, None, False, None, 0
         if device_v:
             draw = _claim_projections(state, plan, seed, sid, dev)
             nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
         else:
-            vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, torch.cuda.current_stream(dev))
+            vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, tstream)
             vptr = V.data_ptr()
         # deferred except for the last bucket of a backward (nothing follows it), which then
         # finishes every earlier deferred decode: nothing is left in flight when it returns
@@ -955,7 +1020,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             pend.clear()
         ars = None
         if defer and comms:
-            ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
+            ars = part.xext if part is not None else state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
             if pk.kind == "callback" and ars.cuda_stream not in pk._streams:
                 pk.known_stream(ars)
         marks = _call_marks(state, _EXCHANGE_MARKS)
@@ -982,7 +1047,9 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         if nplan is not None:
             nplan.v_drawn, nplan.v_stream = nseed, sid
         if vslot >= 0:
-            plan.projection_consumed(vslot, torch.cuda.current_stream(dev))
+            plan.projection_consumed(vslot, tstream)
+        if part is not None:
+            part.join(caller)
         _ht("native_step")
         state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
         state.maybe_increase_iter(bucket)

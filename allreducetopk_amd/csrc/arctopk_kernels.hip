@@ -1541,12 +1541,10 @@ constexpr int kFuseCap = 8192;              // staged candidates per block (32 K
 constexpr int64_t kFuseMaxRows = ARCTOPK_FUSE_MAX_ROWS;  // host rule: largest item of a fused batch
 constexpr int kFuseNT = 256;
 constexpr int kFuseMaxBlocks = 512;         // host rule: two blocks per CU (LDS allows three)
-constexpr int kFuseMaxSpan = ARCTOPK_FUSE_MAX_SPAN;     // host rule: ranges per write block
 
-// ranges [r, r + qn) of item t: one span of consecutive ranges per block (several when the
-// batch has more ranges than kFuseMaxBlocks, so every write block is still resident at once
-// and the refine is paid once per span)
-__device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int r, int qn,
+// range r of item t, one range per block (spans of several consecutive ranges per block, the
+// refine paid once per span, measured slower in rounds 3 and 4 and removed)
+__device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int r,
                                                       const uint32_t* __restrict__ keys,
                                                       MWorkspace* ws, const uint32_t* __restrict__ ckey,
                                                       int32_t* __restrict__ out_idx, int32_t* __restrict__ out_slot,
@@ -1561,9 +1559,9 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     const int nr = it.nranges;
     const uint32_t* src = ckey + it.cand_off;
     const int64_t r0 = (int64_t)r * it.range;
-    const int64_t r1 = min<int64_t>(it.n, r0 + (int64_t)qn * it.range);
+    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
     DIAG_STAMP(g_st_refine, 0);
-    // one round trip: the first-pass state, the per-range counts and this span's first tile
+    // one round trip: the first-pass state, the per-range counts and this range's first tile
     MState s = ws->st[t];
     uint32_t cc[PR], cg[PR], kor = 0u, kand = ~0u;
 #pragma unroll
@@ -1704,8 +1702,8 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     DIAG_STAMP(g_st_refine, 3);
     const uint32_t T = s.prefix;
     if (r == 0 && tid == 0) arc_win_update(ws, it.win, T);  // the next call's first-digit window
-    // candidates before this span (> T, == T) and this span's == T
-    const uint32_t cb = roff[r], ce = r + qn < nr ? roff[r + qn] : nc32;
+    // candidates before this range (> T, == T) and this range's == T
+    const uint32_t cb = roff[r], ce = r + 1 < nr ? roff[r + 1] : nc32;
     uint32_t gb = 0, eb = 0, eo = 0;
     if (all_eq) {  // no candidate above T; every one ties with it
         if (tid == 0) {
@@ -1809,9 +1807,9 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
                                              T* __restrict__ gE, T* __restrict__ out,
                                              float* __restrict__ dlds);
 
-// grid: [write spans (nflat)] [small selects] [ride decode chunks (dr.n)] [V draw (job.n)]
+// grid: [write ranges (nflat)] [small selects] [ride decode chunks (dr.n)] [V draw (job.n)]
 template <typename T, int EF>
-__global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, int nflat, int span,
+__global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, int nflat,
                                                              const uint32_t* __restrict__ keys, MWorkspace* ws,
                                                              const uint32_t* __restrict__ ckey,
                                                              const SegDev* __restrict__ segs,
@@ -1833,15 +1831,12 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
         return;
     }
     const MBatch& b = *bp;
-    int t = 0, r = (int)blockIdx.x;  // flat grid: the spans of the batch's items back to back
-    while (t + 1 < b.cnt) {
-        const int ns = (b.it[t].nranges + span - 1) / span;
-        if (r < ns) break;
-        r -= ns;
+    int t = 0, r = (int)blockIdx.x;  // flat grid: the ranges of the batch's items back to back
+    while (t + 1 < b.cnt && r >= b.it[t].nranges) {
+        r -= b.it[t].nranges;
         ++t;
     }
-    const int r0 = r * span;
-    arc_write_fused_range(b.it[t], t, r0, min(span, b.it[t].nranges - r0), keys, ws, ckey, rowlist, slotmap, dyn);
+    arc_write_fused_range(b.it[t], t, r, keys, ws, ckey, rowlist, slotmap, dyn);
 }
 
 struct KeysGrid {
@@ -3088,7 +3083,7 @@ DecodeRide<T> make_ride(const RideArgs* ra) {
 }
 
 template <typename T, int EF>
-int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int span, int nsm, const uint32_t* ckey, const T* sketch,
+int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int nsm, const uint32_t* ckey, const T* sketch,
                        int32_t ws, int32_t* rowlist, int32_t* slotmap, DecodeRide<T> dr, VDrawJob bj, size_t shm,
                        hipStream_t st) {
     if (shm > 48 * 1024) {
@@ -3097,7 +3092,7 @@ int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int span, int n
         if (ok != hipSuccess) return (int)ok;
     }
     launch_job_kernel(&k_arc_write_fused<T, EF>, dim3(nflat + nsm + dr.n + bj.n), dim3(kFuseNT), shm, st,
-                      (const MBatch*)(p->d_large_batches + bi), nflat, span, (const uint32_t*)p->d_keys, p->d_mws, ckey,
+                      (const MBatch*)(p->d_large_batches + bi), nflat, (const uint32_t*)p->d_keys, p->d_mws, ckey,
                       (const SegDev*)p->d_segs, (const int32_t*)p->d_small, sketch, (int)p->r, make_scale(ws),
                       rowlist, slotmap, dr, bj);
     return (int)hipGetLastError();
@@ -3182,18 +3177,14 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         constexpr bool fuse_ok = ARCTOPK_FUSED_WRITE != 0;  // build-time A/B switch
         // ... and only while every write block is resident at once: each one carries a refine,
         // so a second round of blocks costs more than the refine launch it saves (28 x [512,
-        // 512, 3, 3] as 896 one-range blocks: select 63 -> 74 us).  Blocks take spans of
-        // consecutive ranges instead, as many as keep the grid within kFuseMaxBlocks.
-        int nranges = 0;
-        for (int i = 0; i < b.cnt; ++i) nranges += b.it[i].nranges;
-        const int room = kFuseMaxBlocks - nsm - bj.n;
-        const int span = room > 0 ? std::max(1, (nranges + room - 1) / room) : kFuseMaxSpan + 1;
+        // 512, 3, 3] as 896 one-range blocks: select 63 -> 74 us; spans of several ranges per
+        // block measured slower still, rounds 3 and 4), so larger batches take the refine launch
         int nflat = 0;
-        for (int i = 0; i < b.cnt; ++i) nflat += (b.it[i].nranges + span - 1) / span;
+        for (int i = 0; i < b.cnt; ++i) nflat += b.it[i].nranges;
         // The small selects sharing the launch run as 256-thread blocks: only when none has
         // more than 4,096 rows (1,024-thread blocks select 8 K-row segments faster than these
         // write blocks finish: ResNet-18's third DDP bucket measured 250 -> 241 GB/s fused)
-        if (fuse_ok && maxn <= kFuseMaxRows && span <= kFuseMaxSpan && nflat + nsm + bj.n <= kFuseMaxBlocks &&
+        if (fuse_ok && maxn <= kFuseMaxRows && nflat + nsm + bj.n <= kFuseMaxBlocks &&
             (nsm == 0 || p->small_lds <= 4096 * 4 + 16)) {
             size_t shm = std::max<size_t>((size_t)kFuseCap * 4, nsm ? (size_t)p->small_lds : 0);
             // the deferred decode rides in the last batch's launch (its blocks come after the
@@ -3203,9 +3194,9 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
             const DecodeRide<T> dr = make_ride<T>(take ? ride : nullptr);
             if (take) shm = std::max<size_t>(shm, (size_t)ride->rp->dec_lds_bytes);
             e = take && ride->ef == ARCTOPK_EF21
-                    ? launch_write_fused<T, ARCTOPK_EF21>(p, bi, nflat, span, nsm, ckey, sketch, ws, rowlist, slotmap, dr,
+                    ? launch_write_fused<T, ARCTOPK_EF21>(p, bi, nflat, nsm, ckey, sketch, ws, rowlist, slotmap, dr,
                                                           bj, shm, st)
-                    : launch_write_fused<T, ARCTOPK_EF_NONE>(p, bi, nflat, span, nsm, ckey, sketch, ws, rowlist, slotmap,
+                    : launch_write_fused<T, ARCTOPK_EF_NONE>(p, bi, nflat, nsm, ckey, sketch, ws, rowlist, slotmap,
                                                              dr, bj, shm, st);
             if (e) return e;
             if (bi == 0) *drawn = true;

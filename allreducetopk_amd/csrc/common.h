@@ -39,11 +39,6 @@
 #ifndef ARCTOPK_FUSE_MAX_ROWS
 #define ARCTOPK_FUSE_MAX_ROWS 262144   // largest item whose refine runs in the write blocks
 #endif
-#ifndef ARCTOPK_FUSE_MAX_SPAN
-#define ARCTOPK_FUSE_MAX_SPAN 1        // most ranges per fused write block (A/B: 8 measured
-                                       // slower on 28 x [512,512,3,3] 738 -> 695 GB/s and on
-                                       // the ResNet-50 mix with 1 M-row items 358 -> 256)
-#endif
 #ifndef ARCTOPK_QUAD_DEC
 #define ARCTOPK_QUAD_DEC 1             // short-row (4 <= m < 256) fp32 decode: lane per output quad
 #endif                                 // (0: the chunk composed in an LDS tile)

@@ -221,6 +221,16 @@ int arctopk_comm_init_callback(arctopk_allreduce_fn fn, void* ctx, int32_t nrank
  */
 int arctopk_comm_init_wire(int32_t emul_ranks, double busbw_gbs, double latency_us, int32_t blocks,
                            int32_t device, arctopk_comm** out);
+/*
+ * CU partition for compute/communication overlap: a stream whose kernels
+ * run only on `reserved_cus` of the device's CUs (side = 1: the exchange stream the packed
+ * all-reduce is issued on) or only on the others (side = 0: the stream the codec's kernels run
+ * on), so that the collective's workgroups are never queued behind a codec grid that holds every
+ * CU.  The reserved CUs are the top `reserved_cus` mask bits (the driver deals mask bits out to
+ * the XCDs round robin, so they spread over all eight).  Destroy with arctopk_stream_destroy.
+ */
+int arctopk_stream_create_partition(int32_t device, int32_t reserved_cus, int32_t side, void** stream);
+int arctopk_stream_destroy(void* stream);
 int arctopk_comm_destroy(arctopk_comm* comm);
 int arctopk_comm_size(const arctopk_comm* comm);
 /* in-place SUM all-reduce of `count` elements (ARCTOPK_F32 / ARCTOPK_BF16), stream-ordered */
