@@ -362,6 +362,13 @@ class GroupTopKState(HookState):
         # collective's workgroups never wait for CUs held by an encode grid.  0: one pool.
         self.exchange_cus = int(os.environ.get("ARCTOPK_XCU", "0"))
         self._partition = None
+        # Codec pipelining at world size 1: with deferred decodes, bucket
+        # b's kernels run on codec stream b % codec_streams (event-ordered after the caller's
+        # stream), so bucket b+1's HBM-bound encode runs beside bucket b's latency-bound
+        # multi-block select; the backward's last bucket joins every codec stream back into
+        # the caller's.  0 or 1: the caller's stream only.
+        self.codec_streams = int(os.environ.get("ARCTOPK_CODEC_STREAMS", "0"))
+        self._pipe = None
         # Sketch all-reduces on a communicator of their own ("separate") or on the packed
         # values' communicator ("shared": a sketch then queues behind the previous bucket's
         # packed all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
@@ -475,17 +482,31 @@ class GroupTopKState(HookState):
         """Enqueue deferred decodes in call order (each on the stream of its call) and
         complete their Futures: all of them, or up to and including `upto`'s.  The hook does
         this itself in later calls; a Python wait()/value() on such a Future does it too."""
-        part, used = self._partition, False
+        part, pipe, used, piped = self._partition, self._pipe, False, False
         while self._x_pend:
             plan, fut, marks, t, sid, _keep = self._x_pend.pop(0)
             N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
             used = used or (part is not None and sid == part.cs)
+            piped = piped or (pipe is not None and sid in pipe.raw)
             fut.set_result(t)
             if fut is upto:
                 break
-        if used:  # decodes enqueued on the codec's CU partition: the caller's stream follows them
+        # decodes enqueued on the codec's CU partition or codec streams: the caller's stream
+        # follows them
+        if used:
             part.join(_current_raw_stream(part.dix))
+        if piped:
+            pipe.join_all(_current_raw_stream(pipe.dix))
         self._raise_if_comm_failed()
+
+    def _pipe_for(self, dev) -> "_Pipe":
+        dix = torch.device(dev).index or 0
+        p = self._pipe
+        if p is None or p.dix != dix or len(p.raw) != self.codec_streams:
+            if self._x_pend:
+                self.flush_exchange()
+            p = self._pipe = _Pipe(dix, self.codec_streams)
+        return p
 
     def _partition_for(self, dev) -> "_Partition":
         dix = torch.device(dev).index or 0
@@ -705,6 +726,29 @@ class _Partition:
                     L.arctopk_stream_destroy(h)
                 except Exception:  # interpreter shutdown
                     pass
+
+
+class _Pipe:
+    """Codec streams of the pipelined world-size-1 path (GroupTopKState.codec_streams): bucket
+    b's kernels on stream b % n, entered after the caller's stream (enter); join_all makes the
+    caller's stream follow every codec stream."""
+
+    def __init__(self, dix: int, n: int):
+        dev = torch.device("cuda", dix)
+        self.dix = dix
+        self.ext = [torch.cuda.Stream(device=dev) for _ in range(n)]
+        self.raw = tuple(s.cuda_stream for s in self.ext)
+        self._in = N.DeviceEvent()
+        self._out = [N.DeviceEvent() for _ in range(n)]
+
+    def enter(self, caller: int, i: int) -> None:
+        self._in.record(caller)
+        self._in.wait(self.raw[i])
+
+    def join_all(self, caller: int) -> None:
+        for s, ev in zip(self.raw, self._out):
+            ev.record(s)
+            ev.wait(caller)
 
 
 def _order_after_exchange(state, dev) -> None:
@@ -980,7 +1024,19 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         comms = world_size > 1 or state.force_exchange or state.emulate_wire is not None
         sk = pk = None
         tstream = torch.cuda.current_stream(dev)
-        part = caller = None
+        part = pipe = caller = None
+        # deferred except for the last bucket of a backward (nothing follows it), which then
+        # finishes every earlier deferred decode: nothing is left in flight when it returns
+        dd = state.defer_decode
+        if dd is None:  # DDP's own buckets (or a DDP-registered state): Futures waited at finalize
+            dd = isinstance(bucket, dist.GradBucket) or getattr(state, "_ddp_registered", False)
+        defer = dd and state.async_exchange and not bucket.is_last()
+        if not comms and dd and state.async_exchange and state.codec_streams > 1:
+            # the codec of bucket b on codec stream b % n, after the caller's stream
+            pipe = state._pipe_for(dev)
+            i_ = b % len(pipe.raw)
+            caller, sid, tstream = sid, pipe.raw[i_], pipe.ext[i_]
+            pipe.enter(caller, i_)
         if comms:
             sk, pk = state._exchange_comms(group, dev)  # (a failed communicator: the step returns its status)
             if plan.comm_registered is not pk:
@@ -995,20 +1051,16 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         vslot, vptr, draw, nplan, nseed = -1, None, False, None, 0
         if device_v:
             draw = _claim_projections(state, plan, seed, sid, dev)
-            nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
+            if pipe is None:  # (pipelined: the next bucket's V is read on another stream)
+                nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
         else:
             vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, tstream)
             vptr = V.data_ptr()
-        # deferred except for the last bucket of a backward (nothing follows it), which then
-        # finishes every earlier deferred decode: nothing is left in flight when it returns
-        dd = state.defer_decode
-        if dd is None:  # DDP's own buckets (or a DDP-registered state): Futures waited at finalize
-            dd = isinstance(bucket, dist.GradBucket) or getattr(state, "_ddp_registered", False)
-        defer = dd and state.async_exchange and not bucket.is_last()
         pend = state._x_pend
         # finish first: a caller that skipped buckets, or one whose stream changed since a
         # pending step (its decode is enqueued on that step's own stream)
-        if any(e_[0] is plan or e_[4] != sid for e_ in pend):
+        ok_streams = pipe.raw if pipe is not None else (sid,)
+        if any(e_[0] is plan or e_[4] not in ok_streams for e_ in pend):
             state.flush_exchange()
         # the decode riding in this call's select launch: the previous bucket's without
         # collectives, the one before it with them (its all-reduce has had a whole call to
@@ -1033,7 +1085,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                                       int(err_in), int(draw), seed,
                                       nplan.handle if nplan is not None else None, nseed,
                                       sk.handle if comms else None, pk.handle if comms else None, sid,
-                                      ars.cuda_stream if ars is not None else None, int(defer),
+                                      ars.cuda_stream if ars is not None else None,
+                                      (2 if pipe is not None else 1) if defer else 0,
                                       ride[0].handle if ride is not None else None,
                                       ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
                                       vptr, marks)
@@ -1050,6 +1103,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             plan.projection_consumed(vslot, tstream)
         if part is not None:
             part.join(caller)
+        if pipe is not None and not defer:  # the backward's last bucket: every codec stream
+            pipe.join_all(caller)
         _ht("native_step")
         state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
         state.maybe_increase_iter(bucket)
