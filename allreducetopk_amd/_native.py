@@ -120,8 +120,6 @@ _SIGS = {
     "arctopk_event_record": (c_int32, [c_void_p, c_void_p]),
     "arctopk_event_wait": (c_int32, [c_void_p, c_void_p]),
     "arctopk_event_query": (c_int32, [c_void_p]),
-    "arctopk_stream_create_partition": (c_int32, [c_int32, c_int32, c_int32, POINTER(c_void_p)]),
-    "arctopk_stream_destroy": (c_int32, [c_void_p]),
     "arctopk_event_create_timed": (c_int32, [POINTER(c_void_p)]),
     "arctopk_event_elapsed_ms": (c_int32, [POINTER(ctypes.c_float), c_void_p, c_void_p]),
     "arctopk_round_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),

@@ -356,19 +356,6 @@ class GroupTopKState(HookState):
         # dict(ranks=8, busbw_gbs=350)) instead of real ones; with force_exchange at world
         # size 1 the step then runs beside the local cost of an N-rank ring
         self.emulate_wire = None
-        # CU partition of the exchange path: > 0 runs the packed
-        # all-reduces on a stream restricted to that many CUs and the codec's kernels on a
-        # stream restricted to the others (event-ordered with the caller's stream), so the
-        # collective's workgroups never wait for CUs held by an encode grid.  0: one pool.
-        self.exchange_cus = int(os.environ.get("ARCTOPK_XCU", "0"))
-        self._partition = None
-        # Codec pipelining at world size 1: with deferred decodes, bucket
-        # b's kernels run on codec stream b % codec_streams (event-ordered after the caller's
-        # stream), so bucket b+1's HBM-bound encode runs beside bucket b's latency-bound
-        # multi-block select; the backward's last bucket joins every codec stream back into
-        # the caller's.  0 or 1: the caller's stream only.
-        self.codec_streams = int(os.environ.get("ARCTOPK_CODEC_STREAMS", "0"))
-        self._pipe = None
         # Sketch all-reduces on a communicator of their own ("separate") or on the packed
         # values' communicator ("shared": a sketch then queues behind the previous bucket's
         # packed all-reduce).  DESIGN.md section 6 discusses the two-communicator ordering.
@@ -482,40 +469,13 @@ class GroupTopKState(HookState):
         """Enqueue deferred decodes in call order (each on the stream of its call) and
         complete their Futures: all of them, or up to and including `upto`'s.  The hook does
         this itself in later calls; a Python wait()/value() on such a Future does it too."""
-        part, pipe, used, piped = self._partition, self._pipe, False, False
         while self._x_pend:
             plan, fut, marks, t, sid, _keep = self._x_pend.pop(0)
             N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
-            used = used or (part is not None and sid == part.cs)
-            piped = piped or (pipe is not None and sid in pipe.raw)
             fut.set_result(t)
             if fut is upto:
                 break
-        # decodes enqueued on the codec's CU partition or codec streams: the caller's stream
-        # follows them
-        if used:
-            part.join(_current_raw_stream(part.dix))
-        if piped:
-            pipe.join_all(_current_raw_stream(pipe.dix))
         self._raise_if_comm_failed()
-
-    def _pipe_for(self, dev) -> "_Pipe":
-        dix = torch.device(dev).index or 0
-        p = self._pipe
-        if p is None or p.dix != dix or len(p.raw) != self.codec_streams:
-            if self._x_pend:
-                self.flush_exchange()
-            p = self._pipe = _Pipe(dix, self.codec_streams)
-        return p
-
-    def _partition_for(self, dev) -> "_Partition":
-        dix = torch.device(dev).index or 0
-        p = self._partition
-        if p is None or p.dix != dix or p.cus != self.exchange_cus:
-            if self._x_pend:
-                self.flush_exchange()
-            p = self._partition = _Partition(dix, self.exchange_cus)
-        return p
 
     def state_dict(self) -> dict:
         self.flush_exchange()  # the deferred decode writes gE (EF21)
@@ -687,68 +647,6 @@ class ExchangeFuture(torch.futures.Future):
         if not self.done():
             self._arctopk_state.flush_exchange(upto=self)
         return super().value()
-
-
-class _Partition:
-    """The exchange path's CU partition (GroupTopKState.exchange_cus): the codec's stream `cs`
-    (every CU but the reserved ones) and the exchange stream `xs` (the reserved CUs),
-    arctopk_stream_create_partition.  A call enters with enter(caller) (cs follows the caller's
-    stream) and leaves with join(caller) (the caller's stream follows cs)."""
-
-    def __init__(self, dix: int, cus: int):
-        L = N.lib()
-        self.dix, self.cus = dix, cus
-        hs = []
-        for side in (0, 1):
-            h = N.ctypes.c_void_p()
-            N.check(L.arctopk_stream_create_partition(dix, cus, side, N.ctypes.byref(h)),
-                    "arctopk_stream_create_partition")
-            hs.append(h.value)
-        self.cs, self.xs = hs
-        dev = torch.device("cuda", dix)
-        self.ext = torch.cuda.ExternalStream(self.cs, device=dev)
-        self.xext = torch.cuda.ExternalStream(self.xs, device=dev)
-        self._in, self._out = N.DeviceEvent(), N.DeviceEvent()
-
-    def enter(self, caller: int) -> None:
-        self._in.record(caller)
-        self._in.wait(self.cs)
-
-    def join(self, caller: int) -> None:
-        self._out.record(self.cs)
-        self._out.wait(caller)
-
-    def __del__(self):
-        L = N._lib
-        for h in (getattr(self, "cs", None), getattr(self, "xs", None)):
-            if h and L is not None:
-                try:
-                    L.arctopk_stream_destroy(h)
-                except Exception:  # interpreter shutdown
-                    pass
-
-
-class _Pipe:
-    """Codec streams of the pipelined world-size-1 path (GroupTopKState.codec_streams): bucket
-    b's kernels on stream b % n, entered after the caller's stream (enter); join_all makes the
-    caller's stream follow every codec stream."""
-
-    def __init__(self, dix: int, n: int):
-        dev = torch.device("cuda", dix)
-        self.dix = dix
-        self.ext = [torch.cuda.Stream(device=dev) for _ in range(n)]
-        self.raw = tuple(s.cuda_stream for s in self.ext)
-        self._in = N.DeviceEvent()
-        self._out = [N.DeviceEvent() for _ in range(n)]
-
-    def enter(self, caller: int, i: int) -> None:
-        self._in.record(caller)
-        self._in.wait(self.raw[i])
-
-    def join_all(self, caller: int) -> None:
-        for s, ev in zip(self.raw, self._out):
-            ev.record(s)
-            ev.wait(caller)
 
 
 def _order_after_exchange(state, dev) -> None:
@@ -1023,44 +921,29 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         # communicators), and earlier buckets' deferred decodes
         comms = world_size > 1 or state.force_exchange or state.emulate_wire is not None
         sk = pk = None
-        tstream = torch.cuda.current_stream(dev)
-        part = pipe = caller = None
-        # deferred except for the last bucket of a backward (nothing follows it), which then
-        # finishes every earlier deferred decode: nothing is left in flight when it returns
-        dd = state.defer_decode
-        if dd is None:  # DDP's own buckets (or a DDP-registered state): Futures waited at finalize
-            dd = isinstance(bucket, dist.GradBucket) or getattr(state, "_ddp_registered", False)
-        defer = dd and state.async_exchange and not bucket.is_last()
-        if not comms and dd and state.async_exchange and state.codec_streams > 1:
-            # the codec of bucket b on codec stream b % n, after the caller's stream
-            pipe = state._pipe_for(dev)
-            i_ = b % len(pipe.raw)
-            caller, sid, tstream = sid, pipe.raw[i_], pipe.ext[i_]
-            pipe.enter(caller, i_)
         if comms:
             sk, pk = state._exchange_comms(group, dev)  # (a failed communicator: the step returns its status)
             if plan.comm_registered is not pk:
                 sk.register(plan.sketch)
                 pk.register(plan.packed)
                 plan.comm_registered = pk
-            if state.exchange_cus > 0 and state.async_exchange:
-                # the codec's kernels on the unreserved CUs, ordered after the caller's stream
-                part = state._partition_for(dev)
-                caller, sid, tstream = sid, part.cs, part.ext
-                part.enter(caller)
         vslot, vptr, draw, nplan, nseed = -1, None, False, None, 0
         if device_v:
             draw = _claim_projections(state, plan, seed, sid, dev)
-            if pipe is None:  # (pipelined: the next bucket's V is read on another stream)
-                nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
+            nplan, nseed = _predraw_target(state, b, dtype, dev, sid)
         else:
-            vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, tstream)
+            vslot, V = _host_projections(state, plan, bucket, seed, dtype, dev, torch.cuda.current_stream(dev))
             vptr = V.data_ptr()
+        # deferred except for the last bucket of a backward (nothing follows it), which then
+        # finishes every earlier deferred decode: nothing is left in flight when it returns
+        dd = state.defer_decode
+        if dd is None:  # DDP's own buckets (or a DDP-registered state): Futures waited at finalize
+            dd = isinstance(bucket, dist.GradBucket) or getattr(state, "_ddp_registered", False)
+        defer = dd and state.async_exchange and not bucket.is_last()
         pend = state._x_pend
         # finish first: a caller that skipped buckets, or one whose stream changed since a
         # pending step (its decode is enqueued on that step's own stream)
-        ok_streams = pipe.raw if pipe is not None else (sid,)
-        if any(e_[0] is plan or e_[4] not in ok_streams for e_ in pend):
+        if any(e_[0] is plan or e_[4] != sid for e_ in pend):
             state.flush_exchange()
         # the decode riding in this call's select launch: the previous bucket's without
         # collectives, the one before it with them (its all-reduce has had a whole call to
@@ -1072,7 +955,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             pend.clear()
         ars = None
         if defer and comms:
-            ars = part.xext if part is not None else state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
+            ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
             if pk.kind == "callback" and ars.cuda_stream not in pk._streams:
                 pk.known_stream(ars)
         marks = _call_marks(state, _EXCHANGE_MARKS)
@@ -1085,8 +968,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                                       int(err_in), int(draw), seed,
                                       nplan.handle if nplan is not None else None, nseed,
                                       sk.handle if comms else None, pk.handle if comms else None, sid,
-                                      ars.cuda_stream if ars is not None else None,
-                                      (2 if pipe is not None else 1) if defer else 0,
+                                      ars.cuda_stream if ars is not None else None, int(defer),
                                       ride[0].handle if ride is not None else None,
                                       ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
                                       vptr, marks)
@@ -1100,11 +982,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         if nplan is not None:
             nplan.v_drawn, nplan.v_stream = nseed, sid
         if vslot >= 0:
-            plan.projection_consumed(vslot, tstream)
-        if part is not None:
-            part.join(caller)
-        if pipe is not None and not defer:  # the backward's last bucket: every codec stream
-            pipe.join_all(caller)
+            plan.projection_consumed(vslot, torch.cuda.current_stream(dev))
         _ht("native_step")
         state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
         state.maybe_increase_iter(bucket)

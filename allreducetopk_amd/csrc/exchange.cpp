@@ -462,12 +462,9 @@ int ensure_event(void** ev, unsigned flags) {
 // all-reduce (a stream wait only when the host does not already see it complete).
 namespace {
 int wait_ar(arctopk_plan* p, hipStream_t st) {
-    // 1: after the all-reduce on the exchange stream; 3: after the pack, which may have run
-    // on another stream (defer = 2); 2: same stream, nothing to wait for
-    if (p->x_deferred != 1 && p->x_deferred != 3) return 0;
-    hipEvent_t ev = (hipEvent_t)(p->x_deferred == 1 ? p->x_ev_ar : p->x_ev_packed);
-    const hipError_t q = hipEventQuery(ev);
-    if (q == hipErrorNotReady) return (int)hipStreamWaitEvent(st, ev, 0);
+    if (p->x_deferred != 1) return 0;  // 2: no all-reduce on another stream
+    const hipError_t q = hipEventQuery((hipEvent_t)p->x_ev_ar);
+    if (q == hipErrorNotReady) return (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
     return q == hipSuccess ? 0 : (int)q;
 }
 }  // namespace
@@ -543,14 +540,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // caller's stream, where one idles the GPU several us): the all-reduce stream waits for it,
     // and the watchdog sees the sketch all-reduce before it complete
     const bool async_ar = defer && packed_comm;
-    // defer = 2 without collectives: the decode may be enqueued on another stream (a later
-    // call's), so the pack completes x_ev_packed for it to wait on
-    const bool xstream = defer == 2 && !packed_comm;
-    if (xstream) {
-        if ((e = ensure_event(&p->x_ev_packed, 0))) return e;
-        e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
-                                 p->x_ev_packed);
-    } else if (packed_comm) {
+    if (packed_comm) {
         if ((e = ensure_event(&p->x_ev_packed, 0)) ||
             (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
             return e;
@@ -575,7 +565,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         if (finish[i] && finish[i] != p) e = arctopk_exchange_finish(finish[i], stream, finish_marks ? finish_marks[i] : nullptr);
     if (e) return e;
     if (defer) {
-        p->x_deferred = async_ar ? 1 : xstream ? 3 : 2;
+        p->x_deferred = async_ar ? 1 : 2;
         p->x_bucket = bucket;
         p->x_gerr = gerr;
         p->x_ef = ef;

@@ -465,34 +465,6 @@ extern "C" int arctopk_event_wait(void* stream, void* event) {
     return (int)hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0);
 }
 
-extern "C" int arctopk_stream_create_partition(int32_t device, int32_t reserved_cus, int32_t side,
-                                               void** stream) {
-    if (!stream || (side != 0 && side != 1)) return ARCTOPK_EINVAL;
-    *stream = nullptr;
-    int prev = 0, ncu = 0;
-    hipError_t st = hipGetDevice(&prev);
-    if (st != hipSuccess) return (int)st;
-    if ((st = hipSetDevice(device)) != hipSuccess) return (int)st;
-    st = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-    if (st == hipSuccess && (reserved_cus <= 0 || reserved_cus >= ncu)) st = hipErrorInvalidValue;
-    if (st == hipSuccess) {
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; ++i) {
-            const bool reserved = i >= ncu - reserved_cus;
-            if (reserved == (side == 1)) mask[i / 32] |= 1u << (i % 32);
-        }
-        hipStream_t s = nullptr;
-        st = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
-        if (st == hipSuccess) *stream = (void*)s;
-    }
-    (void)hipSetDevice(prev);
-    return st == hipErrorInvalidValue ? ARCTOPK_EINVAL : (int)st;
-}
-
-extern "C" int arctopk_stream_destroy(void* stream) {
-    return stream ? (int)hipStreamDestroy((hipStream_t)stream) : 0;
-}
-
 extern "C" int arctopk_event_query(void* event) {
     if (!event) return ARCTOPK_EINVAL;
     const hipError_t st = hipEventQuery((hipEvent_t)event);

@@ -195,9 +195,6 @@ def main():
     ap.add_argument("--wire-ranks", type=int, default=8)
     ap.add_argument("--wire-blocks", type=int, default=32,
                     help="workgroups of the emulated collective (its CU footprint)")
-    ap.add_argument("--wire-xcu", type=int, nargs="*", default=[0],
-                    help="emulated-wire lines with the exchange's CU partition (GroupTopKState."
-                         "exchange_cus) set to each of these (0: one CU pool)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -305,10 +302,8 @@ def main():
     wire = []
     if (world == 1 and args.hook == "arc" and not args.host_staged and not args.force_exchange
             and args.backend == "nccl"):
-        xcu0 = st.exchange_cus
-        for bw, xcu in [(b_, x_) for b_ in (args.wire_busbw or []) for x_ in (args.wire_xcu or [0])]:
+        for bw in args.wire_busbw or []:
             st.reset_exchange_comms()
-            st.exchange_cus = xcu
             st.emulate_wire = dict(ranks=args.wire_ranks, busbw_gbs=bw, latency_us=15.0, blocks=args.wire_blocks)
             for _ in range(2):
                 step()
@@ -320,12 +315,11 @@ def main():
             fe = time.perf_counter() - t1
             v = args.steps * bytes_per_step / fe / 1e9
             wire.append({"busbw_gbs": bw, "emulated_ranks": args.wire_ranks, "blocks": args.wire_blocks,
-                         "latency_us": 15.0, "exchange_cus": xcu, "per_gpu_value": round(v, 2),
+                         "latency_us": 15.0, "per_gpu_value": round(v, 2),
                          "implied_aggregate": round(args.wire_ranks * v, 2),
                          "ms_per_bucket": round(fe / args.steps / nb * 1e3, 4)})
         st.reset_exchange_comms()
         st.emulate_wire = None
-        st.exchange_cus = xcu0
 
     phase_ms = {}
     light = {}

@@ -221,16 +221,6 @@ int arctopk_comm_init_callback(arctopk_allreduce_fn fn, void* ctx, int32_t nrank
  */
 int arctopk_comm_init_wire(int32_t emul_ranks, double busbw_gbs, double latency_us, int32_t blocks,
                            int32_t device, arctopk_comm** out);
-/*
- * CU partition for compute/communication overlap: a stream whose kernels
- * run only on `reserved_cus` of the device's CUs (side = 1: the exchange stream the packed
- * all-reduce is issued on) or only on the others (side = 0: the stream the codec's kernels run
- * on), so that the collective's workgroups are never queued behind a codec grid that holds every
- * CU.  The reserved CUs are the top `reserved_cus` mask bits (the driver deals mask bits out to
- * the XCDs round robin, so they spread over all eight).  Destroy with arctopk_stream_destroy.
- */
-int arctopk_stream_create_partition(int32_t device, int32_t reserved_cus, int32_t side, void** stream);
-int arctopk_stream_destroy(void* stream);
 int arctopk_comm_destroy(arctopk_comm* comm);
 int arctopk_comm_size(const arctopk_comm* comm);
 /* in-place SUM all-reduce of `count` elements (ARCTOPK_F32 / ARCTOPK_BF16), stream-ordered */
@@ -245,10 +235,7 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   later step's `ride` / `finish`); with communicators its packed all-reduce runs on
  *   `ar_stream` after the pack kernel, which completes the event that stream waits for (no
  *   marker packet on `stream`), so the caller's stream encodes the next bucket while these
- *   packed values are on the wire.  defer = 2: as 1, and the deferred decode may be enqueued
- *   on another stream than this step's (pipelined codec streams): without collectives the
- *   pack kernel then completes an event that decode waits for.  defer = 0: all-reduce and
- *   decode inline on `stream`.
+ *   packed values are on the wire.  defer = 0: all-reduce and decode inline on `stream`.
  * ride: an earlier step's deferred decode, run inside this step's select launch (extra blocks of
  *   the single-block select launch, or of the multi-block select's last, fused write launch: the
  *   select's latency then hides behind the decode's HBM stream), else right after the select;

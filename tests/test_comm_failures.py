@@ -119,7 +119,3 @@ def test_comm_status_abort_and_bad_wire_params_without_gpu():
     assert L.arctopk_comm_init_wire(8, 350.0, 10.0, 32, 0, ctypes.byref(w)) == 0
     assert L.arctopk_comm_size(w) == 1  # results of a one-rank all-reduce
     assert L.arctopk_comm_destroy(w) == 0
-    s = ctypes.c_void_p()
-    assert L.arctopk_stream_create_partition(0, 32, 2, ctypes.byref(s)) == 1001  # side is 0 or 1
-    assert L.arctopk_stream_create_partition(0, 32, 0, None) == 1001
-    assert L.arctopk_stream_destroy(None) == 0

@@ -131,28 +131,3 @@ def test_emulated_wire_leaves_results_unchanged(ef):
     for i, what in enumerate(("output", "E", "gE")):
         for b in outs[True][i]:
             assert_bitwise(outs[False][i][b], outs[True][i][b], f"bucket {b} {what}, wire vs RCCL")
-
-
-@pytest.mark.parametrize("ef", ["ef14", "ef21"])
-def test_cu_partition_leaves_results_unchanged(ef):
-    """exchange_cus > 0 (the codec on a CU-masked stream, the packed all-reduces on the
-    reserved CUs, event-ordered with the caller's stream): the bits of the one-pool run,
-    waited on by DDP-style Futures and by the Python wait() of a deferred Future."""
-    ensure_group("nccl")
-    outs = {}
-    for cus in (0, 32):
-        st = _state(force_exchange=True, defer=True, ef=ef, seed=5)
-        st.exchange_cus = cus
-        for step in range(3):
-            futs, bufs = _backward(st, step)
-            futs[0].wait()  # flushes the deferred decodes from Python (the join path)
-            for f in futs:
-                f.wait()
-        torch.cuda.synchronize()
-        assert (st._partition is not None) == (cus > 0)
-        outs[cus] = ({b: t.cpu() for b, t in bufs.items()},
-                     {b: e.cpu() for b, e in st.error_dict.items()},
-                     {b: e.cpu() for b, e in st.global_error_dict.items()})
-    for i, what in enumerate(("output", "E", "gE")):
-        for b in outs[0][i]:
-            assert_bitwise(outs[32][i][b], outs[0][i][b], f"bucket {b} {what}, CU partition vs one pool")
