@@ -1270,6 +1270,9 @@ constexpr int kRefineThreads = 1024;
 #define ARCTOPK_REFINE_PRE 64  // tuning switch (A/B builds): candidates per range loaded up front, 64 or 128
 #endif
 constexpr int kRefinePre = ARCTOPK_REFINE_PRE;
+#ifndef ARCTOPK_REFINE_UT
+#define ARCTOPK_REFINE_UT 4  // tuning switch (A/B builds): tail candidates loaded per thread and round
+#endif
 static_assert(kRefineThreads == kMMaxRanges, "one range per thread in the offset scan");
 __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspace* ws,
                                                 const uint32_t* __restrict__ ckey,
@@ -1362,7 +1365,7 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
                 }
             }
         }
-        constexpr int UT = 4;
+        constexpr int UT = ARCTOPK_REFINE_UT;
         for (uint32_t p0 = 0; p0 < ntail; p0 += (uint32_t)NT * UT) {
             uint32_t kv[UT], dst[UT];
 #pragma unroll
@@ -2490,19 +2493,36 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
         const int np = nsel * m;
         const T* pkc = pk + (int64_t)f0 * m;
         int32_t* lmap = reinterpret_cast<int32_t*>(dlds);
-        float* lpk = dlds + nr;
+        float* lpk = dlds + ((nr + 3) & ~3);  // (16-B aligned: quad stores)
         int32_t sv[UR];
-        float pv[UP];
+        [[maybe_unused]] float pv[UP];
+        constexpr int UQ = UP / 4 + 1;  // quads per thread: the range plus up to 3 lead values
+        [[maybe_unused]] float4 pq[UQ];
         [[maybe_unused]] float4 gq[UG];
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
             const int r = (int)threadIdx.x + u * 256;
             sv[u] = r < nr ? sm[r] : -1;
         }
+        // fp32: the packed range as the 16-B quads of the (16-B aligned) packed buffer that
+        // cover it -- a quarter of the load instructions; `lead` values of the first quad
+        // precede the range (the buffer is a whole number of quads: no read past its end)
+        constexpr bool vecp = sizeof(T) == 4 && ARCTOPK_SHORT3_VEC;
+        const int lead = vecp ? (int)((s.packed_off + (int64_t)f0 * m) & 3) : 0;
+        const int nq = (np + lead + 3) >> 2;
+        if constexpr (vecp) {
+            const float4* pq0 = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pkc) - lead);
 #pragma unroll
-        for (int u = 0; u < UP; ++u) {
-            const int p = (int)threadIdx.x + u * 256;
-            pv[u] = p < np ? to_f(pkc[p]) : 0.f;
+            for (int u = 0; u < UQ; ++u) {
+                const int q = (int)threadIdx.x + u * 256;
+                pq[u] = q < nq ? pq0[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const int p = (int)threadIdx.x + u * 256;
+                pv[u] = p < np ? to_f(pkc[p]) : 0.f;
+            }
         }
         if constexpr (EF == ARCTOPK_EF21) {
 #pragma unroll
@@ -2522,10 +2542,19 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
             const int r = (int)threadIdx.x + u * 256;
             if (r < nr) lmap[r] = sv[u] >= 0 ? sv[u] - f0 : -1;
         }
+        if constexpr (vecp) {
+            float4* lq = reinterpret_cast<float4*>(lpk);  // lpk[lead + p]: packed value p
 #pragma unroll
-        for (int u = 0; u < UP; ++u) {
-            const int p = (int)threadIdx.x + u * 256;
-            if (p < np) lpk[p] = pv[u];
+            for (int u = 0; u < UQ; ++u) {
+                const int q = (int)threadIdx.x + u * 256;
+                if (q < nq) lq[q] = pq[u];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const int p = (int)threadIdx.x + u * 256;
+                if (p < np) lpk[p] = pv[u];
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -2542,7 +2571,7 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
                 const int sl = lmap[r];
                 sel[j] = sl >= 0 && sl < nsel && e + j < cnt;
                 any = any || sel[j];
-                float v = sel[j] ? mean1(lpk[sl * m + c]) : 0.f;
+                float v = sel[j] ? mean1(lpk[lead + sl * m + c]) : 0.f;
                 if constexpr (EF == ARCTOPK_EF21) {
                     const float g = j == 0 ? gq[u].x : j == 1 ? gq[u].y : j == 2 ? gq[u].z : gq[u].w;
                     v = sel[j] ? rnd<T>(g + v) : g + 0.f;

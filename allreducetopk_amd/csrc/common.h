@@ -73,6 +73,10 @@
 #ifndef ARCTOPK_SHORT3_CHUNK
 #define ARCTOPK_SHORT3_CHUNK 4096      // ... elements per chunk at most (LDS: 4 (m + 1) / m B each)
 #endif
+#ifndef ARCTOPK_SHORT3_VEC
+#define ARCTOPK_SHORT3_VEC 0           // tuning switch (A/B builds): 1 = the mode-3 decode loads its
+                                       // packed range (fp32) as 16-B quads
+#endif
 #ifndef ARCTOPK_ENC_TARGET_BLOCKS_E
 #define ARCTOPK_ENC_TARGET_BLOCKS_E 4096  // ... for the fp32 kernels that also stream E (large tensors)
 #endif

@@ -245,7 +245,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
             g.dchunk_rows = (int32_t)per;
             for (int64_t row = 0; row < s.n; row += per)
                 dec.push_back(Chunk{(int32_t)i, 3, row, std::min(per, s.n - row)});
-            dec_lds = std::max<int64_t>(dec_lds, (std::min(per, s.n) * (s.m + 1)) * 4);
+            dec_lds = std::max<int64_t>(dec_lds, (std::min(per, s.n) * (s.m + 1) + 12) * 4);  // + alignment, quad lead
         } else if (small_tile && dtype == ARCTOPK_F32 && ARCTOPK_QUAD_DEC) {
             // mode 2: lane per 16-B output quad, rows of whole chunks (no LDS tile)
             const int64_t per = std::max<int64_t>(1, (int64_t)ARCTOPK_QUAD_DEC_CHUNK / s.m);

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 4: parity of the vectorized mode-3 decode variant, A/B of decode / refine variants,
+# SQ counter passes of the short-row workloads on the product library.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r4g gpurun_out/ab
+rm -f gpurun_out/ab/summary.txt
+ARCTOPK_LIB=allreducetopk_amd/lib/var/libarctopk_vec3.so timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_arctopk.py -m gpu -q -k "conv3x3 or resnet18 or resnet50 or end_to_end or golden or bf16" --timeout 120 --timeout-method thread > gpurun_out/r4g/vec3_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/r4g/vec3_tests.log; [ $rc -eq 0 ] || exit $rc
+BENCH_ARGS="--workload resnet18_conv --steps 30" VARIANTS="vec3" bash scripts/gpu_ab_lib.sh || exit 1
+BENCH_ARGS="--workload resnet50_mixed --steps 30" VARIANTS="refut16 refpre128" bash scripts/gpu_ab_lib.sh || exit 1
+BENCH_ARGS="--workload resnet18_ddp --steps 30" VARIANTS="vec3 refut16" bash scripts/gpu_ab_lib.sh || exit 1
+bash scripts/gpu_r4counters.sh gpurun_out/r4g/pmc || exit 1
+echo done
