@@ -117,14 +117,10 @@ __device__ __forceinline__ float4 ef_combine4(float4 x, float4 e) {
 //                   into LDS, then one thread per row forms its R dot products.
 //  ENC_RAW        : 1-D tensors: the sketch is the (EF-applied) values themselves.
 template <typename T, int R, int EF, bool ERR_IN>
-__global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
-                                                const EncTile* __restrict__ tiles,
-                                                const T* __restrict__ G, T* __restrict__ E,
-                                                const T* __restrict__ V,
-                                                T* __restrict__ sketch,
-                                                float* __restrict__ part_buf) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const EncTile t = tiles[blockIdx.x];
+__device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, const EncTile t,
+                                            const T* __restrict__ G, T* __restrict__ E,
+                                            const T* __restrict__ V, T* __restrict__ sketch,
+                                            float* __restrict__ part_buf, float* __restrict__ lds) {
     const SegDev s = segs[t.seg];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -522,6 +518,31 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
 #pragma unroll
                 for (int j = 0; j < R; ++j) put(row * R + j, acc[j]);
             }
+        }
+    }
+}
+
+// One tile per block, or (ARCTOPK_ENC_GRID_CAP > 0, A/B switch) a grid of at most that many
+// blocks walking the tile table in strides: every block is dispatched at once, so a kernel of
+// another stream (a collective) is not queued behind thousands of encode blocks.
+#ifndef ARCTOPK_ENC_GRID_CAP
+#define ARCTOPK_ENC_GRID_CAP 0
+#endif
+constexpr int kEncGridCap = ARCTOPK_ENC_GRID_CAP;
+template <typename T, int R, int EF, bool ERR_IN>
+__global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
+                                                const EncTile* __restrict__ tiles, int ntiles,
+                                                const T* __restrict__ G, T* __restrict__ E,
+                                                const T* __restrict__ V,
+                                                T* __restrict__ sketch,
+                                                float* __restrict__ part_buf) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if constexpr (kEncGridCap == 0) {
+        encode_tile<T, R, EF, ERR_IN>(segs, tiles[blockIdx.x], G, E, V, sketch, part_buf, lds);
+    } else {
+        for (int i = (int)blockIdx.x; i < ntiles; i += (int)gridDim.x) {
+            encode_tile<T, R, EF, ERR_IN>(segs, tiles[i], G, E, V, sketch, part_buf, lds);
+            __syncthreads();  // the next tile restages LDS
         }
     }
 }
@@ -3024,18 +3045,19 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
                     hipStream_t st) {
     if (p->n_enc > 0) {
         const bool use_e = p->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
-        dim3 grid(use_e ? p->n_enc_e : p->n_enc), block(256);
+        const int nt = use_e ? p->n_enc_e : p->n_enc;
+        dim3 grid(kEncGridCap > 0 ? std::min(nt, kEncGridCap) : nt), block(256);
         const size_t lds = (size_t)p->enc_lds_bytes;
         const EncTile* tiles = use_e ? p->d_enc_e : p->d_enc;
         float* pb = p->d_part;
         if (ef == ARCTOPK_EF_NONE)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
         else if (ef == ARCTOPK_EF14 && err_in)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
         else if (ef == ARCTOPK_EF14)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
         else
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
         const int e = (int)hipGetLastError();
         if (e) return e;
     }
