@@ -440,6 +440,12 @@ extern "C" int arctopk_comm_allreduce(arctopk_comm* c, void* buf, int64_t count,
     return 0;
 }
 
+// flags of the pack kernel's stop event (A/B switch): 0 = a timing event with the default
+// (system-scope) release at the kernel's end
+#ifndef ARCTOPK_PACK_EV_FLAGS
+#define ARCTOPK_PACK_EV_FLAGS 0
+#endif
+
 namespace {
 
 inline int mark(void* const* marks, int i, hipStream_t st) {
@@ -541,7 +547,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // and the watchdog sees the sketch all-reduce before it complete
     const bool async_ar = defer && packed_comm;
     if (packed_comm) {
-        if ((e = ensure_event(&p->x_ev_packed, 0)) ||
+        if ((e = ensure_event(&p->x_ev_packed, ARCTOPK_PACK_EV_FLAGS)) ||
             (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
             return e;
         e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,

@@ -18,5 +18,15 @@ for lib in product cap512 cap768; do
   ARCTOPK_LIB=$L timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-phase-events --no-forced-exchange --wire-busbw 350 > gpurun_out/r4g/wire_$lib.log 2>&1 || { tail -5 gpurun_out/r4g/wire_$lib.log; exit 1; }
   tail -1 gpurun_out/r4g/wire_$lib.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$lib', d['value'], [(x['per_gpu_value'], x['ms_per_bucket']) for x in d['emulated_wire']])"
 done
+# the pack's stop event: default (system-scope release) vs device-scope release, forced exchange
+for w in resnet18_ddp headline; do
+  for rep in 1 2; do
+    for lib in product pkev pkev2; do
+      if [ "$lib" = product ]; then L=""; else L="allreducetopk_amd/lib/var/libarctopk_$lib.so"; fi
+      ARCTOPK_LIB=$L timeout -k 10 200 python3 bench.py --workload $w --force-exchange --steps 40 --no-cpu-baseline --no-phase-events --wire-busbw > gpurun_out/r4g/fx_${lib}_$w.log 2>&1 || { tail -5 gpurun_out/r4g/fx_${lib}_$w.log; exit 1; }
+      tail -1 gpurun_out/r4g/fx_${lib}_$w.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('forced $w $lib', d['value'], d['config'].get('hook_path'))"
+    done
+  done
+done
 bash scripts/gpu_r4counters.sh gpurun_out/r4g/pmc || exit 1
 echo done
