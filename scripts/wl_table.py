@@ -13,3 +13,23 @@ for line in open(path):
           f"{p.get('hook_device_total', 0) * 1e3:7.1f} {p.get('encode', 0) * 1e3:6.1f} "
           f"{p.get('select', 0) * 1e3:6.1f} {p.get('pack', 0) * 1e3:6.1f} {p.get('decode', 0) * 1e3:6.1f} "
           f"{r.get('achieved', 0) / 1e3:7.2f} {r.get('hook', {}).get('frac', 0):8.3f}")
+wires = []
+for line in open(path):
+    d = json.loads(line)
+    for w in d.get("emulated_wire") or []:
+        wires.append((d["config"]["workload"], d["config"].get("hook_path", "-"), w))
+    fe = d.get("forced_exchange")
+    if fe:
+        wires.append((d["config"]["workload"], "forced", fe))
+if wires:
+    print()
+    print("exchange path beside an emulated wire (bench line `emulated_wire`: one-rank communicator whose")
+    print("all-reduce costs this GPU an R-rank ring's HBM traffic, CU footprint and time at busBW), and")
+    print("forced-exchange lines (one-rank RCCL, the N > 1 code path):")
+    print(f"{'workload':58s} {'line':>28s} {'per-GPU GB/s':>12s} {'x R (implied)':>13s} {'ms/bucket':>9s}")
+    for wl, hp, w in wires:
+        if "busbw_gbs" in w:
+            tag = f"emulated ws={w['emulated_ranks']} @{w['busbw_gbs']:.0f}GB/s"
+            print(f"{wl:58s} {tag:>28s} {w['per_gpu_value']:12.1f} {w['implied_aggregate']:13.1f} {w['ms_per_bucket']:9.4f}")
+        else:
+            print(f"{wl:58s} {'forced exchange (1-rank RCCL)':>28s} {w['value']:12.1f} {'-':>13s} {w['ms_per_bucket']:9.4f}")
