@@ -2505,8 +2505,11 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
         // of the next chunk's (dfc[1]): the chunk's packed rows are one contiguous range, so
         // the slot map, that range and (EF21) gE are all loaded in ONE round trip, staged in
         // LDS (map: row -> slot within the range), and the chunk is written as 16-B quads.
-        static_assert(ARCTOPK_SHORT3_CHUNK <= 4096, "register staging sized for 4096-element chunks");
-        constexpr int UR = 4, UP = 16, UG = 4;  // rows, packed values, quads per thread
+        static_assert(ARCTOPK_SHORT3_CHUNK % 1024 == 0 && ARCTOPK_SHORT3_CHUNK <= 8192,
+                      "register staging: chunks of 1024 .. 8192 elements");
+        // rows (m >= 4: at most CHUNK / 4), packed values, output quads per thread
+        constexpr int UR = ARCTOPK_SHORT3_CHUNK / 1024, UP = ARCTOPK_SHORT3_CHUNK / 256,
+                      UG = ARCTOPK_SHORT3_CHUNK / 1024;
         const int nr = (int)ch.nrows, cnt = nr * m;
         const int32_t g0 = dfc[0], g1 = dfc[1];
         const int32_t f0 = g0 - (int32_t)s.sel_off;
