@@ -25,6 +25,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -448,6 +449,30 @@ extern "C" int arctopk_comm_allreduce(arctopk_comm* c, void* buf, int64_t count,
 
 namespace {
 
+// Diagnostics: host time of the exchange step's parts (ARCTOPK_HOST_TIMING=1 in the
+// environment at the first step; read and reset by arctopk_diag_host_times)
+constexpr int kHtParts = 8;  // entry, encode, sketch all-reduce, select, pack, packed all-reduce, finish, decode
+std::atomic<int64_t> g_ht_ns[kHtParts];
+std::atomic<int64_t> g_ht_calls{0};
+bool ht_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("ARCTOPK_HOST_TIMING");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+struct HostTimer {
+    bool on = ht_on();
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(int part) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        g_ht_ns[part].fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count(),
+                                std::memory_order_relaxed);
+        t = n;
+    }
+};
+
 inline int mark(void* const* marks, int i, hipStream_t st) {
     if (!marks || !marks[i]) return 0;
     return (int)hipEventRecord((hipEvent_t)marks[i], st);
@@ -506,18 +531,23 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (int f = comm_failed(packed_comm)) return f;
     const int ws = packed_comm ? packed_comm->nranks : 1;
     hipStream_t st = (hipStream_t)stream, as = (hipStream_t)ar_stream;
+    HostTimer ht;
+    if (ht.on) g_ht_calls.fetch_add(1, std::memory_order_relaxed);
     // this bucket's own deferred decode, if a caller never finished it (the hook always does)
     int e = arctopk_exchange_finish(p, stream, nullptr);
     if (!e) e = mark(marks, ARCTOPK_MARK_START, st);
     if (!V) V = p->b_V;
     if (!e && draw && p->info.v_len > 0) e = arctopk_draw_projections(p, seed, const_cast<void*>(V), stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_DRAW, st);
+    ht.lap(0);
     if (!e) e = arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_ENCODE, st);
+    ht.lap(1);
     // one all-reduce for every tensor's sketch (the reference: one per tensor, :33, :58, :88)
     if (!e && sketch_comm) e = arctopk_comm_allreduce(sketch_comm, p->b_sketch, p->info.sketch_len, p->dtype, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_SKETCH_AR, st);
     if (e) return e;
+    ht.lap(2);
     // the select, with an earlier bucket's deferred decode riding in the same launch when
     // both fit (the select's latency hides behind the decode's stream)
     int rode = 0;
@@ -542,6 +572,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_SELECT, st);
     if (e) return e;
+    ht.lap(3);
     // with collectives the pack kernel completes x_ev_packed itself (no marker packet on the
     // caller's stream, where one idles the GPU several us): the all-reduce stream waits for it,
     // and the watchdog sees the sketch all-reduce before it complete
@@ -558,6 +589,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_PACK, st);
     if (e) return e;
+    ht.lap(4);
     if (async_ar) {  // the index-free all-reduce of the packed values (:280) on its own stream
         hipError_t he = hipStreamWaitEvent(as, (hipEvent_t)p->x_ev_packed, 0);
         if (he != hipSuccess) return (int)he;
@@ -566,10 +598,12 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         if (he != hipSuccess) return (int)he;
         Watchdog::get().watch(packed_comm, p->x_ev_ar);
     }
+    ht.lap(5);
     // earlier buckets' deferred decodes the caller wants done now (in its order)
     for (int32_t i = 0; i < nfinish && !e; ++i)
         if (finish[i] && finish[i] != p) e = arctopk_exchange_finish(finish[i], stream, finish_marks ? finish_marks[i] : nullptr);
     if (e) return e;
+    ht.lap(6);
     if (defer) {
         p->x_deferred = async_ar ? 1 : 2;
         p->x_bucket = bucket;
@@ -589,7 +623,17 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
+    ht.lap(7);
     return e;
+}
+
+// Diagnostics (not in the public header): host ns spent in the exchange step's parts since the
+// last read (ARCTOPK_HOST_TIMING=1), summed over `*calls` steps; resets the sums.
+extern "C" int arctopk_diag_host_times(int64_t* ns, int32_t n, int64_t* calls) {
+    if (!ns || n < 0 || !calls) return ARCTOPK_EINVAL;
+    for (int i = 0; i < n && i < kHtParts; ++i) ns[i] = g_ht_ns[i].exchange(0);
+    *calls = g_ht_calls.exchange(0);
+    return 0;
 }
 
 // Diagnostics (not in the public header): the first `bytes` of a plan's multi-block select

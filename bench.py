@@ -258,8 +258,16 @@ def main():
         step()
     torch.cuda.synchronize()
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as _G
+    native_ht = None
     if _G.HOST_TIMES is not None:  # ARCTOPK_HOST_TIMING=1: steady-state calls only
         _G.HOST_TIMES.clear()
+        import ctypes
+        from allreducetopk_amd import _native as N
+        native_ht = N.lib().arctopk_diag_host_times  # (diagnostic export, not in the header)
+        native_ht.restype = ctypes.c_int32
+        native_ht.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        _ns, _calls = (ctypes.c_int64 * 8)(), ctypes.c_int64()
+        native_ht(_ns, 8, ctypes.byref(_calls))  # reset
     # the timed region: K steps, no markers
     dist.barrier()
     torch.cuda.synchronize()
@@ -273,6 +281,12 @@ def main():
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     host_times = dict(_G.HOST_TIMES) if _G.HOST_TIMES is not None else None
+    native_parts = None
+    if native_ht is not None:
+        native_ht(_ns, 8, ctypes.byref(_calls))
+        if _calls.value:
+            native_parts = {k: round(_ns[i] / _calls.value / 1e3, 2) for i, k in enumerate(
+                ("entry", "encode", "sketch_allreduce", "select", "pack", "packed_allreduce", "finish", "decode"))}
 
     # At N = 1 the hook's own path has no collectives; the N > 1 code path (one-rank RCCL
     # communicators, packed all-reduce on the exchange stream, deferred decodes) is timed
@@ -451,6 +465,8 @@ def main():
         calls = max(1, args.steps * nb)
         print("host_us_per_call " + json.dumps({k: round(v / calls * 1e6, 1)
                                                 for k, v in host_times.items()}), flush=True)
+        if native_parts:
+            print("native_step_host_us " + json.dumps(native_parts), flush=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.barrier()
