@@ -492,8 +492,12 @@ int ensure_event(void** ev, unsigned flags) {
 // The deferred decode of plan p's last exchange step, on `stream`: after that step's packed
 // all-reduce (a stream wait only when the host does not already see it complete).
 namespace {
+#ifndef ARCTOPK_WAIT_AR_QUERY
+#define ARCTOPK_WAIT_AR_QUERY 1  // A/B switch: 0 = always enqueue the stream wait (no host query)
+#endif
 int wait_ar(arctopk_plan* p, hipStream_t st) {
     if (p->x_deferred != 1) return 0;  // 2: no all-reduce on another stream
+    if (!ARCTOPK_WAIT_AR_QUERY) return (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
     const hipError_t q = hipEventQuery((hipEvent_t)p->x_ev_ar);
     if (q == hipErrorNotReady) return (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
     return q == hipSuccess ? 0 : (int)q;
