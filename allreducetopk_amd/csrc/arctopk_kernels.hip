@@ -2947,6 +2947,17 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
     decode_chunk<T, EF>(segs, chunks[blockIdx.x], dfirst + blockIdx.x, packed, slotmap, sc, gE, out, dlds);
 }
 
+// Two buckets' decodes in one launch (the backward's last exchange step: the previous bucket's
+// deferred decode and its own), blocks [0, a.n) of `a`, then `b`'s
+template <typename T, int EF>
+__global__ void __launch_bounds__(256) k_decode2(DecodeRide<T> a, DecodeRide<T> b) {
+    extern __shared__ __attribute__((aligned(16))) float dlds[];
+    const int i = (int)blockIdx.x;
+    const DecodeRide<T>& d = i < a.n ? a : b;
+    const int c = i < a.n ? i : i - a.n;
+    decode_chunk<T, EF>(d.segs, d.chunks[c], d.dfirst + c, d.packed, d.slotmap, d.sc, d.gE, d.out, dlds);
+}
+
 // A deferred decode (an earlier bucket's, arctopk_exchange_step's `ride`) riding in the
 // single-block select launch of the current bucket: the select blocks are latency-bound
 // (a few KiB each), the decode chunks stream the bucket, so the select is hidden behind the
@@ -3557,7 +3568,43 @@ extern "C" int arctopk_decode(const arctopk_plan* p, const void* packed, const i
     return arctopk_decode_segments(p, 0, p->nseg, packed, slotmap, ws, ef, gerr, out, stream);
 }
 
+namespace {
+template <typename T>
+int launch_decode_pair(const RideArgs& a, const RideArgs& b, hipStream_t st, hipEvent_t done) {
+    const DecodeRide<T> da = make_ride<T>(&a), db = make_ride<T>(&b);
+    const size_t lds = (size_t)std::max(a.rp->dec_lds_bytes, b.rp->dec_lds_bytes);
+    const dim3 grid(da.n + db.n);
+    if (a.ef == ARCTOPK_EF21) {
+        if (done) hipExtLaunchKernelGGL((k_decode2<T, ARCTOPK_EF21>), grid, dim3(256), lds, st, nullptr, done, 0, da, db);
+        else hipLaunchKernelGGL((k_decode2<T, ARCTOPK_EF21>), grid, dim3(256), lds, st, da, db);
+    } else {
+        if (done) hipExtLaunchKernelGGL((k_decode2<T, ARCTOPK_EF_NONE>), grid, dim3(256), lds, st, nullptr, done, 0, da, db);
+        else hipLaunchKernelGGL((k_decode2<T, ARCTOPK_EF_NONE>), grid, dim3(256), lds, st, da, db);
+    }
+    return (int)hipGetLastError();
+}
+}  // namespace
+
 namespace arctopk {
+// Two plans' whole-bucket decodes in one launch (same dtype and EF class, both with decode
+// chunks, LDS within 48 KiB); `done` as in decode_signal (may be null).  Returns
+// ARCTOPK_EINVAL when the pair does not qualify (the caller then decodes them one by one).
+int decode_pair(const arctopk_plan* pa, int32_t ws_a, int32_t ef_a, void* gerr_a, void* out_a,
+                const arctopk_plan* pb, int32_t ws_b, int32_t ef_b, void* gerr_b, void* out_b, void* stream,
+                void* done) {
+    if (!pa || !pb || !out_a || !out_b || pa->dtype != pb->dtype || ws_a < 1 || ws_b < 1) return ARCTOPK_EINVAL;
+    if ((ef_a == ARCTOPK_EF21) != (ef_b == ARCTOPK_EF21) || ef_a < 0 || ef_a > 2 || ef_b < 0 || ef_b > 2)
+        return ARCTOPK_EINVAL;
+    if (ef_a == ARCTOPK_EF21 && (!gerr_a || !gerr_b)) return ARCTOPK_EINVAL;
+    if (pa->n_dec <= 0 || pb->n_dec <= 0 || std::max(pa->dec_lds_bytes, pb->dec_lds_bytes) > 48 * 1024)
+        return ARCTOPK_EINVAL;
+    if (pa->h_dec_begin[0] != 0 || pb->h_dec_begin[0] != 0) return ARCTOPK_EINVAL;
+    const RideArgs a{pa, ws_a, ef_a, gerr_a, out_a}, b{pb, ws_b, ef_b, gerr_b, out_b};
+    hipStream_t st = (hipStream_t)stream;
+    if (pa->dtype == ARCTOPK_BF16) return launch_decode_pair<bf16_t>(a, b, st, (hipEvent_t)done);
+    return launch_decode_pair<float>(a, b, st, (hipEvent_t)done);
+}
+
 // arctopk_decode whose kernel completes `done` (exchange.cpp)
 int decode_signal(const arctopk_plan* p, const void* packed, const int32_t* slotmap, int32_t ws, int32_t ef,
                   void* gerr, void* out, void* stream, void* done) {

@@ -449,6 +449,9 @@ namespace arctopk {
 int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
                 const arctopk_plan* next, uint64_t next_seed, void* next_V, const arctopk_plan* rp,
                 int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream);
+int decode_pair(const arctopk_plan* pa, int32_t ws_a, int32_t ef_a, void* gerr_a, void* out_a,
+                const arctopk_plan* pb, int32_t ws_b, int32_t ef_b, void* gerr_b, void* out_b, void* stream,
+                void* done);
 int pack_signal(const arctopk_plan* p, const void* grad, void* err, int32_t ef, const int32_t* rowlist,
                 const int32_t* slotmap, void* packed, void* stream, void* done);
 // arctopk_decode whose kernel completes `done`

@@ -441,6 +441,10 @@ extern "C" int arctopk_comm_allreduce(arctopk_comm* c, void* buf, int64_t count,
     return 0;
 }
 
+#ifndef ARCTOPK_DECODE_PAIR
+#define ARCTOPK_DECODE_PAIR 1  // the last step's decode and the last finished one share a launch
+#endif
+
 // flags of the pack kernel's stop event (A/B switch): 0 = a timing event with the default
 // (system-scope) release at the kernel's end
 #ifndef ARCTOPK_PACK_EV_FLAGS
@@ -603,9 +607,16 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         Watchdog::get().watch(packed_comm, p->x_ev_ar);
     }
     ht.lap(5);
+    // the backward's last step (no deferral): the last deferred decode it finishes shares one
+    // launch with its own decode, after its own packed all-reduce (unless markers were asked for)
+    arctopk_plan* pair = nullptr;
+    if (ARCTOPK_DECODE_PAIR && !defer && nfinish > 0 && finish[nfinish - 1] && finish[nfinish - 1] != p &&
+        finish[nfinish - 1]->x_deferred && !(finish_marks && finish_marks[nfinish - 1]) && !marks)
+        pair = finish[nfinish - 1];
     // earlier buckets' deferred decodes the caller wants done now (in its order)
     for (int32_t i = 0; i < nfinish && !e; ++i)
-        if (finish[i] && finish[i] != p) e = arctopk_exchange_finish(finish[i], stream, finish_marks ? finish_marks[i] : nullptr);
+        if (finish[i] && finish[i] != p && finish[i] != pair)
+            e = arctopk_exchange_finish(finish[i], stream, finish_marks ? finish_marks[i] : nullptr);
     if (e) return e;
     ht.lap(6);
     if (defer) {
@@ -619,6 +630,21 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (packed_comm) e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
     if (e) return e;
+    if (pair) {
+        if (packed_comm && (e = ensure_event(&p->x_ev_dec, hipEventDisableTiming | hipEventReleaseToDevice))) return e;
+        if ((e = wait_ar(pair, st))) return e;
+        e = arctopk::decode_pair(pair, pair->x_ws, pair->x_ef, pair->x_gerr, pair->x_bucket, p, ws, ef, gerr, bucket,
+                                 stream, packed_comm ? p->x_ev_dec : nullptr);
+        if (!e) {
+            pair->x_deferred = 0;
+            if (packed_comm) Watchdog::get().watch(packed_comm, p->x_ev_dec);
+            ht.lap(7);
+            return 0;
+        }
+        if (e != ARCTOPK_EINVAL) return e;
+        // the pair does not qualify (dtype, EF class, LDS): one by one
+        if ((e = arctopk_exchange_finish(pair, stream, nullptr))) return e;
+    }
     if (packed_comm) {  // the decode kernel completes x_ev_dec: the inline all-reduce is watched too
         if ((e = ensure_event(&p->x_ev_dec, hipEventDisableTiming | hipEventReleaseToDevice))) return e;
         e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream, p->x_ev_dec);
