@@ -19,14 +19,18 @@ keep() {  # the counters of $1 that this rocprofv3 lists
 }
 P1=$(keep "$P1"); P2=$(keep "$P2")
 echo "pass 1: $P1"; echo "pass 2: $P2"
-for w in $WL; do
-  mkdir -p $OUT/$w
-  ARGS="--workload $w --steps 6 --warmup 3 --no-cpu-baseline --no-forced-exchange --no-phase-events"
+# WL entries: a workload name, or name:extra-args with commas for spaces (headline:--dtype,bf16)
+for ent in $WL; do
+  w=${ent%%:*}; extra=""; [ "$ent" != "$w" ] && extra=$(echo "${ent#*:}" | tr ',' ' ')
+  tag=$(echo "$ent" | tr -c 'a-zA-Z0-9_\n' '_' | sed 's/__*/_/g; s/_$//')
+  w_dir=$OUT/$tag
+  mkdir -p $w_dir
+  ARGS="--workload $w $extra --steps 6 --warmup 3 --no-cpu-baseline --no-forced-exchange --no-phase-events --wire-busbw"
   i=0
   for P in "$P1" "$P2"; do
     i=$((i+1))
-    timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace -T --output-format csv -d $OUT/$w/p$i -o run -- \
-        python3 bench.py $ARGS > $OUT/$w/p$i.log 2>&1 || { echo "pmc pass $i of $w failed"; tail -5 $OUT/$w/p$i.log; exit 1; }
-    echo "$w pass $i done"
+    timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace -T --output-format csv -d $w_dir/p$i -o run -- \
+        python3 bench.py $ARGS > $w_dir/p$i.log 2>&1 || { echo "pmc pass $i of $ent failed"; tail -5 $w_dir/p$i.log; exit 1; }
+    echo "$ent pass $i done"
   done
 done

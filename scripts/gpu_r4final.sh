@@ -47,6 +47,8 @@ LIST
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-forced-exchange --wire-busbw 350 --no-phase-events > gpurun_out/r4final/tr_wire.log 2>&1 || { tail -5 gpurun_out/r4final/tr_wire.log; exit 1; }
   python3 scripts/wire_trace_summary.py gpurun_out/r4final/tr_wire 283 > gpurun_out/r4final/trace_wire_headline.txt
 else
-  bash scripts/gpu_r4counters.sh gpurun_out/r4final/pmc || exit 1
-  for w in resnet18_conv resnet50_mixed; do python3 scripts/sq_summary.py gpurun_out/r4final/pmc/$w > gpurun_out/r4final/sq_$w.txt; done
+  WL="resnet18_conv resnet50_mixed headline:--dtype,bf16 headline:--ef,noef" bash scripts/gpu_r4counters.sh gpurun_out/r4final/pmc || exit 1
+  for w in resnet18_conv resnet50_mixed headline_dtype_bf16 headline_ef_noef; do
+    python3 scripts/sq_summary.py gpurun_out/r4final/pmc/$w > gpurun_out/r4final/sq_$w.txt
+  done
 fi
