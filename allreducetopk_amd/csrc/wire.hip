@@ -19,8 +19,12 @@ namespace arctopk {
 namespace {
 
 constexpr int kWireThreads = 256;
-constexpr int kWireUnroll = 8;                                 // 16-B units per thread per slice
-constexpr int64_t kWireSlice = (int64_t)kWireThreads * kWireUnroll;  // units per paced slice (32 KiB)
+// 16-B units per thread per slice: a slice is one memory round trip, so a workgroup moves at most
+// a slice per round trip.  32 KiB slices (8 units) made the kernel latency-bound beside the
+// encode (~90 slices per workgroup at 350 GB/s x ~5 us round trips > its 283 us pace: the
+// emulated collective ran 387-642 us); 128 KiB slices keep ~22 round trips per workgroup.
+constexpr int kWireUnroll = 32;
+constexpr int64_t kWireSlice = (int64_t)kWireThreads * kWireUnroll;  // units per paced slice (128 KiB)
 
 __global__ void __launch_bounds__(kWireThreads) k_wire(float4* __restrict__ buf, int64_t n4, int64_t moves,
                                                        uint64_t ticks) {
