@@ -960,9 +960,12 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                 pk.known_stream(ars)
         marks = _call_marks(state, _EXCHANGE_MARKS)
         nf = len(fin)
-        fin_plans = (N.c_void_p * max(1, nf))(*[e_[0].handle for e_ in fin])
-        fin_marks = (N.c_void_p * max(1, nf))(*[N.ctypes.cast(e_[2], N.c_void_p).value if e_[2] is not None
-                                                else None for e_ in fin])
+        if nf:
+            fin_plans = (N.c_void_p * nf)(*[e_[0].handle for e_ in fin])
+            fin_marks = (N.c_void_p * nf)(*[N.ctypes.cast(e_[2], N.c_void_p).value if e_[2] is not None
+                                            else None for e_ in fin])
+        else:  # (most calls: no ctypes arrays built per call)
+            fin_plans = fin_marks = None
         _ht("prep")
         st_ = L.arctopk_exchange_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
                                       int(err_in), int(draw), seed,
