@@ -193,7 +193,7 @@ def main():
                     help="at N = 1: also time the exchange path beside an emulated WIRE_RANKS-rank ring "
                          "all-reduce paced to each of these bus bandwidths (GB/s; none: skip)")
     ap.add_argument("--wire-ranks", type=int, default=8)
-    ap.add_argument("--wire-blocks", type=int, default=32,
+    ap.add_argument("--wire-blocks", type=int, default=64,
                     help="workgroups of the emulated collective (its CU footprint)")
     args = ap.parse_args()
 
