@@ -130,7 +130,7 @@ class Comm:
     # ---- emulated wire (measurement only) ---------------------------------------------
     @classmethod
     def wire(cls, device: torch.device, ranks: int = 8, busbw_gbs: float = 350.0,
-             latency_us: float = 15.0, blocks: int = 32) -> "Comm":
+             latency_us: float = 15.0, blocks: int = 64) -> "Comm":
         """World size 1 (buffers unchanged) at the local cost of a `ranks`-rank ring all-reduce
         paced to `busbw_gbs` (arctopk_comm_init_wire)."""
         h = ctypes.c_void_p()
