@@ -1815,7 +1815,7 @@ template <typename T>
 struct DecodeRide {
     const SegDev* segs;
     const Chunk* chunks;
-    const Dec3* d3;         // the mode-3 chunk descriptors
+    const int32_t* dfirst;  // the chunk table (mode 3)
     const T* packed;
     const int32_t* slotmap;
     T* gE;
@@ -1824,8 +1824,8 @@ struct DecodeRide {
     int32_t n;  // chunks (blocks); 0: none
 };
 template <typename T, int EF>
-__device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk* __restrict__ chp,
-                                             const Dec3* __restrict__ d3p,
+__device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                             const int32_t* __restrict__ dfc,
                                              const T* __restrict__ packed,
                                              const int32_t* __restrict__ slotmap, Scale sc,
                                              T* __restrict__ gE, T* __restrict__ out,
@@ -1846,7 +1846,7 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     const int rb = (int)blockIdx.x - ((int)gridDim.x - job.n - dr.n);
     if (rb >= 0) {  // the ride's decode chunks
-        decode_chunk<T, EF>(dr.segs, dr.chunks + rb, dr.d3 + rb, dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
+        decode_chunk<T, EF>(dr.segs, dr.chunks[rb], dr.dfirst + rb, dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
                             reinterpret_cast<float*>(dyn));
         return;
     }
@@ -2137,7 +2137,7 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                                               const T* __restrict__ G, T* __restrict__ E,
                                               const int32_t* __restrict__ rowlist,
                                               const int32_t* __restrict__ slotmap,
-                                              T* __restrict__ packed, Dec3* __restrict__ d3) {
+                                              T* __restrict__ packed, int32_t* __restrict__ dfirst) {
     const Chunk ch = chunks[blockIdx.x];
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
@@ -2206,10 +2206,10 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
                 const int64_t rj = rs[jl];
                 const int64_t rp = jl > 0 ? rs[jl - 1] : before;
                 for (int64_t l = (rp + CR) / CR; l <= rj / CR; ++l)
-                    d3[s.dchunk0 + l].first = (int32_t)(s.sel_off + j);
+                    dfirst[s.dchunk0 + l] = (int32_t)(s.sel_off + j);
                 if (j == s.k_rows - 1)
                     for (int64_t l = (rj + CR) / CR; l <= nch; ++l)
-                        d3[s.dchunk0 + l].first = (int32_t)(s.sel_off + s.k_rows);
+                        dfirst[s.dchunk0 + l] = (int32_t)(s.sel_off + s.k_rows);
             }
         }
         const uint32_t cnt = (uint32_t)(nr * m);
@@ -2485,8 +2485,8 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
 // One decode chunk (256 threads): k_decode's block, or a block of another launch that a
 // deferred decode rides in (k_select_small_dec).  dlds: the small-m chunk tile (dynamic LDS).
 template <typename T, int EF>
-__device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk* __restrict__ chp,
-                                             const Dec3* __restrict__ d3p,
+__device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                             const int32_t* __restrict__ dfc,
                                              const T* __restrict__ packed,
                                              const int32_t* __restrict__ slotmap, Scale sc,
                                              T* __restrict__ gE, T* __restrict__ out,
@@ -2494,15 +2494,15 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
     // mean of the all-reduced values (ref values_memory.div_(ws)), rounded to T
     auto mean4 = [&](float4 v) { return rnd4<T>(sc(v)); };
     auto mean1 = [&](float v) { return rnd<T>(sc(v)); };
-    // one round trip for the chunk's geometry: its mode-3 descriptor (with the `first` the pack
-    // wrote), the next chunk's `first`, and the generic chunk entry (the other modes)
-    const Dec3 d = d3p[0];
-    const int32_t g1 = d3p[1].first;
-    const Chunk ch = *chp;
-    if (d.mode == 3) {
+    const SegDev s = segs[ch.seg];
+    const int m = (int)s.m;
+    const int64_t base = s.offset + ch.row0 * m;
+    const int32_t* sm = slotmap + s.row_off + ch.row0;
+    const T* pk = packed + s.packed_off;
+    if (ch.mode == 3) {
         // Short rows (4 <= m < 256), chunk of nr rows starting on a quad boundary of the bucket.
-        // The pack wrote the bucket-wide index of the chunk's first selected row (d.first) and
-        // of the next chunk's (g1): the chunk's packed rows are one contiguous range, so
+        // The pack wrote the bucket-wide index of the chunk's first selected row (dfc[0]) and
+        // of the next chunk's (dfc[1]): the chunk's packed rows are one contiguous range, so
         // the slot map, that range and (EF21) gE are all loaded in ONE round trip, staged in
         // LDS (map: row -> slot within the range), and the chunk is written as 16-B quads.
         static_assert(ARCTOPK_SHORT3_CHUNK % 1024 == 0 && ARCTOPK_SHORT3_CHUNK <= 8192,
@@ -2510,16 +2510,12 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
         // rows (m >= 4: at most CHUNK / 4), packed values, output quads per thread
         constexpr int UR = ARCTOPK_SHORT3_CHUNK / 1024, UP = ARCTOPK_SHORT3_CHUNK / 256,
                       UG = ARCTOPK_SHORT3_CHUNK / 1024;
-        const int m = d.m;
-        const int64_t base = d.base;
-        const int32_t* sm = slotmap + d.sm;
-        const int nr = d.nrows, cnt = nr * m;
-        const int32_t g0 = d.first;
-        const int32_t f0 = g0 - d.sel_off;
+        const int nr = (int)ch.nrows, cnt = nr * m;
+        const int32_t g0 = dfc[0], g1 = dfc[1];
+        const int32_t f0 = g0 - (int32_t)s.sel_off;
         const int nsel = max(0, min(g1 - g0, nr));
         const int np = nsel * m;
-        const int64_t pofs = d.pbase + (int64_t)g0 * m;  // packed element of the chunk's first value
-        const T* pkc = packed + pofs;
+        const T* pkc = pk + (int64_t)f0 * m;
         int32_t* lmap = reinterpret_cast<int32_t*>(dlds);
         float* lpk = dlds + ((nr + 3) & ~3);  // (16-B aligned: quad stores)
         int32_t sv[UR];
@@ -2536,7 +2532,7 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
         // cover it -- a quarter of the load instructions; `lead` values of the first quad
         // precede the range (the buffer is a whole number of quads: no read past its end)
         constexpr bool vecp = sizeof(T) == 4 && ARCTOPK_SHORT3_VEC;
-        const int lead = vecp ? (int)(pofs & 3) : 0;
+        const int lead = vecp ? (int)((s.packed_off + (int64_t)f0 * m) & 3) : 0;
         const int nq = (np + lead + 3) >> 2;
         if constexpr (vecp) {
             const float4* pq0 = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pkc) - lead);
@@ -2594,7 +2590,7 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int ej = min(e + j, cnt - 1);
-                const uint32_t r = div32((uint32_t)ej, d.magic32);
+                const uint32_t r = div32((uint32_t)ej, s.magic32);
                 const int c = ej - (int)r * m;
                 const int sl = lmap[r];
                 sel[j] = sl >= 0 && sl < nsel && e + j < cnt;
@@ -2620,11 +2616,6 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
         }
         return;
     }
-    const SegDev s = segs[ch.seg];
-    const int m = (int)s.m;
-    const int64_t base = s.offset + ch.row0 * m;
-    const int32_t* sm = slotmap + s.row_off + ch.row0;
-    const T* pk = packed + s.packed_off;
     if constexpr (sizeof(T) == 4) {
         if (ch.mode == 1) {  // m in {1, 2}, 16-B aligned: lane per output quad
             const int nq = (int)((ch.nrows * m + 3) >> 2);
@@ -2948,12 +2939,12 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
 template <typename T, int EF>
 __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
                                                 const Chunk* __restrict__ chunks,
-                                                const Dec3* __restrict__ d3,
+                                                const int32_t* __restrict__ dfirst,
                                                 const T* __restrict__ packed,
                                                 const int32_t* __restrict__ slotmap, Scale sc,
                                                 T* __restrict__ gE, T* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float dlds[];  // small-m chunk tile
-    decode_chunk<T, EF>(segs, chunks + blockIdx.x, d3 + blockIdx.x, packed, slotmap, sc, gE, out, dlds);
+    decode_chunk<T, EF>(segs, chunks[blockIdx.x], dfirst + blockIdx.x, packed, slotmap, sc, gE, out, dlds);
 }
 
 // Two buckets' decodes in one launch (the backward's last exchange step: the previous bucket's
@@ -2964,7 +2955,7 @@ __global__ void __launch_bounds__(256) k_decode2(DecodeRide<T> a, DecodeRide<T> 
     const int i = (int)blockIdx.x;
     const DecodeRide<T>& d = i < a.n ? a : b;
     const int c = i < a.n ? i : i - a.n;
-    decode_chunk<T, EF>(d.segs, d.chunks + c, d.d3 + c, d.packed, d.slotmap, d.sc, d.gE, d.out, dlds);
+    decode_chunk<T, EF>(d.segs, d.chunks[c], d.dfirst + c, d.packed, d.slotmap, d.sc, d.gE, d.out, dlds);
 }
 
 // A deferred decode (an earlier bucket's, arctopk_exchange_step's `ride`) riding in the
@@ -2984,7 +2975,7 @@ __global__ void __launch_bounds__(kST) k_select_small_dec(const SegDev* __restri
         select_small_seg<T, kST>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, dyn);
         return;
     }
-    decode_chunk<T, EF>(dr.segs, dr.chunks + (blockIdx.x - nsel), dr.d3 + (blockIdx.x - nsel), dr.packed,
+    decode_chunk<T, EF>(dr.segs, dr.chunks[blockIdx.x - nsel], dr.dfirst + (blockIdx.x - nsel), dr.packed,
                         dr.slotmap, dr.sc, dr.gE, dr.out,
                         reinterpret_cast<float*>(dyn));
 }
@@ -3146,7 +3137,7 @@ DecodeRide<T> make_ride(const RideArgs* ra) {
     const arctopk_plan* rp = ra->rp;
     dr.segs = rp->d_segs;
     dr.chunks = rp->d_dec;
-    dr.d3 = rp->d_dec3;
+    dr.dfirst = rp->d_dfirst;
     dr.packed = static_cast<const T*>(rp->b_packed);
     dr.slotmap = rp->b_slotmap;
     dr.gE = static_cast<T*>(ra->gerr);
@@ -3305,13 +3296,13 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
 template <typename T, int EF>
 void pack_launch(dim3 grid, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
                  const T* grad, T* err, const int32_t* rowlist, const int32_t* slotmap, T* packed,
-                 Dec3* d3) {
+                 int32_t* dfirst) {
     if (done)
         hipExtLaunchKernelGGL((k_pack<T, EF>), grid, dim3(256), 0, st, nullptr, done, 0, segs, ch, grad, err,
-                              rowlist, slotmap, packed, d3);
+                              rowlist, slotmap, packed, dfirst);
     else
         hipLaunchKernelGGL((k_pack<T, EF>), grid, dim3(256), 0, st, segs, ch, grad, err, rowlist, slotmap,
-                           packed, d3);
+                           packed, dfirst);
 }
 
 template <typename T>
@@ -3324,11 +3315,11 @@ int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* 
     dim3 grid(c1 - c0);
     const Chunk* ch = p->d_pack + c0;
     if (ef == ARCTOPK_EF_NONE)
-        pack_launch<T, ARCTOPK_EF_NONE>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dec3);
+        pack_launch<T, ARCTOPK_EF_NONE>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dfirst);
     else if (ef == ARCTOPK_EF14)
-        pack_launch<T, ARCTOPK_EF14>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dec3);
+        pack_launch<T, ARCTOPK_EF14>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dfirst);
     else if (ef == ARCTOPK_EF21)
-        pack_launch<T, ARCTOPK_EF21>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dec3);
+        pack_launch<T, ARCTOPK_EF21>(grid, st, done, p->d_segs, ch, grad, err, rowlist, slotmap, packed, p->d_dfirst);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -3337,12 +3328,12 @@ int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* 
 // `done` as in pack_launch (the decode after an inline all-reduce, watched by exchange.cpp)
 template <typename T, int EF>
 void decode_launch(dim3 grid, size_t lds, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
-                   const Dec3* d3, const T* packed, const int32_t* slotmap, Scale sc, T* gerr, T* out) {
+                   const int32_t* dfirst, const T* packed, const int32_t* slotmap, Scale sc, T* gerr, T* out) {
     if (done)
-        hipExtLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, nullptr, done, 0, segs, ch, d3,
+        hipExtLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, nullptr, done, 0, segs, ch, dfirst,
                               packed, slotmap, sc, gerr, out);
     else
-        hipLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, segs, ch, d3, packed, slotmap, sc,
+        hipLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, segs, ch, dfirst, packed, slotmap, sc,
                            gerr, out);
 }
 
@@ -3357,10 +3348,10 @@ int launch_decode(const arctopk_plan* p, int c0, int c1, const void* packed_, co
     const Scale sc = make_scale(ws);
     const size_t lds = (size_t)p->dec_lds_bytes;
     if (ef == ARCTOPK_EF21)
-        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, p->d_dec3 + c0, packed, slotmap, sc, gerr,
+        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, p->d_dfirst + c0, packed, slotmap, sc, gerr,
                                        out);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, p->d_dec3 + c0, packed, slotmap, sc,
+        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, p->d_dfirst + c0, packed, slotmap, sc,
                                           gerr, out);
     else
         return ARCTOPK_EINVAL;
@@ -3419,7 +3410,7 @@ int launch_select_ride(const arctopk_plan* p, const void* sketch_, int32_t ws, i
     DecodeRide<T> dr;
     dr.segs = rp->d_segs;
     dr.chunks = rp->d_dec;
-    dr.d3 = rp->d_dec3;
+    dr.dfirst = rp->d_dfirst;
     dr.packed = static_cast<const T*>(rp->b_packed);
     dr.slotmap = rp->b_slotmap;
     dr.gE = static_cast<T*>(rp_gerr);

@@ -371,29 +371,13 @@ struct VDrawJob {      // a projection draw riding in the trailing blocks of ano
     int32_t n;         // trailing blocks (one chunk each); 0: no draw
 };
 
-// Mode-3 decode chunk, self-contained (plan time, one 48-B entry per decode chunk; zero for the
-// other modes): a mode-3 block's first round trip loads its entry and the next entry's `first`
-// and nothing else -- no Chunk / SegDev lookups before the data.  `first` is written by the
-// pack: the bucket-wide index (sel_off + slot) of the chunk's first selected row.
-struct Dec3 {
-    int64_t base;      // bucket element of the chunk's first element (offset + row0 * m)
-    int64_t pbase;     // packed element of bucket-wide slot 0 of the segment (packed_off - sel_off * m)
-    int64_t sm;        // slot-map index of the chunk's first row (row_off + row0)
-    int32_t m, nrows;
-    uint32_t magic32;  // ceil(2^32 / m)
-    int32_t sel_off;
-    int32_t first;     // written by the pack
-    int32_t mode;      // 3, else 0
-};
-static_assert(sizeof(Dec3) == 48, "Dec3 is three 16-B loads");
-
 struct Chunk {         // pack: selected-row range (mode 0) or row range (mode 1); decode: row range
     int32_t seg;
     int32_t mode;      // 1: m in {1, 2}, fp32, 16-B aligned: quad streams over every row;
                        // decode 2: 4 <= m < 256 fp32, lane per output quad;
                        // decode 3: 4 <= m < 256, quad-aligned chunks: the chunk's slot map and
                        //   packed rows staged in LDS, the packed range read from the chunk
-                       //   table the pack wrote (d_dec3), one round trip for the data
+                       //   table the pack wrote (d_dfirst), one round trip for the data
     int64_t row0;
     int64_t nrows;
 };
@@ -427,9 +411,9 @@ struct arctopk_plan {
     int32_t* h_pack_begin;        // [nseg + 1]: first pack chunk of each segment
     int32_t* h_dec_begin;         // [nseg + 1]: first decode chunk of each segment
     int dec_lds_bytes;            // dynamic LDS of the decode launch (small-m chunk tiles)
-    arctopk::Dec3* d_dec3;        // [n_dec + 1]: mode-3 chunk descriptors; `first` (the bucket-wide
-                                  // index of the chunk's first selected row) written by the pack
-                                  // from the row list, read by the chunk (and the next entry)
+    int32_t* d_dfirst;            // [n_dec + 1]: per decode chunk, the bucket-wide index (sel_off +
+                                  // slot) of its first selected row; written by the pack from the
+                                  // row list, read by mode-3 decode chunks (and the next entry)
     uint32_t* d_keys;             // select workspace: one key per row
     int32_t* d_small;             // segments selected by the fused one-block kernel
     int n_small;

@@ -302,24 +302,9 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     if (p->n_enc_e) ALLOC_COPY(p->d_enc_e, enc_e);
     ALLOC_COPY(p->d_pack, pack);
     ALLOC_COPY(p->d_dec, dec);
-    {
-        std::vector<Dec3> d3(dec.size() + 1);
-        std::memset(d3.data(), 0, d3.size() * sizeof(Dec3));
-        for (size_t c = 0; c < dec.size(); ++c) {
-            if (dec[c].mode != 3) continue;
-            const SegDev& g = dsegs[dec[c].seg];
-            Dec3& d = d3[c];
-            d.base = g.offset + dec[c].row0 * g.m;
-            d.pbase = g.packed_off - g.sel_off * g.m;
-            d.sm = g.row_off + dec[c].row0;
-            d.m = (int32_t)g.m;
-            d.nrows = (int32_t)dec[c].nrows;
-            d.magic32 = g.magic32;
-            d.sel_off = (int32_t)g.sel_off;
-            d.mode = 3;
-        }
-        ALLOC_COPY(p->d_dec3, d3);
-    }
+    e = hipMalloc((void**)&p->d_dfirst, (dec.size() + 1) * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(p->d_dfirst, 0, (dec.size() + 1) * sizeof(int32_t));
+    if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
     ALLOC_COPY(p->d_small, small_ids);
     ALLOC_COPY(p->d_large, large_ids);
     ALLOC_COPY(p->d_split, split_ids);
@@ -411,7 +396,7 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_enc_e) (void)hipFree(p->d_enc_e);
     if (p->d_pack) (void)hipFree(p->d_pack);
     if (p->d_dec) (void)hipFree(p->d_dec);
-    if (p->d_dec3) (void)hipFree(p->d_dec3);
+    if (p->d_dfirst) (void)hipFree(p->d_dfirst);
     if (p->d_keys) (void)hipFree(p->d_keys);
     if (p->d_small) (void)hipFree(p->d_small);
     if (p->d_large) (void)hipFree(p->d_large);
