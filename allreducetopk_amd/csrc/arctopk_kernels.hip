@@ -2947,149 +2947,6 @@ __global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
     decode_chunk<T, EF>(segs, chunks[blockIdx.x], dfirst + blockIdx.x, packed, slotmap, sc, gE, out, dlds);
 }
 
-// Persistent mode-3 decode (A/B switch ARCTOPK_DEC3_PERSIST = grid size, 0: off): a block walks
-// chunks c, c + G, ... and issues the next chunk's slot-map / packed / gE loads before it
-// composes and stores the current one, so a chunk's load round trip overlaps the previous
-// chunk's stores (the one-chunk blocks wait a full round trip before their first store).
-#ifndef ARCTOPK_DEC3_PERSIST
-#define ARCTOPK_DEC3_PERSIST 0
-#endif
-template <typename T, int EF>
-__global__ void __launch_bounds__(256) k_decode3p(const SegDev* __restrict__ segs, const Chunk* __restrict__ chunks,
-                                                  const int32_t* __restrict__ dfirst, const T* __restrict__ packed,
-                                                  const int32_t* __restrict__ slotmap, Scale sc, T* __restrict__ gE,
-                                                  T* __restrict__ out, int nch) {
-    extern __shared__ __attribute__((aligned(16))) float dlds[];
-    constexpr int UR = ARCTOPK_SHORT3_CHUNK / 1024, UP = ARCTOPK_SHORT3_CHUNK / 256,
-                  UG = ARCTOPK_SHORT3_CHUNK / 1024;
-    struct Meta {
-        int64_t base;
-        const int32_t* sm;
-        const T* pkc;
-        int nr, m, nsel, f0;
-        uint32_t magic;
-    };
-    auto meta = [&](int c) {
-        const Chunk ch = chunks[c];
-        const SegDev s = segs[ch.seg];
-        const int32_t g0 = dfirst[c], g1 = dfirst[c + 1];
-        Meta x;
-        x.m = (int)s.m;
-        x.base = s.offset + ch.row0 * s.m;
-        x.sm = slotmap + s.row_off + ch.row0;
-        x.nr = (int)ch.nrows;
-        x.f0 = g0 - (int32_t)s.sel_off;
-        x.nsel = max(0, min(g1 - g0, x.nr));
-        x.pkc = packed + s.packed_off + (int64_t)x.f0 * x.m;
-        x.magic = s.magic32;
-        return x;
-    };
-    int32_t sv[UR];
-    float pv[UP];
-    [[maybe_unused]] float4 gq[UG];
-    auto load = [&](const Meta& x) {
-        const int np = x.nsel * x.m, cnt = x.nr * x.m;
-#pragma unroll
-        for (int u = 0; u < UR; ++u) {
-            const int r = (int)threadIdx.x + u * 256;
-            sv[u] = r < x.nr ? x.sm[r] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < UP; ++u) {
-            const int p = (int)threadIdx.x + u * 256;
-            pv[u] = p < np ? to_f(x.pkc[p]) : 0.f;
-        }
-        if constexpr (EF == ARCTOPK_EF21) {
-#pragma unroll
-            for (int u = 0; u < UG; ++u) {
-                const int e = 4 * ((int)threadIdx.x + u * 256);
-                if (e + 4 <= cnt) {
-                    gq[u] = ldq<T, kNtDecode>(gE + x.base + e, 0);
-                } else {
-                    float g4[4] = {0.f, 0.f, 0.f, 0.f};
-                    for (int j = 0; j < 4 && e + j < cnt; ++j) g4[j] = ld1<T>(gE + x.base + e + j);
-                    gq[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
-                }
-            }
-        }
-    };
-    const int G = (int)gridDim.x;
-    int c = (int)blockIdx.x;
-    if (c >= nch) return;
-    Meta cur = meta(c);
-    load(cur);
-    bool has_n = c + G < nch;
-    Meta nxt = has_n ? meta(c + G) : cur;
-    int32_t* lmap = reinterpret_cast<int32_t*>(dlds);
-    for (;;) {
-        const int m = cur.m, nr = cur.nr, cnt = nr * m, np = cur.nsel * m;
-        float* lpk = dlds + ((nr + 3) & ~3);
-#pragma unroll
-        for (int u = 0; u < UR; ++u) {
-            const int r = (int)threadIdx.x + u * 256;
-            if (r < nr) lmap[r] = sv[u] >= 0 ? sv[u] - cur.f0 : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < UP; ++u) {
-            const int p = (int)threadIdx.x + u * 256;
-            if (p < np) lpk[p] = pv[u];
-        }
-        [[maybe_unused]] float4 gcur[UG];
-        if constexpr (EF == ARCTOPK_EF21) {
-#pragma unroll
-            for (int u = 0; u < UG; ++u) gcur[u] = gq[u];
-        }
-        __syncthreads();
-        const bool more = has_n;
-        Meta nn = nxt;
-        bool has_nn = false;
-        if (more) {
-            load(nxt);  // the next chunk's data in flight while this one is composed and stored
-            has_nn = c + 2 * G < nch;
-            if (has_nn) nn = meta(c + 2 * G);
-        }
-#pragma unroll
-        for (int u = 0; u < UG; ++u) {
-            const int e = 4 * ((int)threadIdx.x + u * 256);
-            if (e >= cnt) break;
-            float o[4];
-            bool sel[4], any = false;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int ej = min(e + j, cnt - 1);
-                const uint32_t r = div32((uint32_t)ej, cur.magic);
-                const int cc = ej - (int)r * m;
-                const int sl = lmap[r];
-                sel[j] = sl >= 0 && sl < cur.nsel && e + j < cnt;
-                any = any || sel[j];
-                float v = sel[j] ? rnd<T>(sc(lpk[sl * m + cc])) : 0.f;
-                if constexpr (EF == ARCTOPK_EF21) {
-                    const float g = j == 0 ? gcur[u].x : j == 1 ? gcur[u].y : j == 2 ? gcur[u].z : gcur[u].w;
-                    v = sel[j] ? rnd<T>(g + v) : g + 0.f;
-                }
-                o[j] = v;
-            }
-            if (e + 4 <= cnt) {
-                stq<T, kNtDecode>(out + cur.base + e, 0, make_float4(o[0], o[1], o[2], o[3]));
-                if constexpr (EF == ARCTOPK_EF21)
-                    if (any) stq<T, false>(gE + cur.base + e, 0, make_float4(o[0], o[1], o[2], o[3]));
-            } else {
-                for (int j = 0; j < 4 && e + j < cnt; ++j) {
-                    st1<T>(out + cur.base + e + j, o[j]);
-                    if constexpr (EF == ARCTOPK_EF21)
-                        if (sel[j]) st1<T>(gE + cur.base + e + j, o[j]);
-                }
-            }
-        }
-        __syncthreads();  // lmap / lpk are restaged for the next chunk
-        if (!more) break;
-        c += G;
-        cur = nxt;
-        nxt = nn;
-        has_n = has_nn;
-    }
-}
-
 // Two buckets' decodes in one launch (the backward's last exchange step: the previous bucket's
 // deferred decode and its own), blocks [0, a.n) of `a`, then `b`'s
 template <typename T, int EF>
@@ -3490,23 +3347,6 @@ int launch_decode(const arctopk_plan* p, int c0, int c1, const void* packed_, co
     const Chunk* ch = p->d_dec + c0;
     const Scale sc = make_scale(ws);
     const size_t lds = (size_t)p->dec_lds_bytes;
-    if (ARCTOPK_DEC3_PERSIST > 0 && p->dec_all3 && lds <= 48 * 1024) {
-        if (ef != ARCTOPK_EF_NONE && ef != ARCTOPK_EF14 && ef != ARCTOPK_EF21) return ARCTOPK_EINVAL;
-        const dim3 pg(std::min(c1 - c0, ARCTOPK_DEC3_PERSIST));
-        const int32_t* df = p->d_dfirst + c0;
-        if (ef == ARCTOPK_EF21) {
-            if (done) hipExtLaunchKernelGGL((k_decode3p<T, ARCTOPK_EF21>), pg, dim3(256), lds, st, nullptr, done, 0,
-                                            p->d_segs, ch, df, packed, slotmap, sc, gerr, out, c1 - c0);
-            else hipLaunchKernelGGL((k_decode3p<T, ARCTOPK_EF21>), pg, dim3(256), lds, st, p->d_segs, ch, df, packed,
-                                    slotmap, sc, gerr, out, c1 - c0);
-        } else {
-            if (done) hipExtLaunchKernelGGL((k_decode3p<T, ARCTOPK_EF_NONE>), pg, dim3(256), lds, st, nullptr, done, 0,
-                                            p->d_segs, ch, df, packed, slotmap, sc, gerr, out, c1 - c0);
-            else hipLaunchKernelGGL((k_decode3p<T, ARCTOPK_EF_NONE>), pg, dim3(256), lds, st, p->d_segs, ch, df,
-                                    packed, slotmap, sc, gerr, out, c1 - c0);
-        }
-        return (int)hipGetLastError();
-    }
     if (ef == ARCTOPK_EF21)
         decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, p->d_dfirst + c0, packed, slotmap, sc, gerr,
                                        out);

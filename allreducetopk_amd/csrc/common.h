@@ -411,7 +411,6 @@ struct arctopk_plan {
     int32_t* h_pack_begin;        // [nseg + 1]: first pack chunk of each segment
     int32_t* h_dec_begin;         // [nseg + 1]: first decode chunk of each segment
     int dec_lds_bytes;            // dynamic LDS of the decode launch (small-m chunk tiles)
-    int dec_all3;                 // every decode chunk is mode 3 (the persistent decode may run)
     int32_t* d_dfirst;            // [n_dec + 1]: per decode chunk, the bucket-wide index (sel_off +
                                   // slot) of its first selected row; written by the pack from the
                                   // row list, read by mode-3 decode chunks (and the next entry)

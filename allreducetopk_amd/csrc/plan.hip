@@ -287,7 +287,6 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     std::copy(dec_begin.begin(), dec_begin.end(), p->h_dec_begin);
     p->enc_lds_bytes = lds;
     p->dec_lds_bytes = (int)dec_lds;
-    p->dec_all3 = !dec.empty() && std::all_of(dec.begin(), dec.end(), [](const Chunk& c) { return c.mode == 3; });
     p->n_small = (int)small_ids.size();
     p->n_large = (int)large_ids.size();
     p->small_lds = (int)(((small_rows + 3) & ~3) * 4 + 16);
