@@ -328,10 +328,23 @@ def main():
             torch.cuda.synchronize()
             fe = time.perf_counter() - t1
             v = args.steps * bytes_per_step / fe / 1e9
+            # the wire alone: each bucket's two ring all-reduces (sketch, packed values) at busBW
+            from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import _geometry
+            R_ = args.wire_ranks
+            wire_s = 0.0
+            for sh in layouts:
+                ab = algorithmic_bytes(args.ef, sh, args.ratio, args.r, eb)
+                k_bytes = ab["pack"] // {"noef": 2, "ef14": 3}.get(args.ef, 4)  # selected elements x eb
+                sk_bytes = sum(eb * _geometry(s_)[1] * (1 if len(s_) == 1 else args.r) for s_ in sh)
+                for nbytes in (sk_bytes, k_bytes):
+                    wire_s += 15e-6 + 2 * (R_ - 1) / R_ * nbytes / (bw * 1e9)
+            ceiling = bytes_per_step / wire_s / 1e9
             wire.append({"busbw_gbs": bw, "emulated_ranks": args.wire_ranks, "blocks": args.wire_blocks,
                          "latency_us": 15.0, "per_gpu_value": round(v, 2),
                          "implied_aggregate": round(args.wire_ranks * v, 2),
-                         "ms_per_bucket": round(fe / args.steps / nb * 1e3, 4)})
+                         "ms_per_bucket": round(fe / args.steps / nb * 1e3, 4),
+                         "wire_ceiling_per_gpu": round(ceiling, 2),
+                         "frac_of_wire_ceiling": round(v / ceiling, 4)})
         st.reset_exchange_comms()
         st.emulate_wire = None
 

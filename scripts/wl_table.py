@@ -26,10 +26,13 @@ if wires:
     print("exchange path beside an emulated wire (bench line `emulated_wire`: one-rank communicator whose")
     print("all-reduce costs this GPU an R-rank ring's HBM traffic, CU footprint and time at busBW), and")
     print("forced-exchange lines (one-rank RCCL, the N > 1 code path):")
-    print(f"{'workload':58s} {'line':>28s} {'per-GPU GB/s':>12s} {'x R (implied)':>13s} {'ms/bucket':>9s}")
+    print(f"{'workload':58s} {'line':>28s} {'per-GPU GB/s':>12s} {'x R (implied)':>13s} {'ms/bucket':>9s} "
+          f"{'of wire ceiling':>15s}")
     for wl, hp, w in wires:
         if "busbw_gbs" in w:
             tag = f"emulated ws={w['emulated_ranks']} @{w['busbw_gbs']:.0f}GB/s"
-            print(f"{wl:58s} {tag:>28s} {w['per_gpu_value']:12.1f} {w['implied_aggregate']:13.1f} {w['ms_per_bucket']:9.4f}")
+            fr = w.get("frac_of_wire_ceiling")
+            print(f"{wl:58s} {tag:>28s} {w['per_gpu_value']:12.1f} {w['implied_aggregate']:13.1f} {w['ms_per_bucket']:9.4f} "
+                  f"{'-' if fr is None else f'{fr:.3f}':>15s}")
         else:
             print(f"{wl:58s} {'forced exchange (1-rank RCCL)':>28s} {w['value']:12.1f} {'-':>13s} {w['ms_per_bucket']:9.4f}")
