@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the CU partition and codec pipelining it measured were reverted, see
+#  profiles/r04/experiments_not_kept.txt; the environment switches it sets no longer exist)
 # Round 4: CU partition of the exchange path (GroupTopKState.exchange_cus) beside the emulated
 # 8-rank wire: parity, wire lines at several reserved-CU counts, a kernel trace; host timing of
 # the forced-exchange ResNet-18 DDP buckets.
