@@ -61,12 +61,6 @@
 #ifndef ARCTOPK_DEC_CHUNK
 #define ARCTOPK_DEC_CHUNK 8192         // elements per decode chunk (rows >= 256)
 #endif
-#ifndef ARCTOPK_PACK_TARGET_BLOCKS
-#define ARCTOPK_PACK_TARGET_BLOCKS 0   // tuning switch (A/B builds): pack chunks a bucket aims at (0: fixed)
-#endif
-#ifndef ARCTOPK_PACK_MIN_CHUNK
-#define ARCTOPK_PACK_MIN_CHUNK 1024    // ... but never fewer selected elements per chunk than this
-#endif
 #ifndef ARCTOPK_STREAM_PACK_CHUNK
 #define ARCTOPK_STREAM_PACK_CHUNK 2048 // elements per m <= 2 stream-pack chunk
 #endif

@@ -133,14 +133,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     // chunk sizes (build-time A/B switches, common.h): short rows (m < 256) and the m <= 2
     // streams get smaller chunks, more blocks in flight (ResNet-50 1x1 mix, 2048-element
     // stream pack chunks: 346 -> 356 GB/s; 4096-element decode chunks: +3 %)
-    constexpr int64_t dec_elems = ARCTOPK_DEC_CHUNK;
-    // pack chunks of ARCTOPK_PACK_CHUNK selected elements, or smaller (down to
-    // ARCTOPK_PACK_MIN_CHUNK) so that a small bucket still yields ~ARCTOPK_PACK_TARGET_BLOCKS
-    // chunks (0: fixed size)
-    const int64_t pack_elems = ARCTOPK_PACK_TARGET_BLOCKS > 0
-        ? std::min<int64_t>(ARCTOPK_PACK_CHUNK, std::max<int64_t>(ARCTOPK_PACK_MIN_CHUNK,
-                                                                  info.values_len / ARCTOPK_PACK_TARGET_BLOCKS))
-        : (int64_t)ARCTOPK_PACK_CHUNK;
+    constexpr int64_t pack_elems = ARCTOPK_PACK_CHUNK, dec_elems = ARCTOPK_DEC_CHUNK;
     constexpr int64_t stream_pack_elems = ARCTOPK_STREAM_PACK_CHUNK;
     constexpr int64_t short_dec_elems = ARCTOPK_SHORT_DEC_CHUNK;
     constexpr bool interleave = ARCTOPK_ENC_INTERLEAVE != 0;  // interleaved row tiles
