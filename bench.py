@@ -79,13 +79,33 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4):
                 read=read)
 
 
-def pmc_traffic(workload: str, ef: str, kernel: str):
+def sparse_algorithmic_bytes(hook: str, ef: str, n_el: int, k_el: int, ws: int, eb: int = 4):
+    """Minimum HBM bytes per call of the TopK / RandK baselines (EF14 only; None otherwise).
+
+    TopK: SURVEY.md section 8(d)'s (28 + (8 + 16 ws) rho) B per element -- the EF14 fold
+    (read G, E; write E: 12), a two-pass radix select over |x| (2 x 4), compaction (4), the
+    decode's zero-fill (4), the gathered values and indices (8 rho) and the rank-ordered
+    scatter of every rank's values and indices (16 ws rho), with rho = k / N.
+    RandK: the fold (12), the index draw and the gather (12 rho: indices written, values read
+    and written), the residual zero at the indices (8 rho: indices read, E written), the decode
+    (4 + 8 rho: zero-fill, values and indices read) -> 16 + 28 rho."""
+    if ef != "ef14" or eb != 4:
+        return None
+    if hook == "topk":
+        return int(28 * n_el + (8 + 16 * ws) * k_el)
+    return int(16 * n_el + 28 * k_el)
+
+
+def pmc_traffic(workload: str, ef: str, kernel: str, n_gpus: int = 1):
     """HBM bytes per launch of `kernel` from the newest committed PMC profile of this
     workload (profiles/<round>/pmc_<workload>_<ef>.json, written by
     scripts/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of
-    this same bench command; FETCH_SIZE doubled per the gfx950 correction)."""
+    this same bench command; FETCH_SIZE doubled per the gfx950 correction).  At N > 1 only a
+    profile taken at that N counts (pmc_<workload>_<ef>_n<N>.json): the N = 1 file is never
+    reported for a multi-GPU line."""
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_{workload}_{ef}.json")))
+    suffix = "" if n_gpus == 1 else f"_n{n_gpus}"
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_{workload}_{ef}{suffix}.json")))
     if not paths:
         return None, None, None
     with open(paths[-1]) as fh:
@@ -159,6 +179,55 @@ def cpu_baseline(ef: str, seconds: float, workload: str, label: str, bucket_byte
                       + f"; host CPU share {threads} of {os.cpu_count()} visible"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd, env=None, timeout=None) -> int:
+    """Start `cmd` as n rank processes on this node (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT in their environment, as torch.distributed.run sets them) and
+    return the first non-zero exit status, else 0.  A failing rank ends the others.  Used by
+    `bench.py --gpus N` without a launcher; it runs before this process touches the GPU, and
+    the ranks are children (no exec from this process)."""
+    import subprocess
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    base["MASTER_PORT"] = str(_free_port())
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                 LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0")
+        procs.append(subprocess.Popen(cmd, env=e))
+    t_end = None if timeout is None else time.monotonic() + timeout
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:  # one rank failed: the others would wait for it forever
+                    q.terminate()
+        if t_end is not None and time.monotonic() > t_end:
+            for q in live:
+                q.kill()
+            rc = rc or 124
+            break
+        time.sleep(0.05)
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,13 +264,26 @@ def main():
     ap.add_argument("--wire-ranks", type=int, default=8)
     ap.add_argument("--wire-blocks", type=int, default=64,
                     help="workgroups of the emulated collective (its CU footprint)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's parsed launch (rank, world, master) and exit: no GPU")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks here, one process
+        # per GPU, before anything touches the GPU; rank 0 prints the JSON line
+        rc = launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+        raise SystemExit(rc if rc >= 0 else 128 - rc)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:  # the launch plumbing only (tests): no GPU, no process group
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local, "gpus": args.gpus,
+                          "steps": args.steps, "warmup": args.warmup, "backend": args.backend,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}),
+              flush=True)
+        return
     ndev = torch.cuda.device_count()
     if args.backend == "nccl" and world > ndev:
         raise SystemExit(f"{world} ranks but {ndev} visible GPUs (RCCL needs one GPU per rank)")
@@ -441,7 +523,23 @@ def main():
         roof["read_frac"] = roof["hook"]["read_frac"]
     if roof is not None:
         roof["traffic"], roof["traffic_source"], roof["traffic_lib_match"] = pmc_traffic(
-            args.workload + ("_bf16" if args.dtype == "bf16" else ""), args.ef, "k_encode")
+            args.workload + ("_bf16" if args.dtype == "bf16" else ""), args.ef, "k_encode", world)
+        if roof["traffic"] is None and world > 1:
+            roof["traffic_source"] = f"none: no PMC profile taken at N = {world} (N = 1 files are not reused)"
+    if args.hook != "arc":
+        # the baselines' roofline: their minimum bytes per call over the wall time per bucket
+        # (no markers on this path; the step is device-bound, so wall ~ device time)
+        k_el = sum(max(1, int(bucket_numel([s_]) * args.ratio)) for sh in layouts for s_ in sh) / nb
+        sb = sparse_algorithmic_bytes(args.hook, args.ef, bytes_per_step // nb // eb, int(k_el), world, eb)
+        if sb is not None:
+            wall_s = elapsed / args.steps / nb
+            ach = sb / wall_s / 1e9
+            roof = {"bound": "hbm", "kernel": f"whole {args.hook} hook per bucket (wall time)",
+                    "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "algorithmic_bytes_per_call": sb, "wall_us_per_bucket": round(wall_s * 1e6, 1),
+                    "formula": ("(28 + (8 + 16 ws) rho) B/elem (SURVEY 8d)" if args.hook == "topk"
+                                else "(16 + 28 rho) B/elem (fused RandK minimum)")}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -469,8 +567,14 @@ def main():
         "phase_ms_note": "separate pass, every call marked, decodes inline (not deferred)" if phase_ms else None,
         "roofline": roof,
         "algorithmic_bytes_per_call": {k: int(v) for k, v in alg.items()},
-        "cpu_baseline": None,
+        "cpu_baseline": None if world == 1 else {
+            "value": None, "unit": "GB/s", "cores": 0, "kind": "port",
+            "sample": "not timed at N > 1: the CPU baseline runs on rank 0 of the N = 1 line only "
+                      "(bench contract); see that line's cpu_baseline (ws 1 and ws 2 over gloo)"},
     }
+    if world > 1:
+        out["value_semantics"] = (f"value = bucket bytes of all {world} ranks / wall time (whole-job "
+                                  f"aggregate, bench contract); per_gpu_value = value / {world}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.ef, args.cpu_seconds, args.workload, label,
                                            eb * bucket_numel(shapes), args.hook)

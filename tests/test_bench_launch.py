@@ -1,0 +1,65 @@
+"""bench.py's own launcher (`--gpus N` without torch.distributed.run) and its bench-line
+helpers, on CPU: the rank environment, argument pass-through, failure propagation, and the
+baselines' algorithmic bytes."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import bench
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_launch_ranks_sets_the_rank_environment(tmp_path):
+    code = ("import os, sys; open(os.path.join(sys.argv[1], os.environ['RANK']), 'w').write("
+            "' '.join(os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')))")
+    assert bench.launch_ranks(3, [sys.executable, "-c", code, str(tmp_path)]) == 0
+    seen = [open(tmp_path / str(r)).read().split() for r in range(3)]
+    ports = {s[4] for s in seen}
+    assert len(ports) == 1
+    for r, s in enumerate(seen):
+        assert s[:4] == [str(r), str(r), "3", "127.0.0.1"]
+
+
+def test_launch_ranks_propagates_a_failing_rank_and_stops_the_others():
+    code = ("import os, sys, time\n"
+            "if os.environ['RANK'] == '1': sys.exit(3)\n"
+            "time.sleep(60)")
+    t0 = time.monotonic()
+    assert bench.launch_ranks(2, [sys.executable, "-c", code]) == 3
+    assert time.monotonic() - t0 < 30
+
+
+def test_bench_gpus_n_without_a_launcher_spawns_n_ranks():
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--steps", "5",
+                        "--warmup", "1", "--dry-run"], cwd=REPO, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    for d in lines:
+        assert d["world"] == 2 and d["gpus"] == 2 and d["steps"] == 5 and d["warmup"] == 1
+        assert d["backend"] == "gloo" and d["master"].startswith("127.0.0.1:")
+    assert lines[0]["master"] == lines[1]["master"]
+
+
+def test_bench_refuses_a_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_sparse_algorithmic_bytes_follow_the_survey_formula():
+    n, k = 67_108_864, 13_421_760
+    assert bench.sparse_algorithmic_bytes("topk", "ef14", n, k, 1) == 28 * n + 24 * k
+    assert bench.sparse_algorithmic_bytes("topk", "ef14", n, k, 8) == 28 * n + (8 + 128) * k
+    assert bench.sparse_algorithmic_bytes("randk", "ef14", n, k, 8) == 16 * n + 28 * k
+    assert bench.sparse_algorithmic_bytes("topk", "ef21", n, k, 1) is None
+
+
+def test_pmc_traffic_is_never_the_n1_file_at_n_gt_1():
+    assert bench.pmc_traffic("headline", "ef14", "k_encode", 2) == (None, None, None)
