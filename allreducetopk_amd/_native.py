@@ -57,6 +57,7 @@ _SIGS = {
     "arctopk_plan_describe": (c_int32, [POINTER(c_int64), POINTER(c_int32), c_int32, c_int32, c_double,
                                         c_void_p, POINTER(PlanInfo)]),
     "arctopk_plan_query": (c_int32, [c_void_p, POINTER(PlanInfo)]),
+    "arctopk_plan_group": (c_int32, [c_void_p, c_int32, c_int32, POINTER(c_void_p)]),
     "arctopk_plan_segment": (c_int32, [c_void_p, c_int32, POINTER(Segment)]),
     "arctopk_encode": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                  c_void_p]),

@@ -68,6 +68,35 @@ def _geometry(shape) -> Tuple[int, int, int]:
     return N.SEG_SKETCH, d // m if m else 0, m
 
 
+def group_runs(segs, numel: int, esz: int, target_bytes: int):
+    """[(seg_begin, seg_end), ...]: the bucket's segments cut into runs of about
+    `target_bytes` each (at most one cut per segment boundary), or None when fewer than two
+    runs result.  A run may start only at a segment whose offsets keep the kernels' vector
+    alignment (arctopk_plan_group: bucket, sketch, packed and V offsets multiples of 8
+    elements, slot map of 4); each cut is the valid boundary nearest to an equal share."""
+    ng = min(len(segs), -(-numel * esz // max(1, int(target_bytes))))
+    if ng < 2:
+        return None
+
+    def ok(i):
+        s = segs[i]
+        return (s.offset % 8 == 0 and s.sketch_off % 8 == 0 and s.packed_off % 8 == 0
+                and s.row_off % 4 == 0 and (s.kind != N.SEG_SKETCH or s.v_off % 8 == 0))
+
+    cuts = [0]
+    for j in range(1, ng):
+        goal = numel * j // ng
+        best = None
+        for i in range(cuts[-1] + 1, len(segs)):
+            if ok(i) and (best is None or abs(segs[i].offset - goal) < abs(segs[best].offset - goal)):
+                best = i
+        if best is not None:
+            cuts.append(best)
+    cuts.append(len(segs))
+    runs = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if a < b]
+    return runs if len(runs) >= 2 else None
+
+
 class BucketPlan:
     """Native plan + persistent device buffers of one bucket layout."""
 
@@ -288,6 +317,65 @@ class BucketPlan:
         N.check(N.lib().arctopk_row_energy(self.handle, self.sketch.data_ptr(), world_size,
                                            out.data_ptr(), stream), "arctopk_row_energy")
 
+    def groups(self, target_bytes: int):
+        """The bucket cut into runs of consecutive tensors of about `target_bytes` each (the
+        exchange pipeline's unit), as GroupPlans bound to this plan's
+        buffers; None when the bucket yields fewer than two (one tensor, or a small bucket).
+        Cuts fall only where every buffer offset keeps the kernels' alignment."""
+        key = int(target_bytes)
+        cache = self.__dict__.setdefault("_groups", {})
+        if key in cache:
+            return cache[key]
+        esz = torch.empty(0, dtype=self.dtype).element_size()
+        runs = group_runs(self.segments, int(self.info.numel), esz, key)
+        out = [GroupPlan(self, a, b) for a, b in runs] if runs else None
+        cache[key] = out
+        return out
+
+
+class GroupPlan:
+    """A run of consecutive tensors [seg_begin, seg_end) of a bucket plan (arctopk_plan_group):
+    its own native plan, bound to the parent's buffers at the run's offsets, so its sketch,
+    row list, slot map, packed values and projections are slices of the parent's.  The exchange
+    step runs it as it runs a bucket."""
+
+    def __init__(self, parent: BucketPlan, seg_begin: int, seg_end: int):
+        L = N.lib()
+        handle = N.c_void_p()
+        N.check(L.arctopk_plan_group(parent.handle, seg_begin, seg_end, N.ctypes.byref(handle)),
+                f"arctopk_plan_group({seg_begin}, {seg_end})")
+        self.handle = handle
+        self.parent = parent
+        self.seg_begin, self.seg_end = seg_begin, seg_end
+        info = N.PlanInfo()
+        N.check(L.arctopk_plan_query(handle, N.ctypes.byref(info)), "arctopk_plan_query")
+        self.info = info
+        self.dtype, self.device, self.r = parent.dtype, parent.device, parent.r
+        s0 = parent.segments[seg_begin]
+        self.offset = int(s0.offset)  # first bucket element of the run
+        vb = next((int(s.v_off) for s in parent.segments[seg_begin:seg_end] if s.kind == N.SEG_SKETCH), 0)
+        self.v_off = vb
+        self.sketch = parent.sketch[int(s0.sketch_off):int(s0.sketch_off) + max(1, info.sketch_len)]
+        self.packed = parent.packed[int(s0.packed_off):int(s0.packed_off) + max(1, info.packed_len)]
+        self.rowlist = parent.rowlist[int(s0.sel_off):]
+        self.slotmap = parent.slotmap[int(s0.row_off):]
+        self.V = parent.V_ring[0][vb:]
+        N.check(L.arctopk_plan_bind(handle, self.sketch.data_ptr(), self.rowlist.data_ptr(),
+                                    self.slotmap.data_ptr(), self.packed.data_ptr(), self.V.data_ptr()),
+                "arctopk_plan_bind")
+        self.v_drawn = None
+        self.v_stream = None
+        self.comm_registered = None
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and N._lib is not None:
+            try:
+                N._lib.arctopk_plan_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self.handle = None
+
 
 class GroupTopKState(HookState):
     """State of the ARC-TopK hook (reference :143-171; same constructor)."""
@@ -363,6 +451,14 @@ class GroupTopKState(HookState):
         if self.sketch_comm not in ("separate", "shared"):
             raise ValueError("ARCTOPK_SKETCH_COMM must be 'separate' or 'shared'")
         self._comms = None  # (group, device, sketch Comm, packed Comm), see init_exchange_comms
+        # The exchange pipeline below a bucket: "auto" runs a bucket as
+        # groups of consecutive tensors of about `group_bytes` when its all-reduce would leave
+        # the wire idle (the first bucket after the pipeline drained, the backward's last);
+        # "all": every bucket; "off": whole buckets.  Results are the same bits either way.
+        self.exchange_groups = os.environ.get("ARCTOPK_EXCHANGE_GROUPS", "auto")
+        if self.exchange_groups not in ("auto", "all", "off"):
+            raise ValueError("ARCTOPK_EXCHANGE_GROUPS must be 'auto', 'all' or 'off'")
+        self.group_bytes = int(float(os.environ.get("ARCTOPK_GROUP_MIB", "64")) * (1 << 20))
         # The plan of a bucket is found by its buffer's identity (no gradients() walk per
         # call).  DDP rebuilds its buckets once, after the first iteration, and the caching
         # allocator may hand a rebuilt bucket the same block: for the first
@@ -472,6 +568,8 @@ class GroupTopKState(HookState):
         while self._x_pend:
             plan, fut, marks, t, sid, _keep = self._x_pend.pop(0)
             N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
+            if fut is None:  # a group of a bucket: its last group's entry holds the Future
+                continue
             fut.set_result(t)
             if fut is upto:
                 break
@@ -941,47 +1039,93 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             dd = isinstance(bucket, dist.GradBucket) or getattr(state, "_ddp_registered", False)
         defer = dd and state.async_exchange and not bucket.is_last()
         pend = state._x_pend
+        marks = _call_marks(state, _EXCHANGE_MARKS)
+        # The exchange pipeline below a bucket: with collectives, a bucket
+        # may run as groups of consecutive tensors, each group its own encode -> sketch
+        # all-reduce -> select -> pack -> packed all-reduce on the exchange stream, so the wire
+        # starts on the first group while later ones are encoded.  Selection is per tensor and
+        # both all-reduces are elementwise: the results are the bucket's bits.  Each group pays
+        # one collective latency, so "auto" groups only the buckets whose all-reduce would
+        # otherwise leave the wire idle: the first after the pipeline drained (nothing in flight)
+        # and the backward's last (its decode is the drain).
+        units = None
+        if (comms and state.async_exchange and marks is None and state.exchange_groups != "off"
+                and (state.exchange_groups == "all" or not pend or bucket.is_last())):
+            units = plan.groups(state.group_bytes)
+        grouped = units is not None
+        if not grouped:
+            units = (plan,)
         # finish first: a caller that skipped buckets, or one whose stream changed since a
         # pending step (its decode is enqueued on that step's own stream)
-        if any(e_[0] is plan or e_[4] != sid for e_ in pend):
+        if any(getattr(e_[0], "parent", e_[0]) is plan or e_[4] != sid for e_ in pend):
             state.flush_exchange()
         # the decode riding in this call's select launch: the previous bucket's without
         # collectives, the one before it with them (its all-reduce has had a whole call to
         # finish, so the select is not held back waiting for it)
         depth = 2 if comms else 1
-        ride = pend.pop(0) if len(pend) >= depth else None
-        fin = pend[:] if not defer else []
-        if not defer:
-            pend.clear()
         ars = None
-        if defer and comms:
+        if comms and (defer or grouped):
             ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
             if pk.kind == "callback" and ars.cuda_stream not in pk._streams:
                 pk.known_stream(ars)
-        marks = _call_marks(state, _EXCHANGE_MARKS)
-        nf = len(fin)
-        if nf:
-            fin_plans = (N.c_void_p * nf)(*[e_[0].handle for e_ in fin])
-            fin_marks = (N.c_void_p * nf)(*[N.ctypes.cast(e_[2], N.c_void_p).value if e_[2] is not None
-                                            else None for e_ in fin])
-        else:  # (most calls: no ctypes arrays built per call)
-            fin_plans = fin_marks = None
-        _ht("prep")
-        st_ = L.arctopk_exchange_step(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
-                                      int(err_in), int(draw), seed,
-                                      nplan.handle if nplan is not None else None, nseed,
-                                      sk.handle if comms else None, pk.handle if comms else None, sid,
-                                      ars.cuda_stream if ars is not None else None, int(defer),
-                                      ride[0].handle if ride is not None else None,
-                                      ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
-                                      vptr, marks)
-        if st_:
-            if comms:
-                for c in (sk, pk):
-                    c.check(st_, "arctopk_exchange_step")
-            N.check(st_, "arctopk_exchange_step")
-        for e_ in ([ride] if ride is not None else []) + fin:  # their decodes are enqueued now
-            e_[1].set_result(e_[3])
+        if defer:
+            fut = ExchangeFuture()
+            fut._arctopk_state = state
+        else:
+            fut = torch.futures.Future()
+        esz = input_tensor.element_size()
+        x_p, e_p, g_p = input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr)
+        nu = len(units)
+        for ui, u in enumerate(units):
+            last_u = ui == nu - 1
+            u_defer = defer if last_u else True  # a group's decode is finished by a later one
+            if grouped:
+                if u.comm_registered is not pk:
+                    sk.register(u.sketch)
+                    pk.register(u.packed)
+                    u.comm_registered = pk
+                off = u.offset * esz
+                u_x, u_e, u_g = x_p + off, (e_p + off if e_p else None), (g_p + off if g_p else None)
+                if device_v:  # V drawn by group 0 and then by each group's select for the next
+                    u_draw = int(draw and ui == 0)
+                    u_next, u_nseed = (units[ui + 1], seed) if (draw and not last_u) else (None, 0)
+                    u_vptr = None
+                else:
+                    u_draw, u_next, u_nseed = 0, None, 0
+                    u_vptr = vptr + u.v_off * esz
+                if last_u:
+                    u_next, u_nseed = nplan, nseed
+            else:
+                u_x, u_e, u_g, u_draw, u_next, u_nseed, u_vptr = x_p, e_p, g_p, draw, nplan, nseed, vptr
+            ride = pend.pop(0) if len(pend) >= depth else None
+            fin = pend[:] if not u_defer else []
+            if not u_defer:
+                pend.clear()
+            nf = len(fin)
+            if nf:
+                fin_plans = (N.c_void_p * nf)(*[e_[0].handle for e_ in fin])
+                fin_marks = (N.c_void_p * nf)(*[N.ctypes.cast(e_[2], N.c_void_p).value if e_[2] is not None
+                                                else None for e_ in fin])
+            else:  # (most calls: no ctypes arrays built per call)
+                fin_plans = fin_marks = None
+            _ht("prep")
+            st_ = L.arctopk_exchange_step(u.handle, u_x, u_e, u_g, ef, int(err_in), int(u_draw), seed,
+                                          u_next.handle if u_next is not None else None, u_nseed,
+                                          sk.handle if comms else None, pk.handle if comms else None, sid,
+                                          ars.cuda_stream if (ars is not None and u_defer) else None,
+                                          int(u_defer), ride[0].handle if ride is not None else None,
+                                          ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
+                                          u_vptr, marks)
+            if st_:
+                if comms:
+                    for c in (sk, pk):
+                        c.check(st_, "arctopk_exchange_step")
+                N.check(st_, "arctopk_exchange_step")
+            for e_ in ([ride] if ride is not None else []) + fin:  # their decodes are enqueued now
+                if e_[1] is not None:
+                    e_[1].set_result(e_[3])
+            if u_defer:
+                pend.append((u, fut if last_u else None, marks, input_tensor, sid, (err, gerr)))
         if nplan is not None:
             nplan.v_drawn, nplan.v_stream = nseed, sid
         if vslot >= 0:
@@ -989,12 +1133,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         _ht("native_step")
         state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
         state.maybe_increase_iter(bucket)
-        if defer:
-            fut = ExchangeFuture()
-            fut._arctopk_state = state
-            pend.append((plan, fut, marks, input_tensor, sid, (err, gerr)))
-        else:
-            fut = torch.futures.Future()
+        if not defer:
             fut.set_result(input_tensor)
         _ht("tail")
         return fut

@@ -30,32 +30,6 @@ void launch_job_kernel(void (*f)(P...), dim3 grid, dim3 block, size_t shm, hipSt
 }
 }  // namespace
 
-DIAG_STAMPS(g_st_keys)
-DIAG_STAMPS(g_st_refine)
-#ifdef ARCTOPK_STAMPS
-extern "C" int arctopk_diag_stamps_k(int which, unsigned long long* host) {
-    return (int)(which == 0 ? hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_keys), sizeof(g_st_keys))
-                            : hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_refine), sizeof(g_st_refine)));
-}
-#endif
-
-#ifndef ARCTOPK_DIAG_KEYS
-#define ARCTOPK_DIAG_KEYS 0  // diagnostic builds only (scripts/selbench.hip): 1 = key pass without
-#endif                       // the histogram merge, 2 = also without the LDS histogram
-#ifndef ARCTOPK_DIAG_STOP
-#define ARCTOPK_DIAG_STOP 0  // diagnostic builds only: 1 = large-segment select stops after the key pass
-#endif
-#ifdef ARCTOPK_SEL_STAMPS  // diagnostic build only (scripts/seltest.hip): phase timestamps
-__device__ unsigned long long g_sel_stamps[64];
-#define SEL_STAMP(i)                                                        \
-    do {                                                                    \
-        __syncthreads();                                                    \
-        if (threadIdx.x == 0 && blockIdx.x == 0) g_sel_stamps[i] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define SEL_STAMP(i) do {} while (0)
-#endif
-
 namespace {
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -338,12 +312,6 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
                 if (st_ == steps - 1) {
 #pragma unroll
                     for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
-#ifdef ARCTOPK_ENC_LANE0_BF16  // A/B: lane 0 stores all R sums
-                    if (lane == 0) {
-#pragma unroll
-                        for (int j = 0; j < R; ++j) put(r_ * R + j, acc[j]);
-                    }
-#else
                     if (lane < R) {
                         float v = acc[0];
 #pragma unroll
@@ -351,7 +319,6 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
                             if (lane == j) v = acc[j];
                         put(r_ * R + lane, v);
                     }
-#endif
 #pragma unroll
                     for (int j = 0; j < R; ++j) acc[j] = 0.f;
                 }
@@ -395,7 +362,7 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
         for (int j = 0; j < R; ++j) acc[j] = 0.f;
         // packed FMAs (v_pk_fma_f32) on the G-only stream (A/B: noef headline encode 57.7 -> 53.1
         // us; with E loads the EF14 encode measured 140 -> 146 us, so those keep scalar FMAs)
-        constexpr bool kPk = ARCTOPK_ENC_PKFMA == 1 || (ARCTOPK_ENC_PKFMA == 2 && !LOAD_E);
+        constexpr bool kPk = !LOAD_E;
         f2_t acc2[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) acc2[j] = f2_t{0.f, 0.f};
@@ -522,13 +489,7 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
     }
 }
 
-// One tile per block, or (ARCTOPK_ENC_GRID_CAP > 0, A/B switch) a grid of at most that many
-// blocks walking the tile table in strides: every block is dispatched at once, so a kernel of
-// another stream (a collective) is not queued behind thousands of encode blocks.
-#ifndef ARCTOPK_ENC_GRID_CAP
-#define ARCTOPK_ENC_GRID_CAP 0
-#endif
-constexpr int kEncGridCap = ARCTOPK_ENC_GRID_CAP;
+// One tile per block.
 template <typename T, int R, int EF, bool ERR_IN>
 __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                                                 const EncTile* __restrict__ tiles, int ntiles,
@@ -537,14 +498,7 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                                                 T* __restrict__ sketch,
                                                 float* __restrict__ part_buf) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    if constexpr (kEncGridCap == 0) {
-        encode_tile<T, R, EF, ERR_IN>(segs, tiles[blockIdx.x], G, E, V, sketch, part_buf, lds);
-    } else {
-        for (int i = (int)blockIdx.x; i < ntiles; i += (int)gridDim.x) {
-            encode_tile<T, R, EF, ERR_IN>(segs, tiles[i], G, E, V, sketch, part_buf, lds);
-            __syncthreads();  // the next tile restages LDS
-        }
-    }
+    encode_tile<T, R, EF, ERR_IN>(segs, tiles[blockIdx.x], G, E, V, sketch, part_buf, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -632,10 +586,6 @@ constexpr int kST = 256;
 constexpr int kCandMax = 256;
 
 constexpr int kRegB = 8;  // register path: rows per thread (n <= kRegB * threads)
-#ifndef ARCTOPK_SEL_REG
-#define ARCTOPK_SEL_REG 1  // tuning switch (A/B builds): 0 = LDS-key path for every small segment
-#endif
-constexpr bool kSelRegPath = ARCTOPK_SEL_REG != 0;
 
 struct SmallSel {
     uint32_t hist[256];
@@ -716,7 +666,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const T* sk = sketch + s.sketch_off;
-    SEL_STAMP(0);
     for (int i = tid; i < 256; i += NT) sh.hist[i] = 0;  // first pass's histogram
     uint32_t key[B];
     if (R == 4 && s.kind == ARCTOPK_SEG_SKETCH && (s.sketch_off & 3) == 0) {
@@ -735,7 +684,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
                                                         R, sc, s.kind))
                                 : 0u;
     }
-    SEL_STAMP(8);
     uint32_t kor = 0u, kand = ~0u;
 #pragma unroll
     for (int u = 0; u < B; ++u)
@@ -760,7 +708,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
         kor |= sh.wor[w];
         kand &= sh.wand[w];
     }
-    SEL_STAMP(1);
     const uint32_t diff = kor ^ kand;
     int bit = diff ? 32 - __clz(diff) : 0;
     uint32_t prefix = kand & ~((bit == 32) ? 0xFFFFFFFFu : ((1u << bit) - 1u));
@@ -781,7 +728,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
             if (u * NT + tid < n && (key[u] & mask) == prefix)
                 atomicAdd(&sh.hist[(key[u] >> shift) & dmask], 1u);
         __syncthreads();
-        SEL_STAMP(5);
         if (wave == 0) {  // lane l owns digits 255-4l .. 252-4l (descending)
             uint32_t c[4], sum = 0;
 #pragma unroll
@@ -840,7 +786,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
             }
             for (int i = (int)nc + tid; i < (int)((nc + 3) & ~3u); i += NT) sh.cand[i] = 0u;  // pad to x4
             __syncthreads();
-            SEL_STAMP(6);
             const uint4* c4 = reinterpret_cast<const uint4*>(sh.cand);
             for (int t = tid; t < (int)nc; t += NT) {
                 const uint32_t v = sh.cand[t];
@@ -859,7 +804,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
                 }
             }
             __syncthreads();
-            SEL_STAMP(7);
             ranked = true;
             break;
         }
@@ -873,7 +817,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
         thr = prefix;
         need_eq = kk;
     }
-    SEL_STAMP(2);
     uint64_t bg[B], be[B];
 #pragma unroll
     for (int u = 0; u < B; ++u) {
@@ -891,7 +834,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
     __syncthreads();
     if (wave == 0) table_exscan2<NW>(sh.tg, sh.te);
     __syncthreads();
-    SEL_STAMP(3);
     int32_t* rl = rowlist + s.sel_off;
     int32_t* sm = slotmap + s.row_off;
 #pragma unroll
@@ -910,7 +852,6 @@ __device__ __forceinline__ void select_small_reg(const SegDev& s, const T* __res
             }
         }
     }
-    SEL_STAMP(4);
 }
 
 template <typename T, int NT>
@@ -922,14 +863,13 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
     __shared__ SmallSel sh;
     const SegDev s = segs[seg_id];
     const int n = (int)s.n;
-    if (kSelRegPath && n <= kRegB * NT) {
+    if (n <= kRegB * NT) {
         select_small_reg<T, NT>(s, sketch, R, sc, rowlist, slotmap, sh);
         return;
     }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int stride = (s.kind == ARCTOPK_SEG_RAW) ? 1 : R;
     const T* sk = sketch + s.sketch_off;
-    SEL_STAMP(0);
     uint32_t kor = 0u, kand = ~0u;
     if (R == 4 && s.kind == ARCTOPK_SEG_SKETCH && (s.sketch_off & 3) == 0) {
         // one quad per row; 8 rows' loads in flight per thread before any use
@@ -974,7 +914,6 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
         kor |= sh.wor[w];
         kand &= sh.wand[w];
     }
-    SEL_STAMP(1);
     // bits [bit-1 .. 0] still vary among matching keys
     const uint32_t diff = kor ^ kand;
     int bit = diff ? 32 - __clz(diff) : 0;
@@ -993,7 +932,6 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
             if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & dmask], 1u);
         }
         __syncthreads();
-        SEL_STAMP(5);
         if (wave == 0) {  // lane l owns digits 255-4l .. 252-4l (descending)
             uint32_t c[4], sum = 0;
 #pragma unroll
@@ -1044,7 +982,6 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
                 if (in) sh.cand[wb + (uint32_t)__popcll(bm & lt)] = key;
             }
             __syncthreads();
-            SEL_STAMP(6);
             const int nc = (int)sh.ncand;
             for (int i = nc + tid; i < ((nc + 3) & ~3); i += NT) sh.cand[i] = 0u;  // pad to x4
             __syncthreads();
@@ -1066,7 +1003,6 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
                 }
             }
             __syncthreads();
-            SEL_STAMP(7);
             ranked = true;
             break;
         }
@@ -1080,7 +1016,6 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
         thr = prefix;
         need_eq = kk;
     }
-    SEL_STAMP(2);
     // index-ordered compaction over contiguous per-thread row ranges (multiples of 4
     // rows, read as 16-B LDS vectors; the key array is padded to a multiple of 4)
     const int per = (((n + NT - 1) / NT) + 3) & ~3;
@@ -1101,7 +1036,6 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
     int64_t take_eq = need_eq - eq_before;
     take_eq = take_eq < 0 ? 0 : (take_eq > eq ? eq : take_eq);
     int64_t slot = block_exscan_s(gt + take_eq, sh.wsum);
-    SEL_STAMP(3);
     int32_t* rl = rowlist + s.sel_off;
     int32_t* sm = slotmap + s.row_off;
     int64_t eq_seen = 0;
@@ -1127,7 +1061,6 @@ __device__ __forceinline__ void select_small_seg(const SegDev* __restrict__ segs
             }
         }
     }
-    SEL_STAMP(4);
 }
 
 template <typename T, int NT>
@@ -1138,10 +1071,6 @@ __global__ void __launch_bounds__(NT) k_select_small(const SegDev* __restrict__ 
                                                       int32_t* __restrict__ slotmap, VDrawJob job) {
     if (maybe_draw_v<T>(job, NT)) return;  // trailing blocks: the next call's projections
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
-#ifdef ARCTOPK_DIAG_SEL_TWICE  // diagnostic builds only: second pass runs with a warm I-cache
-    select_small_seg<T, NT>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, keys);
-    __syncthreads();
-#endif
     select_small_seg<T, NT>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, keys);
 }
 
@@ -1325,11 +1254,9 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
         v[q] = lane < cap ? src[(int64_t)r * it.range + lane] : 0u;
         if constexpr (kRefinePre > 64) v2[q] = lane + 64 < cap ? src[(int64_t)r * it.range + 64 + lane] : 0u;
     }
-    if constexpr (kArcLocalDigit) {
-        // every reader of the key pass's histogram (the compact launch) is done: zero it for
-        // the next key pass
-        for (int i = tid; i < kMBins; i += NT) ws->hist[t][i] = 0u;
-    }
+    // every reader of the key pass's histogram (the compact launch) is done: zero it for the
+    // next key pass
+    for (int i = tid; i < kMBins; i += NT) ws->hist[t][i] = 0u;
     const uint32_t gt_above = tid < nr ? gt_raw : 0u;  // keys above the bin
     const uint32_t my_cnt = tid < nr ? cnt_raw : 0u;
     const uint32_t my_tail = my_cnt > (uint32_t)kRefinePre ? my_cnt - (uint32_t)kRefinePre : 0u;
@@ -1405,7 +1332,6 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
         }
         __syncthreads();
     }
-    DIAG_STAMP(g_st_refine, 2);
     auto key_at = [&](int64_t i) -> uint32_t { return staged ? stage[i] : src[gidx((uint32_t)i)]; };
     while (s.bit > 0) {
         const int w = s.bit < W2 ? s.bit : W2;
@@ -1442,7 +1368,6 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
         s.bit = shift;
         __syncthreads();  // s_digit / s_acc / h are rewritten by the next round
     }
-    DIAG_STAMP(g_st_refine, 3);
     const uint32_t T = s.prefix;
     const uint32_t* cgt;  // per-range candidates above / equal to T
     const uint32_t* ceq;
@@ -1501,7 +1426,6 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
         ceq = roff;
     }
     __syncthreads();
-    DIAG_STAMP(g_st_refine, 4);
     const int r = tid;
     const uint32_t gt = (tid < nr ? cgt[tid] : 0u) + gt_above;
     const uint32_t eq = tid < nr ? ceq[tid] : 0u;
@@ -1516,7 +1440,6 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
     }
     if (tid == 0) {
         ws->st[t] = s;  // the write pass reads the threshold (prefix)
-        arc_win_update(ws, it.win, s.prefix);  // the next call's first-digit window
     }
 }
 
@@ -1533,25 +1456,17 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __r
                                                                Scale sc, int32_t* __restrict__ rowlist,
                                                                int32_t* __restrict__ slotmap,
                                                                VDrawJob job) {
-    DIAG_STAMP(g_st_refine, 0);
     if (maybe_draw_v<T>(job, kRefineThreads)) {
-        DIAG_STAMP(g_st_refine, 1);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     const MBatch& b = *bp;
     if ((int)blockIdx.x < b.cnt) {
-#ifdef ARCTOPK_DIAG_REFINE_TWICE  // diagnostic builds only: the second pass runs warm
-        arc_refine_item(b, (int)blockIdx.x, ws, ckey, dyn);
-        __syncthreads();
-        DIAG_STAMP(g_st_refine, 5);
-#endif
         arc_refine_item(b, (int)blockIdx.x, ws, ckey, dyn);
     }
     else
         select_small_seg<T, kRefineThreads>(segs, small_ids[blockIdx.x - b.cnt], sketch, R, sc, rowlist,
                                             slotmap, dyn);
-    DIAG_STAMP(g_st_refine, 1);
 }
 
 // ---- the refine folded into the write pass (items of up to kFuseMaxRows rows) ----
@@ -1584,7 +1499,6 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     const uint32_t* src = ckey + it.cand_off;
     const int64_t r0 = (int64_t)r * it.range;
     const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
-    DIAG_STAMP(g_st_refine, 0);
     // one round trip: the first-pass state, the per-range counts and this range's first tile
     MState s = ws->st[t];
     uint32_t cc[PR], cg[PR], kor = 0u, kand = ~0u;
@@ -1682,7 +1596,6 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
             }
         }
     };
-    DIAG_STAMP(g_st_refine, 2);
     while (s.bit > 0) {
         const int w = s.bit < W2 ? s.bit : W2;
         const int shift = s.bit - w;
@@ -1723,9 +1636,7 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
         s.bit = shift;
         __syncthreads();  // s_digit / s_acc / h are rewritten by the next round
     }
-    DIAG_STAMP(g_st_refine, 3);
     const uint32_t T = s.prefix;
-    if (r == 0 && tid == 0) arc_win_update(ws, it.win, T);  // the next call's first-digit window
     // candidates before this range (> T, == T) and this range's == T
     const uint32_t cb = roff[r], ce = r + 1 < nr ? roff[r + 1] : nc32;
     uint32_t gb = 0, eb = 0, eo = 0;
@@ -1752,7 +1663,6 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
     take = take < 0 ? 0 : (take > (int64_t)teo ? (int64_t)teo : take);
     uint32_t take_left = (uint32_t)take;
     int64_t run = (int64_t)gabove + tgb + min<int64_t>(kk, (int64_t)teb);
-    DIAG_STAMP(g_st_refine, 4);
     // the write of this range (k_arc_write's body): ballot compaction in index order
     for (int64_t tile = r0; tile < r1; tile += kMTile) {
         const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
@@ -1802,10 +1712,6 @@ __device__ __forceinline__ void arc_write_fused_range(const MItem it, int t, int
         run += tgt + te;
         take_left -= te;
     }
-#ifdef ARCTOPK_STAMPS
-    __syncthreads();
-#endif
-    DIAG_STAMP(g_st_refine, 1);
 }
 
 // A deferred decode (an earlier bucket's, arctopk_exchange_step's `ride`) riding in a launch of
@@ -1872,8 +1778,7 @@ struct KeysGrid {
 // the multi-block select (mselect.h): each block histograms its keys' top 12 bits in LDS
 // and merges the non-empty bins into the segment's global histogram.  The bin holding the
 // k-th largest key is then derived from that histogram by each block of the next launches
-// (ms_arc_digit_local; with ARCTOPK_ARC_LOCAL_DIGIT=0, by this kernel's last block:
-// ms_arc_first_digit).
+// (ms_arc_digit_local).
 template <typename T, int KT>
 __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs,
                                                   const int32_t* __restrict__ ids, int first,
@@ -1884,17 +1789,12 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
     // LDS sets the occupancy, and every block of the grid must be resident in one round
     __shared__ uint32_t h[kMBins];
     __shared__ uint32_t s_nnz;
-    DIAG_STAMP(g_st_keys, 0);
     // flat grid: item t owns blocks [kg.first[t], kg.first[t + 1])
     int t = 0;
     while ((int)blockIdx.x >= kg.first[t + 1]) ++t;
     const int bx = (int)blockIdx.x - kg.first[t];
     const uint32_t nblk = (uint32_t)(kg.first[t + 1] - kg.first[t]);
     const SegDev s = segs[ids[first + t]];
-    const ArcWin w = arc_win(ws, first + t < kMWin ? first + t : -1);  // (plan: MItem::win)
-#ifdef ARCTOPK_STAMPS
-    if (threadIdx.x == 0) g_st_keys[blockIdx.x * 8 + 4] = (unsigned long long)t;
-#endif
     for (int i = threadIdx.x; i < kMBins; i += KT) h[i] = 0u;
     if (threadIdx.x == 0) s_nnz = 0u;
     __syncthreads();
@@ -1903,12 +1803,11 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
     int64_t row = (int64_t)bx * KT + threadIdx.x;
     const T* sk = sketch + s.sketch_off;
     uint32_t* kout = keys + s.row_off;
-    // The two edge bins are counted in registers: they can be hot (a first-digit window puts every
-    // key below it in bin 0, ~10 % of a 1x1-conv item; tied zero rows all land in bin 0), and
-    // LDS atomics of a wave on ONE word serialise (measured: a window cost the select 16 us)
+    // The two edge bins are counted in registers: they can be hot (tied zero rows all land in
+    // bin 0), and LDS atomics of a wave on ONE word serialise
     uint32_t c_lo = 0, c_hi = 0;
     auto count = [&](uint32_t key) {
-        const uint32_t dg = arc_digit(key, w);
+        const uint32_t dg = arc_digit(key);
         if (dg == 0u) ++c_lo;
         else if (dg == (uint32_t)kMBins - 1u) ++c_hi;
         else atomicAdd(&h[dg], 1u);
@@ -1925,9 +1824,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
                 if (rr < s.n) {
                     const uint32_t key = energy_key(energy4<T>(v[u].x, v[u].y, v[u].z, v[u].w, sc));
                     kout[rr] = key;
-#if ARCTOPK_DIAG_KEYS < 2
                     count(key);
-#endif
                 }
             }
         }
@@ -1956,11 +1853,6 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
         if (c_hi) atomicAdd(&h[kMBins - 1], c_hi);
     }
     __syncthreads();
-    DIAG_STAMP(g_st_keys, 1);
-#if ARCTOPK_DIAG_KEYS >= 1  // diagnostic builds (scripts/selbench.hip): stop after the LDS pass
-    if (h[threadIdx.x] == 12345678u) kout[0] = 0u;
-    return;
-#endif
     // Merge into the item's global histogram.  Memory-side atomics cost about one wave
     // instruction per 50 ns per CU whatever their lane count, so the non-empty bins are first
     // compacted into a dense LDS list (in place: bin << 20 | count, counts < 2^20 rows per
@@ -1993,17 +1885,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
         for (int i = threadIdx.x; i < kMBins; i += KT)
             if (h[i]) atomicAdd(&ws->hist[t][hist_slot(i)], h[i]);
     }
-    DIAG_STAMP(g_st_keys, 2);
-    if constexpr (kArcLocalDigit) {  // the compact and refine blocks derive the digit themselves
-        DIAG_STAMP(g_st_keys, 3);
-        return;
-    }
-    if (!ms_arrive_last(&ws->done[t].v, nblk)) {
-        DIAG_STAMP(g_st_keys, 3);
-        return;
-    }
-    ms_arc_first_digit<KT>(ws, t, s.k_rows, w, h);
-    DIAG_STAMP(g_st_keys, 3);
+    // (the compact and refine blocks derive the bin of the k-th key from the merged histogram)
 }
 
 __device__ __forceinline__ bool row_path(const SegDev& s) { return s.vec && s.m >= 256; }
@@ -2036,19 +1918,6 @@ __device__ __forceinline__ float4 pack4(const T* __restrict__ G, T* __restrict__
     return v;
 }
 
-#ifndef ARCTOPK_PACK_FULL_QUADS
-#define ARCTOPK_PACK_FULL_QUADS 1  // tuning switch (A/B builds): 0 = rewrite only quads with a selected row
-#endif
-constexpr bool kPackFullQuads = ARCTOPK_PACK_FULL_QUADS != 0;
-#ifndef ARCTOPK_PACK_PAIRS
-#define ARCTOPK_PACK_PAIRS 1  // tuning switch (A/B builds): 0 = scalar gathers for even short rows
-#endif
-constexpr bool kPackPairs = ARCTOPK_PACK_PAIRS != 0;
-#ifndef ARCTOPK_PACK_QUADS
-#define ARCTOPK_PACK_QUADS 0  // tuning switch (A/B builds): 1 = 16-B quads for even short rows (measured
-                              // slower: 28 x [512,512,3,3] pack 60 -> 80 us)
-#endif
-constexpr bool kPackQuads = ARCTOPK_PACK_QUADS != 0;
 
 // Pack of a row range of an m in {1, 2} fp32 segment (Chunk mode 1): lane per 16-B quad of
 // the segment (4 / 2 rows), slot map read alongside; selected rows go to packed[slot * m],
@@ -2096,7 +1965,6 @@ __device__ __forceinline__ void pack_stream_small(const SegDev& s, const Chunk& 
             const float gv[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
             const float ev[4] = {e[u].x, e[u].y, e[u].z, e[u].w};
             float en[4] = {ev[0], ev[1], ev[2], ev[3]};
-            bool any = false;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int rj = j / m;  // row of element j within the quad
@@ -2113,18 +1981,15 @@ __device__ __forceinline__ void pack_stream_small(const SegDev& s, const Chunk& 
                         en[j] = ev[j] + v;
                     }
                     pk[(int64_t)slot * m + (j - rj * m)] = v;
-                    any = true;
                 }
             }
             if constexpr (EF != ARCTOPK_EF_NONE) {
                 // every quad rewritten (unchanged values where no row is selected): whole
                 // lines leave L2 instead of masked partial writes (read-modify-write at HBM)
-                if (any || kPackFullQuads) {
-                    if (el + 4 <= seg_end) {
-                        *reinterpret_cast<float4*>(E + el) = make_float4(en[0], en[1], en[2], en[3]);
-                    } else {
-                        for (int j = 0; j < 4 && el + j < seg_end; ++j) E[el + j] = en[j];
-                    }
+                if (el + 4 <= seg_end) {
+                    *reinterpret_cast<float4*>(E + el) = make_float4(en[0], en[1], en[2], en[3]);
+                } else {
+                    for (int j = 0; j < 4 && el + j < seg_end; ++j) E[el + j] = en[j];
                 }
             }
         }
@@ -2214,86 +2079,7 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
         }
         const uint32_t cnt = (uint32_t)(nr * m);
         const int64_t dbase = s.packed_off + ch.row0 * m;
-        if constexpr (sizeof(T) == 4 && kPackQuads) {
-            if ((m & 1) == 0 && (s.offset & 1) == 0) {
-                // even m (3x3 / 5x5 conv rows, 72 / 200 B; rows start 8-B aligned): each row is
-                // read -- and EF14 / EF21 rewritten -- as the 16-B quads of the bucket that
-                // cover it (their first / last may hold half a neighbour row: loaded, never
-                // stored), so a 72-B row costs 5 quad loads and 5 stores instead of 9 + 9 of
-                // 8 B (the counter profile had this pack stalled at instruction issue); the
-                // packed values leave as 8-B pairs (a row's packed position is 8-B aligned).
-                const int nq = (m + 5) >> 2;  // quads a row spans at most
-                const uint32_t units = (uint32_t)(nr * nq);
-                const uint32_t qmagic = (uint32_t)(((1ull << 32) + (uint64_t)nq - 1) / (uint64_t)nq);
-                const int64_t seg_end = s.offset + s.n * m;
-                const float* Gf = reinterpret_cast<const float*>(G);
-                float* Ef = reinterpret_cast<float*>(E);
-                float* df = reinterpret_cast<float*>(dst);
-                constexpr int Q = 8;
-                for (uint32_t u0 = threadIdx.x; u0 < units; u0 += 256 * Q) {
-                    int64_t qa[Q];
-                    int lo[Q], hi[Q], jr[Q];  // in-row elements [lo, hi) of the quad; row of the chunk
-                    float4 va[Q], vb[Q];
-#pragma unroll
-                    for (int u = 0; u < Q; ++u) {
-                        const uint32_t un = min(u0 + u * 256, units - 1);
-                        const uint32_t j = div32(un, qmagic);
-                        const int q = (int)(un - j * (uint32_t)nq);
-                        const int64_t s0 = s.offset + (int64_t)rs[j] * m;
-                        qa[u] = (s0 & ~(int64_t)3) + 4 * q;
-                        lo[u] = (int)max<int64_t>(0, s0 - qa[u]);
-                        hi[u] = (int)min<int64_t>(4, s0 + m - qa[u]);
-                        jr[u] = (int)j;
-                    }
-#pragma unroll
-                    for (int u = 0; u < Q; ++u) {
-                        // whole quad when it lies inside the segment, else only the in-row half
-                        const bool whole = qa[u] + 4 <= seg_end && qa[u] >= s.offset;
-                        const int64_t h = qa[u] + (lo[u] ? 2 : 0);
-                        if constexpr (EF != ARCTOPK_EF14) {
-                            if (whole) va[u] = *reinterpret_cast<const float4*>(Gf + qa[u]);
-                            else if (hi[u] > lo[u]) {
-                                const float2 t2 = *reinterpret_cast<const float2*>(Gf + h);
-                                va[u] = lo[u] ? make_float4(0.f, 0.f, t2.x, t2.y) : make_float4(t2.x, t2.y, 0.f, 0.f);
-                            }
-                        }
-                        if constexpr (EF != ARCTOPK_EF_NONE) {
-                            if (whole) vb[u] = *reinterpret_cast<const float4*>(Ef + qa[u]);
-                            else if (hi[u] > lo[u]) {
-                                const float2 t2 = *reinterpret_cast<const float2*>(Ef + h);
-                                vb[u] = lo[u] ? make_float4(0.f, 0.f, t2.x, t2.y) : make_float4(t2.x, t2.y, 0.f, 0.f);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < Q; ++u) {
-                        if (u0 + u * 256 >= units || hi[u] <= lo[u]) continue;  // (a quad past the row)
-                        float4 v, en;
-                        if constexpr (EF == ARCTOPK_EF_NONE) {
-                            v = va[u];
-                        } else if constexpr (EF == ARCTOPK_EF14) {
-                            v = vb[u];
-                            en = make_float4(0.f, 0.f, 0.f, 0.f);
-                        } else {
-                            v = make_float4(va[u].x - vb[u].x, va[u].y - vb[u].y, va[u].z - vb[u].z, va[u].w - vb[u].w);
-                            en = add4(vb[u], v);
-                        }
-                        if constexpr (EF != ARCTOPK_EF_NONE) {
-                            if (lo[u] == 0 && hi[u] == 4) *reinterpret_cast<float4*>(Ef + qa[u]) = en;
-                            else if (lo[u]) *reinterpret_cast<float2*>(Ef + qa[u] + 2) = make_float2(en.z, en.w);
-                            else *reinterpret_cast<float2*>(Ef + qa[u]) = make_float2(en.x, en.y);
-                        }
-                        // packed position of the quad's first in-row element
-                        const int64_t s0 = s.offset + (int64_t)rs[jr[u]] * m;
-                        const int64_t pp = (int64_t)jr[u] * m + (qa[u] + lo[u] - s0);
-                        if (lo[u] == 0) *reinterpret_cast<float2*>(df + pp) = make_float2(v.x, v.y);
-                        if (hi[u] == 4) *reinterpret_cast<float2*>(df + pp + (lo[u] ? 0 : 2)) = make_float2(v.z, v.w);
-                    }
-                }
-                return;
-            }
-        }
-        if constexpr (sizeof(T) == 4 && kPackPairs) {
+        if constexpr (sizeof(T) == 4) {
             if ((m & 1) == 0 && (s.offset & 1) == 0) {
                 // even m (3x3 / 5x5 conv rows, 72 / 200 B): 8-B units.  Every unit lies in one
                 // row and both ends are 8-B aligned, so a wave's loads cover ~512 contiguous
@@ -2517,36 +2303,19 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
         const int np = nsel * m;
         const T* pkc = pk + (int64_t)f0 * m;
         int32_t* lmap = reinterpret_cast<int32_t*>(dlds);
-        float* lpk = dlds + ((nr + 3) & ~3);  // (16-B aligned: quad stores)
+        float* lpk = dlds + ((nr + 3) & ~3);
         int32_t sv[UR];
-        [[maybe_unused]] float pv[UP];
-        constexpr int UQ = UP / 4 + 1;  // quads per thread: the range plus up to 3 lead values
-        [[maybe_unused]] float4 pq[UQ];
+        float pv[UP];
         [[maybe_unused]] float4 gq[UG];
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
             const int r = (int)threadIdx.x + u * 256;
             sv[u] = r < nr ? sm[r] : -1;
         }
-        // fp32: the packed range as the 16-B quads of the (16-B aligned) packed buffer that
-        // cover it -- a quarter of the load instructions; `lead` values of the first quad
-        // precede the range (the buffer is a whole number of quads: no read past its end)
-        constexpr bool vecp = sizeof(T) == 4 && ARCTOPK_SHORT3_VEC;
-        const int lead = vecp ? (int)((s.packed_off + (int64_t)f0 * m) & 3) : 0;
-        const int nq = (np + lead + 3) >> 2;
-        if constexpr (vecp) {
-            const float4* pq0 = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(pkc) - lead);
 #pragma unroll
-            for (int u = 0; u < UQ; ++u) {
-                const int q = (int)threadIdx.x + u * 256;
-                pq[u] = q < nq ? pq0[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < UP; ++u) {
-                const int p = (int)threadIdx.x + u * 256;
-                pv[u] = p < np ? to_f(pkc[p]) : 0.f;
-            }
+        for (int u = 0; u < UP; ++u) {
+            const int p = (int)threadIdx.x + u * 256;
+            pv[u] = p < np ? to_f(pkc[p]) : 0.f;
         }
         if constexpr (EF == ARCTOPK_EF21) {
 #pragma unroll
@@ -2566,19 +2335,10 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
             const int r = (int)threadIdx.x + u * 256;
             if (r < nr) lmap[r] = sv[u] >= 0 ? sv[u] - f0 : -1;
         }
-        if constexpr (vecp) {
-            float4* lq = reinterpret_cast<float4*>(lpk);  // lpk[lead + p]: packed value p
 #pragma unroll
-            for (int u = 0; u < UQ; ++u) {
-                const int q = (int)threadIdx.x + u * 256;
-                if (q < nq) lq[q] = pq[u];
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < UP; ++u) {
-                const int p = (int)threadIdx.x + u * 256;
-                if (p < np) lpk[p] = pv[u];
-            }
+        for (int u = 0; u < UP; ++u) {
+            const int p = (int)threadIdx.x + u * 256;
+            if (p < np) lpk[p] = pv[u];
         }
         __syncthreads();
 #pragma unroll
@@ -2595,7 +2355,7 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
                 const int sl = lmap[r];
                 sel[j] = sl >= 0 && sl < nsel && e + j < cnt;
                 any = any || sel[j];
-                float v = sel[j] ? mean1(lpk[lead + sl * m + c]) : 0.f;
+                float v = sel[j] ? mean1(lpk[sl * m + c]) : 0.f;
                 if constexpr (EF == ARCTOPK_EF21) {
                     const float g = j == 0 ? gq[u].x : j == 1 ? gq[u].y : j == 2 ? gq[u].z : gq[u].w;
                     v = sel[j] ? rnd<T>(g + v) : g + 0.f;
@@ -3060,7 +2820,7 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
     if (p->n_enc > 0) {
         const bool use_e = p->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
         const int nt = use_e ? p->n_enc_e : p->n_enc;
-        dim3 grid(kEncGridCap > 0 ? std::min(nt, kEncGridCap) : nt), block(256);
+        dim3 grid(nt), block(256);
         const size_t lds = (size_t)p->enc_lds_bytes;
         const EncTile* tiles = use_e ? p->d_enc_e : p->d_enc;
         float* pb = p->d_part;
@@ -3170,11 +2930,8 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
     *drawn = false;
     if (rode) *rode = false;
     const T* sketch = static_cast<const T*>(sketch_);
-#ifndef ARCTOPK_DIAG_NOSMALL
-#define ARCTOPK_DIAG_NOSMALL 0  // diagnostic builds only: skip the single-block select
-#endif
     // with large segments, the small segments' selects run inside the first batch's refine
-    if (p->n_small && !ARCTOPK_DIAG_NOSMALL && p->n_large_batches == 0) {
+    if (p->n_small && p->n_large_batches == 0) {
         // one block per segment: 1024 threads once a segment has more than 4096 rows (the
         // radix rounds and the compaction are per-block latency chains)
         constexpr int64_t big_rows = ARCTOPK_SEL_BIG_ROWS;  // rows for 1024 threads (build-time A/B)
@@ -3225,21 +2982,14 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         else
             hipLaunchKernelGGL((k_arc_keys<T, 1024>), dim3(kg.first[b.cnt]), dim3(1024), 0, st, p->d_segs,
                                p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg);
-#if ARCTOPK_DIAG_STOP == 1 || ARCTOPK_DIAG_KEYS >= 1  // diagnostic builds only
-        continue;
-#endif
         int e = ms_arc_compact(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, st);
         if (e) return e;
-#if ARCTOPK_DIAG_STOP == 2  // diagnostic builds only: stop after the compact pass
-        continue;
-#endif
-        const int nsm = (bi == 0 && !ARCTOPK_DIAG_NOSMALL) ? p->n_small : 0;
+        const int nsm = bi == 0 ? p->n_small : 0;
         VDrawJob bj = job;
         if (bi != 0) bj.n = 0;
         uint32_t* ckey = reinterpret_cast<uint32_t*>(p->d_mws + 1);
         // items of at most kFuseMaxRows rows: the refine runs inside the write blocks (one
         // launch fewer)
-        constexpr bool fuse_ok = ARCTOPK_FUSED_WRITE != 0;  // build-time A/B switch
         // ... and only while every write block is resident at once: each one carries a refine,
         // so a second round of blocks costs more than the refine launch it saves (28 x [512,
         // 512, 3, 3] as 896 one-range blocks: select 63 -> 74 us; spans of several ranges per
@@ -3249,7 +2999,7 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         // The small selects sharing the launch run as 256-thread blocks: only when none has
         // more than 4,096 rows (1,024-thread blocks select 8 K-row segments faster than these
         // write blocks finish: ResNet-18's third DDP bucket measured 250 -> 241 GB/s fused)
-        if (fuse_ok && maxn <= kFuseMaxRows && nflat + nsm + bj.n <= kFuseMaxBlocks &&
+        if (maxn <= kFuseMaxRows && nflat + nsm + bj.n <= kFuseMaxBlocks &&
             (nsm == 0 || p->small_lds <= 4096 * 4 + 16)) {
             size_t shm = std::max<size_t>((size_t)kFuseCap * 4, nsm ? (size_t)p->small_lds : 0);
             // the deferred decode rides in the last batch's launch (its blocks come after the
@@ -3325,6 +3075,45 @@ int launch_pack(const arctopk_plan* p, int c0, int c1, const void* grad_, void* 
     return (int)hipGetLastError();
 }
 
+// The mode-3 decode chunk table from a slot map alone (the public decode entry points): for
+// mode-3 segment s (one block each), entry dchunk0 + l, l in [0, nch], is the bucket-wide index
+// of the first selected row at or after row l * CR -- sel_off plus the selected rows before
+// it -- exactly what the pack writes (k_pack, small-m branch); entry nch is the next segment's
+// first, written alike by both segments when that one is mode 3 too.
+__global__ void __launch_bounds__(256) k_dfirst(const SegDev* __restrict__ segs, const int32_t* __restrict__ m3,
+                                                const int32_t* __restrict__ slotmap, int32_t* __restrict__ dfirst) {
+    const SegDev s = segs[m3[blockIdx.x]];
+    const int64_t CR = s.dchunk_rows;
+    const int64_t nch = (s.n + CR - 1) / CR;
+    const int32_t* sm = slotmap + s.row_off;
+    __shared__ int32_t wsum[4];
+    int32_t carry = (int32_t)s.sel_off;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t l0 = 0; l0 <= nch; l0 += 256) {
+        const int64_t l = l0 + threadIdx.x;
+        int32_t cnt = 0;
+        if (l < nch)
+            for (int64_t r = l * CR, re = min(s.n, (l + 1) * CR); r < re; ++r) cnt += sm[r] >= 0 ? 1 : 0;
+        int32_t x = cnt;  // inclusive scan over the wave, then over the block's 4 waves
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        int32_t before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            if (w < wave) before += wsum[w];
+            total += wsum[w];
+        }
+        if (l <= nch) dfirst[s.dchunk0 + l] = carry + before + x - cnt;
+        carry += total;
+        __syncthreads();
+    }
+}
+
 // `done` as in pack_launch (the decode after an inline all-reduce, watched by exchange.cpp)
 template <typename T, int EF>
 void decode_launch(dim3 grid, size_t lds, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
@@ -3338,8 +3127,9 @@ void decode_launch(dim3 grid, size_t lds, hipStream_t st, hipEvent_t done, const
 }
 
 template <typename T>
-int launch_decode(const arctopk_plan* p, int c0, int c1, const void* packed_, const int32_t* slotmap,
-                  int32_t ws, int32_t ef, void* gerr_, void* out_, hipStream_t st, hipEvent_t done = nullptr) {
+int launch_decode(const arctopk_plan* p, int c0, int c1, const int32_t* dfirst, const void* packed_,
+                  const int32_t* slotmap, int32_t ws, int32_t ef, void* gerr_, void* out_, hipStream_t st,
+                  hipEvent_t done = nullptr) {
     const T* packed = static_cast<const T*>(packed_);
     T* gerr = static_cast<T*>(gerr_);
     T* out = static_cast<T*>(out_);
@@ -3348,10 +3138,10 @@ int launch_decode(const arctopk_plan* p, int c0, int c1, const void* packed_, co
     const Scale sc = make_scale(ws);
     const size_t lds = (size_t)p->dec_lds_bytes;
     if (ef == ARCTOPK_EF21)
-        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, p->d_dfirst + c0, packed, slotmap, sc, gerr,
+        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, dfirst + c0, packed, slotmap, sc, gerr,
                                        out);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, p->d_dfirst + c0, packed, slotmap, sc,
+        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, dfirst + c0, packed, slotmap, sc,
                                           gerr, out);
     else
         return ARCTOPK_EINVAL;
@@ -3558,8 +3348,17 @@ extern "C" int arctopk_decode_segments(const arctopk_plan* p, int32_t seg_begin,
     const int c0 = p->h_dec_begin[seg_begin], c1 = p->h_dec_begin[seg_end];
     if (c1 == c0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (p->dtype == ARCTOPK_BF16) return launch_decode<bf16_t>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st);
-    return launch_decode<float>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st);
+    // mode-3 chunks read their packed range from a chunk table; the one the plan's pack writes
+    // describes the pack's own row list, so here it is derived from the slot map given (the
+    // caller may hand any slot map and packed buffer of arctopk_select / arctopk_pack's format)
+    if (p->n_m3) {
+        hipLaunchKernelGGL(k_dfirst, dim3(p->n_m3), dim3(256), 0, st, p->d_segs, p->d_m3, slotmap, p->d_dfirst_pub);
+        const hipError_t he = hipGetLastError();
+        if (he != hipSuccess) return (int)he;
+    }
+    if (p->dtype == ARCTOPK_BF16)
+        return launch_decode<bf16_t>(p, c0, c1, p->d_dfirst_pub, packed, slotmap, ws, ef, gerr, out, st);
+    return launch_decode<float>(p, c0, c1, p->d_dfirst_pub, packed, slotmap, ws, ef, gerr, out, st);
 }
 
 extern "C" int arctopk_decode(const arctopk_plan* p, const void* packed, const int32_t* slotmap,
@@ -3605,18 +3404,20 @@ int decode_pair(const arctopk_plan* pa, int32_t ws_a, int32_t ef_a, void* gerr_a
     return launch_decode_pair<float>(a, b, st, (hipEvent_t)done);
 }
 
-// arctopk_decode whose kernel completes `done` (exchange.cpp)
+// The whole-bucket decode of the packed values and slot map this plan's own last pack wrote
+// (its chunk table, d_dfirst, describes them); `done` (may be null): an event the kernel
+// completes (exchange.cpp)
 int decode_signal(const arctopk_plan* p, const void* packed, const int32_t* slotmap, int32_t ws, int32_t ef,
                   void* gerr, void* out, void* stream, void* done) {
-    if (!p || !packed || !slotmap || !out || ws < 1 || !done) return ARCTOPK_EINVAL;
+    if (!p || !packed || !slotmap || !out || ws < 1) return ARCTOPK_EINVAL;
     if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
     if (ef == ARCTOPK_EF21 && !gerr) return ARCTOPK_EINVAL;
     const int c0 = p->h_dec_begin[0], c1 = p->h_dec_begin[p->nseg];
     hipStream_t st = (hipStream_t)stream;
-    if (c1 == c0) return (int)hipEventRecord((hipEvent_t)done, st);
+    if (c1 == c0) return done ? (int)hipEventRecord((hipEvent_t)done, st) : 0;
     if (p->dtype == ARCTOPK_BF16)
-        return launch_decode<bf16_t>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
-    return launch_decode<float>(p, c0, c1, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
+        return launch_decode<bf16_t>(p, c0, c1, p->d_dfirst, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
+    return launch_decode<float>(p, c0, c1, p->d_dfirst, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
 }
 }  // namespace arctopk
 
@@ -3736,7 +3537,7 @@ extern "C" int arctopk_step(const arctopk_plan* p, void* bucket, void* err, void
     if (!e) e = step_mark(marks, ARCTOPK_MARK_SELECT, st);
     if (!e) e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, st);
     if (!e) e = step_mark(marks, ARCTOPK_MARK_PACK, st);
-    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, 1, ef, gerr, bucket, st);
+    if (!e) e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, 1, ef, gerr, bucket, st, nullptr);
     if (!e) e = step_mark(marks, ARCTOPK_MARK_DECODE, st);
     return e;
 }

@@ -5,22 +5,8 @@
 
 #include "arctopk.h"
 
-// Diagnostic builds only (-DARCTOPK_STAMPS, scripts/selbench.hip): per-block timestamps of
-// the multi-block select kernels, [block][8 slots] in 100 MHz ticks (s_memrealtime).
-#ifdef ARCTOPK_STAMPS
-#define DIAG_STAMPS(name) __device__ unsigned long long name[4096 * 8];
-#define DIAG_STAMP(arr, i)                                                                    \
-    do {                                                                                      \
-        if (threadIdx.x == 0 && blockIdx.x < 4096)                                            \
-            arr[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                     \
-    } while (0)
-#else
-#define DIAG_STAMPS(name)
-#define DIAG_STAMP(arr, i) do {} while (0)
-#endif
-
-// Build-time A/B switches (build(defines=[...]) makes variants; the product library has
-// no run-time tuning knobs).  Selects:
+// Build-time tuning constants (build(defines=[...]) makes A/B variants; the product library
+// has no run-time tuning knobs and one code path per feature).  Selects:
 #ifndef ARCTOPK_SEL_BIG_ROWS
 #define ARCTOPK_SEL_BIG_ROWS 4096      // single-block select: 1024 threads above this many rows
 #endif
@@ -39,14 +25,8 @@
 #ifndef ARCTOPK_FUSE_MAX_ROWS
 #define ARCTOPK_FUSE_MAX_ROWS 262144   // largest item whose refine runs in the write blocks
 #endif
-#ifndef ARCTOPK_QUAD_DEC
-#define ARCTOPK_QUAD_DEC 1             // short-row (4 <= m < 256) fp32 decode: lane per output quad
-#endif                                 // (0: the chunk composed in an LDS tile)
 #ifndef ARCTOPK_QUAD_DEC_CHUNK
-#define ARCTOPK_QUAD_DEC_CHUNK 8192    // ... elements per chunk
-#endif
-#ifndef ARCTOPK_FUSED_WRITE
-#define ARCTOPK_FUSED_WRITE 1          // refine folded into the write blocks where it fits
+#define ARCTOPK_QUAD_DEC_CHUNK 8192    // short-row (4 <= m < 256) fp32 decode, lane per output quad: elements per chunk
 #endif
 #ifndef ARCTOPK_TOPK_HIST_BLOCKS
 #define ARCTOPK_TOPK_HIST_BLOCKS 1024  // TopK select: histogram blocks per batch
@@ -67,16 +47,9 @@
 #ifndef ARCTOPK_SHORT_DEC_CHUNK
 #define ARCTOPK_SHORT_DEC_CHUNK 4096   // elements per short-row (m < 256) decode chunk
 #endif
-#ifndef ARCTOPK_SHORT3_DEC
-#define ARCTOPK_SHORT3_DEC 1           // short-row decode (4 <= m < 256, quad-aligned tensors): mode 3
-#endif
 #ifndef ARCTOPK_SHORT3_CHUNK
-#define ARCTOPK_SHORT3_CHUNK 4096      // ... elements per chunk at most (LDS: 4 (m + 1) / m B each)
-#endif
-#ifndef ARCTOPK_SHORT3_VEC
-#define ARCTOPK_SHORT3_VEC 0           // tuning switch (A/B builds): 1 = the mode-3 decode loads its
-                                       // packed range (fp32) as 16-B quads
-#endif
+#define ARCTOPK_SHORT3_CHUNK 4096      // short-row decode of quad-aligned tensors (mode 3): elements per
+#endif                                 // chunk at most (LDS: 4 (m + 1) / m B each)
 #ifndef ARCTOPK_ENC_TARGET_BLOCKS_E
 #define ARCTOPK_ENC_TARGET_BLOCKS_E 4096  // ... for the fp32 kernels that also stream E (large tensors)
 #endif
@@ -90,26 +63,14 @@
 #ifndef ARCTOPK_ENC_ROWS_MULT
 #define ARCTOPK_ENC_ROWS_MULT 1        // rows per wave-per-row encode tile rounded up to a multiple
 #endif
-#ifndef ARCTOPK_ENC_PKFMA
-#define ARCTOPK_ENC_PKFMA 2            // fp32 encode: packed FMAs over even / odd columns (1: always,
-#endif                                 // 2: on the G-only stream (noef, first EF14 call), 0: never)
 #ifndef ARCTOPK_ENC_UNITS_G_ONLY
 #define ARCTOPK_ENC_UNITS_G_ONLY 4     // fp32 encode without E loads: 16-B units per lane per step
 #endif
 #ifndef ARCTOPK_ENC_UNITS_GE
 #define ARCTOPK_ENC_UNITS_GE 4         // fp32 encode with E loads: 16-B units of G (and of E) per lane per step
 #endif
-#ifndef ARCTOPK_ENC_NT_LOAD
-#define ARCTOPK_ENC_NT_LOAD 1          // fp32 encode rows: nontemporal G / E loads
-#endif
-#ifndef ARCTOPK_ENC_NT_STORE
-#define ARCTOPK_ENC_NT_STORE 1         // fp32 encode rows: nontemporal E stores
-#endif
 #ifndef ARCTOPK_ENC_UNITS_BF16
 #define ARCTOPK_ENC_UNITS_BF16 4       // bf16 encode rows: 16-B units per lane per step
-#endif
-#ifndef ARCTOPK_ENC_INTERLEAVE
-#define ARCTOPK_ENC_INTERLEAVE 1       // encode row tiles interleaved (1) or contiguous ranges (0)
 #endif
 
 namespace arctopk {
@@ -322,17 +283,12 @@ template <typename T, bool NT = false> __device__ __forceinline__ void st1(T* p,
     }
 }
 
-// streaming hints of the pack / decode kernels (build-time A/B switches)
-#ifndef ARCTOPK_NT_PACK
-#define ARCTOPK_NT_PACK 1
-#endif
-#ifndef ARCTOPK_NT_DECODE
-#define ARCTOPK_NT_DECODE 1
-#endif
-constexpr bool kNtPack = ARCTOPK_NT_PACK != 0;
-constexpr bool kNtDecode = ARCTOPK_NT_DECODE != 0;
-constexpr bool kEncNtLoad = ARCTOPK_ENC_NT_LOAD != 0;
-constexpr bool kEncNtStore = ARCTOPK_ENC_NT_STORE != 0;
+// streaming (nontemporal) hints: the pack's E accesses, the decode's output stores, the
+// encode's G / E loads and E stores (each measured faster than plain accesses)
+constexpr bool kNtPack = true;
+constexpr bool kNtDecode = true;
+constexpr bool kEncNtLoad = true;
+constexpr bool kEncNtStore = true;
 constexpr int kSmallTileRows = 1024;  // rows of a small-m pack/decode chunk (LDS slot table)
 
 // encode tile modes
@@ -414,6 +370,10 @@ struct arctopk_plan {
     int32_t* d_dfirst;            // [n_dec + 1]: per decode chunk, the bucket-wide index (sel_off +
                                   // slot) of its first selected row; written by the pack from the
                                   // row list, read by mode-3 decode chunks (and the next entry)
+    int32_t* d_dfirst_pub;        // [n_dec + 1]: the same table, derived from the slot map handed to
+                                  // the public decode entry points (k_dfirst), never the pack's
+    int32_t* d_m3;                // segments with mode-3 decode chunks, and their number
+    int n_m3;
     uint32_t* d_keys;             // select workspace: one key per row
     int32_t* d_small;             // segments selected by the fused one-block kernel
     int n_small;
@@ -454,7 +414,7 @@ int decode_pair(const arctopk_plan* pa, int32_t ws_a, int32_t ef_a, void* gerr_a
                 void* done);
 int pack_signal(const arctopk_plan* p, const void* grad, void* err, int32_t ef, const int32_t* rowlist,
                 const int32_t* slotmap, void* packed, void* stream, void* done);
-// arctopk_decode whose kernel completes `done`
+// the decode of the plan's own last pack (its chunk table); `done` (may be null) completed by the kernel
 int decode_signal(const arctopk_plan* p, const void* packed, const int32_t* slotmap, int32_t ws, int32_t ef,
                   void* gerr, void* out, void* stream, void* done);
 // the watchdog stops looking at a plan's events (arctopk_plan_destroy)
@@ -466,5 +426,5 @@ struct WireParams {
     double latency_us;  // fixed cost per all-reduce
     int32_t blocks;     // workgroups (the collective's CU footprint)
 };
-int wire_allreduce(const WireParams& w, void* buf, int64_t bytes, hipStream_t st);
+int wire_allreduce(const WireParams& w, void* buf, int64_t bytes, hipStream_t st, hipEvent_t done);
 }

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -127,6 +128,13 @@ struct arctopk_comm {
     std::atomic<int> err{0};             // sticky failure status
     std::mutex mu;                       // RCCL calls of the caller vs the watchdog's abort
     arctopk::WireParams wire{};          // WIRE
+    // WIRE: the communicator's operations run one after another whatever stream they are issued
+    // on, as RCCL serialises the collectives of one communicator: each emulated all-reduce
+    // completes wire_ev (its kernel's own completion signal), and one issued on another stream
+    // than the previous first waits for it
+    hipEvent_t wire_ev = nullptr;
+    hipStream_t wire_last = nullptr;
+    bool wire_used = false;
 };
 
 namespace {
@@ -236,8 +244,31 @@ class Watchdog {
                     items_.pop_back();
                 }
             }
-            if (fail) fail_all_locked(fail);
+            if (fail) {
+                fail_all_locked(fail);
+                if (teardown_on_failure()) {
+                    // as ProcessGroupNCCL's async error handling: work queued behind the failed
+                    // collective (decode, copy-back, optimizer step) would run on partially
+                    // reduced buffers once the aborted kernels exit, so the process ends here
+                    std::fprintf(stderr,
+                                 "[arctopk] exchange watchdog: a collective failed or stayed pending past the "
+                                 "timeout (status %d); communicators aborted, ending the process so that no "
+                                 "partially reduced update is applied (ARCTOPK_ASYNC_ERROR_HANDLING=0 or 2: "
+                                 "raise from the hook instead)\n",
+                                 fail);
+                    std::fflush(stderr);
+                    std::_Exit(1);
+                }
+            }
         }
+    }
+    // ARCTOPK_ASYNC_ERROR_HANDLING, else TORCH_NCCL_ASYNC_ERROR_HANDLING, with torch's meaning:
+    // 1 / 3 (torch's default): tear the process down; 0 / 2: abort the communicators only
+    static bool teardown_on_failure() {
+        const char* v = std::getenv("ARCTOPK_ASYNC_ERROR_HANDLING");
+        if (!v || !*v) v = std::getenv("TORCH_NCCL_ASYNC_ERROR_HANDLING");
+        if (!v || !*v) return true;
+        return v[0] == '1' || v[0] == '3';
     }
     std::mutex mu_;
     std::condition_variable cv_;
@@ -391,6 +422,7 @@ extern "C" int arctopk_comm_destroy(arctopk_comm* c) {
             c->nccl = nullptr;
         }
     }
+    if (c->wire_ev) (void)hipEventDestroy(c->wire_ev);
     delete c;
     return e;
 }
@@ -404,8 +436,24 @@ extern "C" int arctopk_comm_allreduce(arctopk_comm* c, void* buf, int64_t count,
     if (int f = comm_failed(c)) return f;
     if (count == 0) return 0;
     if (c->kind == arctopk_comm::CALLBACK) return c->fn(c->ctx, buf, count, dtype, stream);
-    if (c->kind == arctopk_comm::WIRE)
-        return arctopk::wire_allreduce(c->wire, buf, count * (dtype == ARCTOPK_BF16 ? 2 : 4), (hipStream_t)stream);
+    if (c->kind == arctopk_comm::WIRE) {
+        std::lock_guard<std::mutex> lc(c->mu);
+        hipStream_t st = (hipStream_t)stream;
+        if (!c->wire_ev) {
+            const hipError_t he = hipEventCreateWithFlags(&c->wire_ev, hipEventDisableTiming);
+            if (he != hipSuccess) return (int)he;
+        }
+        if (c->wire_used && c->wire_last != st) {
+            const hipError_t he = hipStreamWaitEvent(st, c->wire_ev, 0);
+            if (he != hipSuccess) return (int)he;
+        }
+        const int e = arctopk::wire_allreduce(c->wire, buf, count * (dtype == ARCTOPK_BF16 ? 2 : 4), st, c->wire_ev);
+        if (!e) {
+            c->wire_last = st;
+            c->wire_used = true;
+        }
+        return e;
+    }
     std::unique_lock<std::mutex> lc(c->mu);
     if (!c->nccl) return c->err.load() ? c->err.load() : ARCTOPK_EABORTED;
     ncclResult_t r = c->rccl->all_reduce(buf, buf, (size_t)count, dtype == ARCTOPK_BF16 ? ncclBfloat16 : ncclFloat32,
@@ -441,15 +489,6 @@ extern "C" int arctopk_comm_allreduce(arctopk_comm* c, void* buf, int64_t count,
     return 0;
 }
 
-#ifndef ARCTOPK_DECODE_PAIR
-#define ARCTOPK_DECODE_PAIR 1  // the last step's decode and the last finished one share a launch
-#endif
-
-// flags of the pack kernel's stop event (A/B switch): 0 = a timing event with the default
-// (system-scope) release at the kernel's end
-#ifndef ARCTOPK_PACK_EV_FLAGS
-#define ARCTOPK_PACK_EV_FLAGS 0
-#endif
 
 namespace {
 
@@ -496,12 +535,8 @@ int ensure_event(void** ev, unsigned flags) {
 // The deferred decode of plan p's last exchange step, on `stream`: after that step's packed
 // all-reduce (a stream wait only when the host does not already see it complete).
 namespace {
-#ifndef ARCTOPK_WAIT_AR_QUERY
-#define ARCTOPK_WAIT_AR_QUERY 1  // A/B switch: 0 = always enqueue the stream wait (no host query)
-#endif
 int wait_ar(arctopk_plan* p, hipStream_t st) {
     if (p->x_deferred != 1) return 0;  // 2: no all-reduce on another stream
-    if (!ARCTOPK_WAIT_AR_QUERY) return (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
     const hipError_t q = hipEventQuery((hipEvent_t)p->x_ev_ar);
     if (q == hipErrorNotReady) return (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0);
     return q == hipSuccess ? 0 : (int)q;
@@ -514,7 +549,7 @@ extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* cons
     hipStream_t st = (hipStream_t)stream;
     int e = wait_ar(p, st);
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
-    if (!e) e = arctopk_decode(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, stream);
+    if (!e) e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, stream, nullptr);
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
     if (!e) p->x_deferred = 0;
     return e;
@@ -569,8 +604,8 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
             e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
         }
         if (!e && !rode) {  // a separate decode launch after the select
-            e = arctopk_decode(ride, ride->b_packed, ride->b_slotmap, ride->x_ws, ride->x_ef, ride->x_gerr,
-                               ride->x_bucket, stream);
+            e = arctopk::decode_signal(ride, ride->b_packed, ride->b_slotmap, ride->x_ws, ride->x_ef, ride->x_gerr,
+                                       ride->x_bucket, stream, nullptr);
             if (!e) ride->x_deferred = 0;
             if (!e) e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
         }
@@ -586,7 +621,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // and the watchdog sees the sketch all-reduce before it complete
     const bool async_ar = defer && packed_comm;
     if (packed_comm) {
-        if ((e = ensure_event(&p->x_ev_packed, ARCTOPK_PACK_EV_FLAGS)) ||
+        if ((e = ensure_event(&p->x_ev_packed, 0)) ||
             (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
             return e;
         e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
@@ -610,7 +645,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // the backward's last step (no deferral): the last deferred decode it finishes shares one
     // launch with its own decode, after its own packed all-reduce (unless markers were asked for)
     arctopk_plan* pair = nullptr;
-    if (ARCTOPK_DECODE_PAIR && !defer && nfinish > 0 && finish[nfinish - 1] && finish[nfinish - 1] != p &&
+    if (!defer && nfinish > 0 && finish[nfinish - 1] && finish[nfinish - 1] != p &&
         finish[nfinish - 1]->x_deferred && !(finish_marks && finish_marks[nfinish - 1]) && !marks)
         pair = finish[nfinish - 1];
     // earlier buckets' deferred decodes the caller wants done now (in its order)
@@ -650,7 +685,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream, p->x_ev_dec);
         if (!e) Watchdog::get().watch(packed_comm, p->x_ev_dec);
     } else {
-        e = arctopk_decode(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream);
+        e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream, nullptr);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
     ht.lap(7);
@@ -664,33 +699,4 @@ extern "C" int arctopk_diag_host_times(int64_t* ns, int32_t n, int64_t* calls) {
     for (int i = 0; i < n && i < kHtParts; ++i) ns[i] = g_ht_ns[i].exchange(0);
     *calls = g_ht_calls.exchange(0);
     return 0;
-}
-
-// Diagnostics (not in the public header): the first `bytes` of a plan's multi-block select
-// workspace (arctopk::MWorkspace: histograms, first-digit windows, item states, per-range
-// counts), copied to the host after the device is idle.
-extern "C" int arctopk_diag_mws(const arctopk_plan* p, void* host, int64_t bytes) {
-    if (!p || !host || bytes < 0) return ARCTOPK_EINVAL;
-    if (!p->d_mws) return ARCTOPK_EINVAL;
-    hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(host, p->d_mws, (size_t)bytes, hipMemcpyDeviceToHost);
-    return (int)e;
-}
-
-// Diagnostics (not in the public header): the plan's row-energy keys (select workspace), as
-// the last select left them.
-extern "C" int arctopk_diag_keys(const arctopk_plan* p, uint32_t* host, int64_t n) {
-    if (!p || !host || n < 0 || n > p->info.rows_total) return ARCTOPK_EINVAL;
-    hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(host, p->d_keys, (size_t)n * 4, hipMemcpyDeviceToHost);
-    return (int)e;
-}
-
-// Diagnostics (not in the public header): overwrite `bytes` of the plan's select workspace at
-// byte offset `off` (e.g. a first-digit window) from the host.
-extern "C" int arctopk_diag_set_mws(const arctopk_plan* p, int64_t off, const void* host, int64_t bytes) {
-    if (!p || !host || off < 0 || bytes < 0 || !p->d_mws) return ARCTOPK_EINVAL;
-    hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(reinterpret_cast<char*>(p->d_mws) + off, host, (size_t)bytes, hipMemcpyHostToDevice);
-    return (int)e;
 }

@@ -36,7 +36,6 @@ struct MItem {
     int64_t cand_cap;  // candidate-list capacity
     int32_t range;     // keys per range (multiple of kMTile)
     int32_t nranges;   // ceil(n / range) <= kMMaxRanges
-    int32_t win;       // ARC: index of the item's first-digit window (MWorkspace::win_*), -1: none
     int32_t pad_;
 };
 
@@ -64,14 +63,9 @@ struct alignas(128) MCounter {
 };
 __host__ __device__ constexpr int hist_slot(int bin) { return ((bin & 127) << 5) | (bin >> 7); }
 
-constexpr int kMWin = 4096;        // ARC items with a first-digit window (per plan)
 
 struct MWorkspace {
     uint32_t hist[kMB][kMBins];  // indexed by hist_slot(bin)
-    // ARC first-digit windows, kept across calls (see arc_digit): item i's keys are binned by
-    // (key >> win_sh[i]) - win_base[i], clamped to the 4096 bins; win_sh 0 = no window yet
-    uint32_t win_sh[kMWin];
-    uint32_t win_base[kMWin];
     MState st[kMB];
     MCounter ncand[kMB];
     MCounter done[kMB];          // blocks of the running kernel that finished, per item
@@ -149,121 +143,24 @@ __device__ inline void ms_init_item(MWorkspace* ws, int t, int64_t k, uint32_t k
     }
 }
 
-// ARC first pass, run by the LAST block of the fused key kernel (NT threads) once every
-// block merged its LDS histogram of the keys' top 12 value bits (bits 30..19: energies are
-// non-negative and NaN maps to 0x7FFFFFFF, so bit 31 is always clear) into
-// ws->hist[t]: read-and-clear the bins (leaving them zero for the next call), find the
-// bin holding the k-th largest key, and start the item in candidate mode on that bin
-// (cand_cap = n for ARC items: every key of the bin fits).
+// ARC first pass: every block of the fused key kernel merges its LDS histogram of the keys'
+// top 12 value bits (bits 30..19: energies are non-negative and NaN maps to 0x7FFFFFFF, so
+// bit 31 is always clear) into ws->hist[t]; the blocks of the next launches find the bin
+// holding the k-th largest key there (ms_arc_digit_local) and start the item in candidate
+// mode on that bin (cand_cap = n for ARC items: every key of the bin fits).  A first-pass bin
+// spans 1/16 of an octave of energy.
 constexpr int kArcShift = 31 - 12;
-
-// ---- ARC first digit: the top 12 value bits, or a window around the last call's threshold ----
-// With the top 12 bits, a first-pass bin spans 1/16 of an octave of energy, and the bin holding
-// the k-th largest key of a 1 M-row item holds ~14 K keys (1x1-conv rows, compress ratio 0.2):
-// the compact and refine passes then move and radix-sort all of them.  After a call, the
-// refine centres the item's window on the exact threshold T it found: 4096 bins of
-// 2^kArcWinShift keys (1/512 octave, +-4 octaves around T), so the bin of the next call's
-// k-th key holds ~30x fewer keys.  Keys outside the window fall into the two edge bins; if the
-// k-th key lands there (the energies moved by > 16x), that bin is not a bit prefix and the
-// refine resolves all 32 bits of its keys -- slower, never wrong.
-constexpr uint32_t kArcWinShift = 14;
-struct ArcWin {
-    uint32_t sh, base;
-};
-__device__ inline ArcWin arc_win(const MWorkspace* ws, int idx) {
-    ArcWin w{(uint32_t)kArcShift, 0u};
-    if (idx >= 0) {
-        const uint32_t sh = ws->win_sh[idx];
-        if (sh) w = ArcWin{sh, ws->win_base[idx]};
-    }
-    return w;
-}
-__device__ __forceinline__ uint32_t arc_digit(uint32_t key, ArcWin w) {
-    // (max before the subtraction: written as `h < base ? 0 : min(h - base, 4095)`, the
-    // compiler of ROCm 7.2 dropped the comparison and kept the wrapping subtraction)
-    const uint32_t h = max(key >> w.sh, w.base);
-    return min(h - w.base, (uint32_t)kMBins - 1u);
-}
-// the bin d as a radix state: a bit prefix, or (edge bin of a window) no decided bits
-__device__ inline void arc_bin_state(ArcWin w, uint32_t d, uint32_t* prefix, uint32_t* mask, int32_t* bit) {
-    const bool lo_edge = d == 0 && w.base > 0;
-    const bool hi_edge = d == (uint32_t)kMBins - 1 && (0x7FFFFFFFu >> w.sh) > w.base + (uint32_t)kMBins - 1;
-    if (lo_edge || hi_edge) {
-        *prefix = 0u;
-        *mask = 0u;
-        *bit = 32;
-    } else {
-        *prefix = (d + w.base) << w.sh;
-        *mask = ~((1u << w.sh) - 1u);
-        *bit = (int32_t)w.sh;
-    }
-}
-// the window of the next call, centred on this call's threshold T
-#ifndef ARCTOPK_ARC_WINDOW
-#define ARCTOPK_ARC_WINDOW 0  // tuning switch (A/B builds): 1 = first-digit window (measured slower: the
-                              // key pass merges ~4,000 non-empty bins per block instead of ~100,
-                              // ResNet-50 mix keys 22.7 -> 41.7 us, refine 20.6 -> 14.9)
-#endif
-__device__ inline void arc_win_update(MWorkspace* ws, int idx, uint32_t T) {
-    if (idx < 0 || !ARCTOPK_ARC_WINDOW) return;
-    constexpr uint32_t top = 0x7FFFFFFFu >> kArcWinShift;  // largest key >> shift
-    const uint32_t c = T >> kArcWinShift;
-    uint32_t base = c > (uint32_t)kMBins / 2 ? c - (uint32_t)kMBins / 2 : 0u;
-    if (base + (uint32_t)kMBins - 1 > top) base = top + 1 - (uint32_t)kMBins;
-    ws->win_base[idx] = base;
-    ws->win_sh[idx] = kArcWinShift;
-}
-template <int NT>
-__device__ inline void ms_arc_first_digit(MWorkspace* ws, int t, int64_t k, ArcWin w, uint32_t* lds_h /* kMBins */) {
-    __shared__ uint32_t s_w[NT / 64], s_d, s_acc;
-    constexpr int PER = kMBins / NT;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    ms_take_hist(ws, t, kMBins, lds_h);
-    __syncthreads();
-    uint32_t c[PER], sum = 0;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        c[q] = lds_h[kMBins - 1 - (tid * PER + q)];  // descending
-        sum += c[q];
-    }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0;
-    for (int w = 0; w < wave; ++w) before += s_w[w];
-    const uint64_t excl = (uint64_t)before + incl - sum;
-    if (excl < (uint64_t)k && excl + sum >= (uint64_t)k) {
-        uint64_t acc = excl;
-        int q = 0;
-        for (; q < PER - 1; ++q) {
-            if (acc + c[q] >= (uint64_t)k) break;
-            acc += c[q];
-        }
-        s_d = (uint32_t)(kMBins - 1 - (tid * PER + q));
-        s_acc = (uint32_t)acc;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        MState& g = ws->st[t];
-        arc_bin_state(w, s_d, &g.prefix, &g.mask, &g.bit);
-        g.kk = k - (int64_t)s_acc;
-        g.cand = 1;
-        g.p1 = g.prefix;
-        g.m1 = g.mask;
-        g.ncand = 0;
-        ws->ncand[t].v = 0;
-    }
+__device__ __forceinline__ uint32_t arc_digit(uint32_t key) { return key >> kArcShift; }
+// the bin d as a radix state: its bit prefix
+__device__ inline void arc_bin_state(uint32_t d, uint32_t* prefix, uint32_t* mask, int32_t* bit) {
+    *prefix = d << kArcShift;
+    *mask = ~((1u << kArcShift) - 1u);
+    *bit = kArcShift;
 }
 
-// The same first-pass digit derived by every ARC compact block from the merged histogram
-// that an EARLIER launch (the key pass) finished, with plain loads: this takes the
-// last-block hand-off (arrival counter + read-back, ~4.5 us of serial tail) out of the key
-// pass.  Two levels over the slot layout (slot L*32 + g holds bin g*128 + L): with NT a
+// The first-pass digit derived by every ARC compact block from the merged histogram that an
+// EARLIER launch (the key pass) finished, with plain loads (no last-block hand-off in the key
+// pass).  Two levels over the slot layout (slot L*32 + g holds bin g*128 + L): with NT a
 // multiple of 32, thread tid's PER slots all belong to bin group g = tid & 31, so group
 // totals need no transposition; wave 0 picks the group holding the k-th largest key, then
 // the bin inside it from that group's 128 counts.  lds: NT + 128 words.  Returns the bin d
@@ -328,10 +225,6 @@ __device__ inline void ms_arc_digit_local(const uint32_t* __restrict__ hist_t, i
     *acc_out = s_acc2;
 }
 
-#ifndef ARCTOPK_ARC_LOCAL_DIGIT
-#define ARCTOPK_ARC_LOCAL_DIGIT 1  // tuning switch (A/B builds): 0 = the key pass's last block picks the digit
-#endif
-constexpr bool kArcLocalDigit = ARCTOPK_ARC_LOCAL_DIGIT != 0;
 
 // host-side geometry of one item: fills range / nranges / cand_cap (cand_off by caller)
 void ms_item_geometry(MItem& it);

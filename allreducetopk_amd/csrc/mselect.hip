@@ -61,8 +61,6 @@ __device__ __forceinline__ bool ms_locate(const MBatch& b, int* t, int* r) {
     return false;
 }
 
-DIAG_STAMPS(g_st_compact)
-DIAG_STAMPS(g_st_write)
 
 static int total_ranges(const MBatch& b) {
     int n = 0;
@@ -266,19 +264,17 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
                                                      uint32_t* __restrict__ ckey) {
     const MBatch& b = *bp;
     __shared__ uint32_t lds[4], s_cnt[4], s_and[4];
-    DIAG_STAMP(g_st_compact, 0);
     int t, r;
     if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
-    const ArcWin w = arc_win(ws, it.win);
     uint32_t d;  // the first-pass bin (keys above it are selected; its keys are the candidates)
-    if constexpr (kArcLocalDigit) {
+    {
         __shared__ uint32_t lds_d[256 + 128];
         uint32_t acc;
         ms_arc_digit_local<256>(ws->hist[t], it.k, lds_d, &d, &acc);
         if (r == 0 && threadIdx.x == 0) {  // the item's state for the refine (next launch)
             MState g;
-            arc_bin_state(w, d, &g.prefix, &g.mask, &g.bit);
+            arc_bin_state(d, &g.prefix, &g.mask, &g.bit);
             g.cand = 1;
             g.kk = it.k - (int64_t)acc;
             g.p1 = g.prefix;
@@ -286,11 +282,6 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
             g.ncand = 0;
             ws->st[t] = g;
         }
-    } else {
-        // the key pass's last block left the bin's radix state: recover d from a key of it
-        // (prefix bins only; with a window, ARCTOPK_ARC_LOCAL_DIGIT = 0 is not supported)
-        const MState s = ws->st[t];
-        d = arc_digit(s.p1, w);
     }
     const int64_t r0 = (int64_t)r * it.range;
     const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
@@ -308,7 +299,7 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
             const bool valid = wb + j * 64 + lane < r1;
-            const uint32_t dj = arc_digit(kv[j], w);
+            const uint32_t dj = arc_digit(kv[j]);
             gt += (valid && dj > d) ? 1u : 0u;
             bm[j] = __ballot(valid && dj == d);
             nin += popc64(bm[j]);
@@ -352,7 +343,6 @@ __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ 
         ws->cand_or[t][r] = s_cnt[0] | s_cnt[1] | s_cnt[2] | s_cnt[3];
         ws->cand_and[t][r] = s_and[0] & s_and[1] & s_and[2] & s_and[3];
     }
-    DIAG_STAMP(g_st_compact, 1);
 }
 
 // Per-range counts of the bin's keys > T and == T (T = the final prefix), added to the
@@ -491,7 +481,6 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* _
                                               int32_t* __restrict__ out_idx, void* __restrict__ out_val,
                                               int32_t* __restrict__ out_slot, void* zero_x) {
     __shared__ uint32_t s_eq[4], s_gt[4];
-    DIAG_STAMP(g_st_write, 0);
     int t, r;
     if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
@@ -562,20 +551,9 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* _
         run += tgt + te;
         take_left -= te;
     }
-#ifdef ARCTOPK_STAMPS
-    __syncthreads();
-#endif
-    DIAG_STAMP(g_st_write, 1);
 }
 
 }  // namespace
-
-#ifdef ARCTOPK_STAMPS
-extern "C" int arctopk_diag_stamps_m(int which, unsigned long long* host) {
-    return (int)(which == 0 ? hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_compact), sizeof(g_st_compact))
-                            : hipMemcpyFromSymbol(host, HIP_SYMBOL(g_st_write), sizeof(g_st_write)));
-}
-#endif
 
 void ms_item_geometry(MItem& it) {
     const int64_t tiles = (it.n + kMTile - 1) / kMTile;
@@ -585,7 +563,6 @@ void ms_item_geometry(MItem& it) {
     // candidates: the k-th key's 12-bit bin; a few % of n on gradient-like data, all of
     // n on degenerate data (e.g. a zero tensor) -> full mode past the cap
     it.cand_cap = it.n <= 65536 ? it.n : std::max<int64_t>(65536, it.n / 8);
-    it.win = -1;  // ARC plans assign first-digit windows (plan.hip)
     it.pad_ = 0;
 }
 

@@ -136,7 +136,6 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     constexpr int64_t pack_elems = ARCTOPK_PACK_CHUNK, dec_elems = ARCTOPK_DEC_CHUNK;
     constexpr int64_t stream_pack_elems = ARCTOPK_STREAM_PACK_CHUNK;
     constexpr int64_t short_dec_elems = ARCTOPK_SHORT_DEC_CHUNK;
-    constexpr bool interleave = ARCTOPK_ENC_INTERLEAVE != 0;  // interleaved row tiles
     int64_t part_len = 0, split_rows_max = 0;
     // vector paths: 16-B encode units (4 fp32 / 8 bf16 elements) need m and the offset to be
     // multiples of va; pack / decode quads need 4
@@ -200,15 +199,10 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 const int64_t c0 = part * clen;
                 const int64_t cl = std::min<int64_t>(clen, s.m - c0);
                 std::vector<EncTile>& dst = tab ? enc_e : enc;
-                for (int64_t ti = 0; ti < ntiles; ++ti) {
-                    if (interleave)  // rows ti, ti + ntiles, ...: consecutive blocks, adjacent rows
-                        dst.push_back(EncTile{(int32_t)i, mode, ti, (s.n - ti + ntiles - 1) / ntiles,
-                                              (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1,
-                                              (int32_t)ntiles});
-                    else
-                        dst.push_back(EncTile{(int32_t)i, mode, ti * per, std::min(per, s.n - ti * per),
-                                              (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1, 1});
-                }
+                // tile ti holds rows ti, ti + ntiles, ...: consecutive blocks read adjacent rows
+                for (int64_t ti = 0; ti < ntiles; ++ti)
+                    dst.push_back(EncTile{(int32_t)i, mode, ti, (s.n - ti + ntiles - 1) / ntiles,
+                                          (int32_t)c0, (int32_t)cl, nparts > 1 ? part : -1, (int32_t)ntiles});
                 lds = std::max<int>(lds, (int)(cl * r * 4));
             }
         }
@@ -239,14 +233,14 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
         // mode 3 (short rows, quad-aligned data): chunks of <= ARCTOPK_SHORT3_CHUNK elements whose
         // first elements are quad-aligned (rows per chunk a multiple of 4 / gcd(m, 4))
         const int64_t q3 = 4 / std::gcd<int64_t>(s.m, 4);
-        if (small_tile && ARCTOPK_SHORT3_DEC && s.offset % 4 == 0 &&
+        if (small_tile && s.offset % 4 == 0 &&
             (int64_t)ARCTOPK_SHORT3_CHUNK / s.m >= q3) {
             const int64_t per = (int64_t)ARCTOPK_SHORT3_CHUNK / s.m / q3 * q3;
             g.dchunk_rows = (int32_t)per;
             for (int64_t row = 0; row < s.n; row += per)
                 dec.push_back(Chunk{(int32_t)i, 3, row, std::min(per, s.n - row)});
             dec_lds = std::max<int64_t>(dec_lds, (std::min(per, s.n) * (s.m + 1) + 12) * 4);  // + alignment, quad lead
-        } else if (small_tile && dtype == ARCTOPK_F32 && ARCTOPK_QUAD_DEC) {
+        } else if (small_tile && dtype == ARCTOPK_F32) {
             // mode 2: lane per 16-B output quad, rows of whole chunks (no LDS tile)
             const int64_t per = std::max<int64_t>(1, (int64_t)ARCTOPK_QUAD_DEC_CHUNK / s.m);
             for (int64_t row = 0; row < s.n; row += per)
@@ -304,7 +298,16 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     ALLOC_COPY(p->d_dec, dec);
     e = hipMalloc((void**)&p->d_dfirst, (dec.size() + 1) * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemset(p->d_dfirst, 0, (dec.size() + 1) * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&p->d_dfirst_pub, (dec.size() + 1) * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(p->d_dfirst_pub, 0, (dec.size() + 1) * sizeof(int32_t));
     if (e != hipSuccess) { arctopk_plan_destroy(p); return (int)e; }
+    {
+        std::vector<int32_t> m3;
+        for (size_t i = 0; i < dsegs.size(); ++i)
+            if (dsegs[i].dchunk_rows > 0) m3.push_back((int32_t)i);
+        p->n_m3 = (int)m3.size();
+        ALLOC_COPY(p->d_m3, m3);
+    }
     ALLOC_COPY(p->d_small, small_ids);
     ALLOC_COPY(p->d_large, large_ids);
     ALLOC_COPY(p->d_split, split_ids);
@@ -331,8 +334,6 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 it.slot_off = sg.row_off;
                 ms_item_geometry(it);
                 it.cand_cap = it.n;  // ARC: every key of the first-pass bin is a candidate
-                const int gi = bi * kMB + i;  // = the key pass's item index (first + t)
-                it.win = gi < kMWin ? gi : -1;
                 it.cand_off = cap;
                 cap += it.cand_cap;
             }
@@ -374,6 +375,87 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     return 0;
 }
 
+// A plan over segments [seg_begin, seg_end) of `parent` (a group of consecutive tensors of the
+// bucket): its own work tables, the parent's geometry and projection draws.  A tensor's
+// geometry depends on (kind, n, m) only, so each segment is planned as a [n] (RAW) or [n, m]
+// (SKETCH) tensor; the draw table keeps the parent's Philox offsets (a tensor's V is the one
+// the whole bucket's draw gives it), with V offsets relative to the group's first SKETCH tensor.
+// The group's offsets differ from the parent's by the group's base offsets, which must keep
+// every alignment the kernels test (16-B units: multiples of 8 elements).
+extern "C" int arctopk_plan_group(const arctopk_plan* parent, int32_t seg_begin, int32_t seg_end,
+                                  arctopk_plan** out) {
+    if (!parent || !out || seg_begin < 0 || seg_end > parent->nseg || seg_begin >= seg_end) return ARCTOPK_EINVAL;
+    *out = nullptr;
+    const arctopk_segment& b0 = parent->h_segs[seg_begin];
+    if (b0.offset % 8 || b0.sketch_off % 8 || b0.packed_off % 8 || b0.row_off % 4)
+        return ARCTOPK_EINVAL;
+    int64_t vbase = -1;
+    for (int i = seg_begin; i < seg_end && vbase < 0; ++i)
+        if (parent->h_segs[i].kind == ARCTOPK_SEG_SKETCH) vbase = parent->h_segs[i].v_off;
+    if (vbase > 0 && vbase % 8) return ARCTOPK_EINVAL;
+    std::vector<int64_t> dims;
+    std::vector<int32_t> nd;
+    for (int i = seg_begin; i < seg_end; ++i) {
+        const arctopk_segment& s = parent->h_segs[i];
+        dims.push_back(s.n);
+        if (s.kind == ARCTOPK_SEG_SKETCH) dims.push_back(s.m);
+        nd.push_back(s.kind == ARCTOPK_SEG_SKETCH ? 2 : 1);
+    }
+    arctopk_plan* c = nullptr;
+    int e = arctopk_plan_create(dims.data(), nd.data(), (int32_t)nd.size(), parent->r, parent->ratio,
+                                parent->dtype, parent->device, &c);
+    if (e) return e;
+    for (int i = seg_begin; i < seg_end; ++i) {  // same geometry, offsets shifted by the base
+        const arctopk_segment& s = parent->h_segs[i];
+        const arctopk_segment& g = c->h_segs[i - seg_begin];
+        if (g.kind != s.kind || g.n != s.n || g.m != s.m || g.k_rows != s.k_rows ||
+            g.offset != s.offset - b0.offset || g.sketch_off != s.sketch_off - b0.sketch_off ||
+            g.packed_off != s.packed_off - b0.packed_off || g.sel_off != s.sel_off - b0.sel_off ||
+            g.row_off != s.row_off - b0.row_off ||
+            (s.kind == ARCTOPK_SEG_SKETCH && g.v_off != s.v_off - vbase)) {
+            arctopk_plan_destroy(c);
+            return ARCTOPK_EINVAL;
+        }
+    }
+    // the parent's draws of this group's SKETCH tensors
+    std::vector<VDraw> vd(parent->nseg);
+    int nvd = 0;
+    uint64_t adv = 0;
+    e = vdraw_table(parent->h_segs, parent->nseg, parent->r, parent->device, vd.data(), &nvd, &adv);
+    if (e) { arctopk_plan_destroy(c); return e; }
+    std::vector<VDraw> mine;
+    for (int i = 0, j = 0; i < parent->nseg; ++i) {
+        if (parent->h_segs[i].kind != ARCTOPK_SEG_SKETCH) continue;
+        if (i >= seg_begin && i < seg_end) {
+            VDraw d = vd[j];
+            d.v_off -= vbase;
+            mine.push_back(d);
+        }
+        ++j;
+    }
+    std::vector<VChunk> vc;
+    for (size_t i = 0; i < mine.size(); ++i)
+        for (int64_t lo = 0; lo < mine[i].numel; lo += kVChunk)
+            vc.push_back({(int32_t)i, (uint32_t)lo, (uint32_t)std::min<int64_t>(mine[i].numel, lo + kVChunk)});
+    hipError_t he = hipSetDevice(parent->device);
+    if (c->d_vdraw) (void)hipFree(c->d_vdraw);
+    if (c->d_vchunk) (void)hipFree(c->d_vchunk);
+    c->d_vdraw = nullptr;
+    c->d_vchunk = nullptr;
+    if (he == hipSuccess) he = hipMalloc((void**)&c->d_vdraw, std::max<size_t>(1, mine.size() * sizeof(VDraw)));
+    if (he == hipSuccess && !mine.empty())
+        he = hipMemcpy(c->d_vdraw, mine.data(), mine.size() * sizeof(VDraw), hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMalloc((void**)&c->d_vchunk, std::max<size_t>(1, vc.size() * sizeof(VChunk)));
+    if (he == hipSuccess && !vc.empty())
+        he = hipMemcpy(c->d_vchunk, vc.data(), vc.size() * sizeof(VChunk), hipMemcpyHostToDevice);
+    if (he != hipSuccess) { arctopk_plan_destroy(c); return (int)he; }
+    c->n_vdraw = (int)mine.size();
+    c->n_vchunk = (int)vc.size();
+    c->vdraw_advance = parent->vdraw_advance;  // (the bucket's: reseeds use the parent's)
+    *out = c;
+    return 0;
+}
+
 extern "C" int arctopk_plan_describe(const int64_t* dims, const int32_t* ndims, int32_t ntensors,
                                      int32_t r, double compress_ratio, arctopk_segment* segs_out,
                                      arctopk_plan_info* info) {
@@ -397,6 +479,8 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->d_pack) (void)hipFree(p->d_pack);
     if (p->d_dec) (void)hipFree(p->d_dec);
     if (p->d_dfirst) (void)hipFree(p->d_dfirst);
+    if (p->d_dfirst_pub) (void)hipFree(p->d_dfirst_pub);
+    if (p->d_m3) (void)hipFree(p->d_m3);
     if (p->d_keys) (void)hipFree(p->d_keys);
     if (p->d_small) (void)hipFree(p->d_small);
     if (p->d_large) (void)hipFree(p->d_large);

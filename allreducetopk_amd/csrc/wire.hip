@@ -11,6 +11,7 @@
 // share of the traffic by the device's constant-rate clock so that the whole takes at least
 // latency + 2 (R - 1) / R * B / busBW.  Under HBM contention it runs slower than its pace:
 // that is what it is for.  Not a collective, not in the product path of any hook.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -56,7 +57,9 @@ __global__ void __launch_bounds__(kWireThreads) k_wire(float4* __restrict__ buf,
 
 }  // namespace
 
-int wire_allreduce(const WireParams& w, void* buf, int64_t bytes, hipStream_t st) {
+// `done` (may be null): completed by the kernel's own completion signal (the communicator's
+// serialisation event, exchange.cpp)
+int wire_allreduce(const WireParams& w, void* buf, int64_t bytes, hipStream_t st, hipEvent_t done) {
     if (bytes < 0 || (bytes && !buf) || w.ranks < 1 || w.blocks < 1) return ARCTOPK_EINVAL;
     int dev = 0, khz = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -68,8 +71,12 @@ int wire_allreduce(const WireParams& w, void* buf, int64_t bytes, hipStream_t st
     const uint64_t ticks = (uint64_t)(us * (double)khz / 1e3);
     const int64_t n4 = bytes / 16;
     const int64_t moves = n4 > 0 ? (int64_t)(frac * (double)n4 + 0.5) : 0;
-    hipLaunchKernelGGL(k_wire, dim3(w.blocks), dim3(kWireThreads), 0, st, static_cast<float4*>(buf),
-                       n4 > 0 ? n4 : 1, moves, ticks);
+    if (done)
+        hipExtLaunchKernelGGL(k_wire, dim3(w.blocks), dim3(kWireThreads), 0, st, nullptr, done, 0,
+                              static_cast<float4*>(buf), n4 > 0 ? n4 : 1, moves, ticks);
+    else
+        hipLaunchKernelGGL(k_wire, dim3(w.blocks), dim3(kWireThreads), 0, st, static_cast<float4*>(buf),
+                           n4 > 0 ? n4 : 1, moves, ticks);
     return (int)hipGetLastError();
 }
 

@@ -107,6 +107,21 @@ int arctopk_plan_destroy(arctopk_plan* plan);
 int arctopk_plan_describe(const int64_t* dims, const int32_t* ndims, int32_t ntensors, int32_t r,
                           double compress_ratio, arctopk_segment* segs_out, arctopk_plan_info* info);
 int arctopk_plan_query(const arctopk_plan* plan, arctopk_plan_info* info);
+/*
+ * A plan over the consecutive segments [seg_begin, seg_end) of `parent` (a group of the bucket's
+ * tensors): the exchange pipeline's unit below a bucket.  Geometry, k and
+ * projections (the parent's Philox offsets) are the parent's; every offset is relative to the
+ * group's first segment, so bind the group to the parent's buffers at those segment's offsets
+ * (sketch_off, row_off, row_off, packed_off, first SKETCH v_off) and pass bucket / residual
+ * pointers at its element offset.  ARCTOPK_EINVAL when the group's base offsets are not
+ * multiples of 8 elements (sketch, packed, bucket, V) and 4 (slot map), which keeps every vector
+ * path of the kernels aligned as in the parent.  Destroy with arctopk_plan_destroy.
+ * Replaces: nothing in the reference (its per-tensor sketch all-reduce, :33, :58, :88, is the
+ * finest grain; the group is a run of those tensors).
+ */
+int arctopk_plan_group(const arctopk_plan* parent, int32_t seg_begin, int32_t seg_end,
+                       arctopk_plan** out);
+
 int arctopk_plan_segment(const arctopk_plan* plan, int32_t i, arctopk_segment* seg);
 
 /*
@@ -202,8 +217,13 @@ int arctopk_comm_init_rccl(const char* rccl_path, const void* id, int32_t nranks
  * pending `timeout_ms` after it was enqueued, aborts EVERY RCCL communicator of the library
  * (the GPU kernels of an aborted communicator exit) and leaves the error sticky:
  * arctopk_comm_status returns it, and every later exchange step on the communicator returns
- * it instead of enqueueing work.  arctopk_comm_init_rccl = timeout 0: blocking creation, no
- * watchdog.  The device current on the calling thread is left unchanged.
+ * it instead of enqueueing work.  Work already queued behind the failed collective (the decode,
+ * the caller's copy-back and optimizer step) would then run on partially reduced buffers, so,
+ * as ProcessGroupNCCL's async error handling does by default, the watchdog then ends the
+ * process (stderr message, exit status 1).  ARCTOPK_ASYNC_ERROR_HANDLING (else torch's
+ * TORCH_NCCL_ASYNC_ERROR_HANDLING) = 0 or 2 keeps it alive: the error is then raised by the
+ * next exchange step.  arctopk_comm_init_rccl = timeout 0: blocking creation, no watchdog.  The
+ * device current on the calling thread is left unchanged.
  */
 int arctopk_comm_init_rccl_timeout(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
                                    int32_t device, int64_t timeout_ms, arctopk_comm** out);
@@ -282,7 +302,11 @@ int arctopk_pack(const arctopk_plan* plan, const void* grad, void* err, int32_t 
  * K4 decode.  From the all-reduced packed values:
  *   NONE/EF14 : out = scatter(packed / world_size) into zeros
  *   EF21      : out = gE + scatter(packed / world_size); gE[sel] = out[sel]
- * `out` may alias the bucket (it is the bucket in the hook).
+ * `out` may alias the bucket (it is the bucket in the hook).  `packed` and `slotmap` are all
+ * it reads of the selection: any slot map of arctopk_select's format (per row its slot within
+ * the segment, ascending with the row, or -1) and packed values laid out as arctopk_pack
+ * writes them, whatever ran on the plan before (the short-row chunks derive their packed
+ * ranges from the slot map given, in one extra launch).
  * Replaces: values_memory.div_(ws) (:281), input_tensor.zero_() (:284), the
  * per-tensor index_put scatter (:131-141) and gE.add_/input.copy_ (:288-290).
  */

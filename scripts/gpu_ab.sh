@@ -1,21 +1,16 @@
 #!/bin/bash
-# A/B of library build variants through bench.py (ARCTOPK_LIB selects the library).
+# A/B of library variants on one box: bench.py (args in BENCH_ARGS) with each lib, interleaved.
+# Summary lines go to stdout and gpurun_out/ab/summary.txt (appended, tagged by BENCH_ARGS).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
-L=allreducetopk_amd/lib
+TAG=$(echo "${BENCH_ARGS}" | tr -c 'a-zA-Z0-9_' '_' | sed 's/__*/_/g')
 for rep in 1 2; do
-  for v in ${VARIANTS:-libarctopk.so}; do
-    for ef in ${EFS:-ef14}; do
-      ARCTOPK_LIB=$L/$v timeout -k 10 200 python bench.py --ef $ef --steps 30 --warmup 5 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab/$v.$ef.$rep.log 2>&1 || { echo "bench $v failed"; tail -20 gpurun_out/ab/$v.$ef.$rep.log; exit 1; }
-      python - "$v $ef" gpurun_out/ab/$v.$ef.$rep.log <<'PY'
-import json, sys
-d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-ph = d["phase_ms"]
-print(f"{sys.argv[1]:28s} value {d['value']:8.1f} GB/s  ms/bucket {d['ms_per_bucket']:.4f}  " +
-      "  ".join(f"{k} {v*1e3:6.1f}" for k, v in ph.items()))
-PY
-    done
+  for lib in ${AB_LIBS:-product} ${VARIANTS}; do
+    if [ "$lib" = product ]; then L=""; else L="allreducetopk_amd/lib/var/libarctopk_$lib.so"; fi
+    LOG=gpurun_out/ab/${lib}${TAG}.log
+    ARCTOPK_LIB=$L timeout -k 10 200 python bench.py --steps 50 --no-cpu-baseline --no-forced-exchange --wire-busbw ${BENCH_ARGS} > $LOG 2>&1 || { tail -5 $LOG; exit 1; }
+    tail -1 $LOG | python -c "import json,sys; d=json.loads(sys.stdin.read()); p=d['phase_ms']; print('${BENCH_ARGS}', '$lib', d['config']['hook_path'], d['value'], round(d['roofline']['avg_launch_us'],1), round(d['roofline']['hook']['device_us'],1), {k: round(v*1e3,1) for k,v in p.items()})" | tee -a gpurun_out/ab/summary.txt
   done
 done

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-4 counter profile of the short-row workloads: per-kernel SQ instruction / wait
-# counters (occupancy, issue vs latency) in passes of their own (<= 8 SQ + 2 GRBM each).
-# Usage: gpu_r4counters.sh [OUT] ; WL overrides the workloads.
+# Counter profile of bench workloads: per-kernel SQ instruction / wait counters (occupancy,
+# issue vs latency) in rocprofv3 --pmc passes of their own (<= 8 SQ + 2 GRBM each); summarise
+# with scripts/sq_summary.py OUT/<workload>.
+# Usage: gpu_counters.sh [OUT] ; WL overrides the workloads (name or name:extra,args).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

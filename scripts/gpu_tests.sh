@@ -1,11 +1,15 @@
 #!/bin/bash
-# GPU parity suite only (pass extra pytest args, e.g. a -k filter, in PYTEST_ARGS).
+# GPU tests on one box: `bash scripts/gpu_tests.sh [pytest selection...]` (default: the whole
+# -m gpu suite), log in gpurun_out/$OUT/pytest_gpu.log; stops the call on failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+OUT=gpurun_out/${OUT:-tests}
+mkdir -p "$OUT"
+timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 240 --timeout-method thread \
+    > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
-grep -E "PASSED|FAILED|ERROR" gpurun_out/pytest_gpu.log | tail -15
-tail -3 gpurun_out/pytest_gpu.log
-exit $rc
+tail -3 "$OUT/pytest_gpu.log"
+if [ $rc -ne 0 ]; then
+  echo "pytest rc=$rc"; grep -E "Error|FAIL|assert" "$OUT/pytest_gpu.log" | head -40; exit $rc
+fi

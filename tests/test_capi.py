@@ -150,3 +150,33 @@ def test_residual_checks_before_any_kernel():
     table = {0: t}
     got = _residual_on(table, 0, bucket, "error_dict")
     assert got.is_contiguous() and table[0] is got and torch.equal(got, t)
+
+
+@pytest.mark.parametrize("shapes", SHAPE_SETS)
+@pytest.mark.parametrize("target", [1 << 12, 1 << 20, 64 << 20])
+def test_group_runs_cut_only_at_aligned_boundaries(lib, shapes, target):
+    """The exchange groups (arctopk_plan_group): consecutive runs covering every segment once,
+    each starting where the kernels' alignment holds, about `target` bytes each."""
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import group_runs
+    st, segs, info = _describe(lib, shapes)
+    assert st == 0
+    runs = group_runs(segs, info.numel, 4, target)
+    if runs is None:
+        return
+    assert runs[0][0] == 0 and runs[-1][1] == len(segs) and len(runs) >= 2
+    for (a, b), (c, _) in zip(runs, runs[1:]):
+        assert a < b == c
+    for a, _ in runs:
+        s = segs[a]
+        assert s.offset % 8 == 0 and s.sketch_off % 8 == 0 and s.packed_off % 8 == 0 and s.row_off % 4 == 0
+        assert s.kind != N.SEG_SKETCH or s.v_off % 8 == 0
+    assert len(runs) <= -(-info.numel * 4 // target)
+
+
+def test_group_runs_headline_bucket():
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import group_runs
+    st, segs, info = _describe(N.lib(), [[2048, 2048]] * 16)
+    assert group_runs(segs, info.numel, 4, 64 << 20) == [(0, 4), (4, 8), (8, 12), (12, 16)]
+    assert group_runs(segs, info.numel, 4, 256 << 20) is None
+    st, segs, info = _describe(N.lib(), [[32000, 2048]])
+    assert group_runs(segs, info.numel, 4, 64 << 20) is None  # one tensor: never cut

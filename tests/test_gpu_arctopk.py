@@ -429,12 +429,12 @@ def test_select_crowded_first_bin(fill):
         assert torch.all(r_[1:] > r_[:-1])
 
 
-def test_select_first_digit_window_across_calls():
-    """The multi-block select bins the next call's keys in a window centred on the last
-    threshold (mselect.h, arc_digit): calls whose energies stay inside it, jump far above or
-    below it (the k-th key in an edge bin: a full 32-bit radix of that bin), collapse to ties,
-    or come back -- every call exact under the tie rule, on one plan (1 M-row 1x1-conv items,
-    131 K-row 3x3 items, a 40 K-row 2-D item, and 1-D tensors riding along)."""
+def test_select_across_calls_with_jumping_energies():
+    """The multi-block select on one plan over calls whose energies stay put, jump by 1e5 up or
+    1e-7 down, collapse to ties or to zero, and come back (its workspace -- histograms, item
+    states, arrival counters -- is left clean by each call): every call exact under the tie
+    rule (1 M-row 1x1-conv items, 131 K-row 3x3 items, a 40 K-row 2-D item, and 1-D tensors
+    riding along)."""
     shapes = [(2048, 1024, 1, 1), (512, 512, 3, 3), (40000, 8), (2048,), (512,)]
     segs = A.segments(shapes, 0.2)
     plan = BucketPlan(shapes, 4, 0.2, torch.float32, DEV)
@@ -445,7 +445,7 @@ def test_select_first_digit_window_across_calls():
         for s in segs:
             w = s.n if s.kind == A.RAW else s.n * 4
             P = (torch.randn(w, generator=gen) * scale).reshape(-1, 1 if s.kind == A.RAW else 4)
-            if call == 4:  # half the rows tied at one value inside the (moved) window
+            if call == 4:  # half the rows tied at one value
                 P[::2] = P[0]
             Ps.append(P[:, 0].contiguous() if s.kind == A.RAW else P)
         ref = torch.cat([p.flatten() for p in Ps])
@@ -699,3 +699,45 @@ def test_torch_op_layer_matches_direct_calls(ef):
         outs.append([t.clone().cpu() for t in (plan.sketch, plan.rowlist, plan.slotmap, plan.packed, E, gE, G)])
     for a, b_, what in zip(outs[0], outs[1], ("sketch", "rowlist", "slotmap", "packed", "E", "gE", "out")):
         assert_bitwise(b_, a, f"ops vs direct: {what}")
+
+
+@pytest.mark.parametrize("ef", ["noef", "ef21"])
+def test_public_decode_needs_only_its_slot_map(ef):
+    """arctopk_decode on a fresh plan with a slot map and packed buffer built by the caller (no
+    select or pack ever ran on the plan), then again after a pack of OTHER rows on the same
+    plan: the short-row (mode 3) chunks derive their packed ranges from the slot map handed in,
+    never from the plan's last pack."""
+    shapes = [[40, 16, 3, 3], [10], [96, 40], [64, 64, 3, 3], [33, 130], [8, 8, 5, 5]]
+    segs = A.segments(shapes, 0.2)
+    numel = bucket_numel(shapes)
+    plan = BucketPlan([tuple(s) for s in shapes], 4, 0.2, torch.float32, DEV)
+    stream = torch.cuda.current_stream().cuda_stream
+    ws = 2
+    for trial in range(2):
+        g = torch.Generator().manual_seed(77 + trial)
+        rows = [torch.sort(torch.randperm(s.n, generator=g)[:s.k_rows]).values for s in plan.segments]
+        sm = torch.full((plan.info.rows_total,), -1, dtype=torch.int32)
+        packed = torch.zeros(plan.info.packed_len)
+        vals = []
+        for s, r_ in zip(plan.segments, rows):
+            sm[s.row_off + r_] = torch.arange(s.k_rows, dtype=torch.int32)
+            v = torch.randn(s.k_rows * s.m, generator=g)
+            packed[s.packed_off:s.packed_off + v.numel()] = v
+            vals.append(v)
+        gE = torch.randn(numel, generator=g)
+        out = torch.full((numel,), float("nan"), device=DEV)
+        gE_d = gE.to(DEV) if ef == "ef21" else None
+        packed_d, sm_d = packed.to(DEV), sm.to(DEV)  # (kept alive: the allocator reuses freed blocks)
+        N.check(N.lib().arctopk_decode(plan.handle, packed_d.data_ptr(), sm_d.data_ptr(), ws,
+                                       N.EF_CODE[ef], N.ptr(gE_d), out.data_ptr(), stream), "arctopk_decode")
+        torch.cuda.synchronize()
+        ref = A.decode(torch.cat(vals), ws, rows, segs, numel, torch.float32)
+        if ef == "ef21":  # out = gE + scatter(mean); gE[sel] = out[sel]
+            ref = gE + ref
+            assert_bitwise(gE_d, ref, f"trial {trial} gE")
+        assert_bitwise(out, ref, f"trial {trial} output")
+        if trial == 0:  # a pack of other rows on the same plan rewrites the plan's own chunk table
+            G = _rand_bucket(shapes, 5).to(DEV)
+            plan.encode(G, None, N.EF_NONE, True, torch.randn(max(1, plan.info.v_len), device=DEV), stream)
+            plan.select(1, stream)
+            plan.pack(G, None, N.EF_NONE, stream)

@@ -131,3 +131,59 @@ def test_emulated_wire_leaves_results_unchanged(ef):
     for i, what in enumerate(("output", "E", "gE")):
         for b in outs[True][i]:
             assert_bitwise(outs[False][i][b], outs[True][i][b], f"bucket {b} {what}, wire vs RCCL")
+
+
+_WATCHDOG_CHILD = r"""
+import os, sys, time
+sys.path.insert(0, os.getcwd()); sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+import torch
+from parity import ensure_group
+ensure_group("nccl")
+from allreducetopk_amd.bucket import SyntheticBucket
+from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
+st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback="ef14")
+st.force_exchange = True
+st.defer_decode = True
+shapes = [[256, 512], [96, 40], [10]]
+def call(last):
+    x = torch.randn(256 * 512 + 96 * 40 + 10, device="cuda:0")
+    return G.group_topk_hook(st, SyntheticBucket(x, shapes, index=0, is_last=last))
+call(True).wait(); torch.cuda.synchronize()
+assert st._comms[3].timeout_s == 0.2
+torch.cuda._sleep(3_000_000_000)  # the next collectives queue behind ~1 s of GPU time
+call(False)
+time.sleep(3.0)  # the watchdog sees them pending past 0.2 s
+print("ALIVE", flush=True)
+try:
+    call(True)
+except RuntimeError as e:
+    print("RAISED", e, flush=True)
+torch.cuda.synchronize()
+"""
+
+
+@pytest.mark.parametrize("handling", ["default", "0"])
+def test_watchdog_timeout_tears_down_or_raises(handling, tmp_path):
+    """A collective pending past the communicator's timeout (one-rank RCCL behind a GPU sleep,
+    ARCTOPK_COMM_TIMEOUT_S=0.2): by default the watchdog ends the process before any partially
+    reduced update can be applied (ProcessGroupNCCL's async error handling); with
+    ARCTOPK_ASYNC_ERROR_HANDLING=0 the process lives and the next hook call raises."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, ARCTOPK_COMM_TIMEOUT_S="0.2", MASTER_ADDR="127.0.0.1")
+    env.pop("ARCTOPK_ASYNC_ERROR_HANDLING", None)
+    env.pop("TORCH_NCCL_ASYNC_ERROR_HANDLING", None)
+    if handling != "default":
+        env["ARCTOPK_ASYNC_ERROR_HANDLING"] = handling
+    script = tmp_path / "child.py"
+    script.write_text(_WATCHDOG_CHILD)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, str(script)], cwd=repo, env=env, capture_output=True, text=True,
+                       timeout=120)
+    if handling == "default":
+        assert r.returncode == 1, (r.returncode, r.stdout[-1000:], r.stderr[-2000:])
+        assert "ending the process" in r.stderr and "ALIVE" not in r.stdout
+    else:
+        assert r.returncode == 0, (r.returncode, r.stdout[-1000:], r.stderr[-2000:])
+        assert "ALIVE" in r.stdout and "RAISED" in r.stdout and "timed out" in r.stdout
