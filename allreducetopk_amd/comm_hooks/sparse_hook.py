@@ -99,29 +99,23 @@ def _workspace(state, device, numels) -> torch.Tensor:
     return ws
 
 
-def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch.Tensor]":
+def _sparse_hook_impl(state: SparseState, bucket, c4: bool = False) -> "torch.futures.Future[torch.Tensor]":
     if state.use_error_feedback == "ef21" and state.large_batch_init:
-        # reference: sparse_hook_sync_large_batch_ef21 (sparse_hook.py:331-416,
-        # sparse_hook_c4.py:353-457), reached only when large_batch_init is set by hand
-        # (both constructors hard-code False)
-        raise NotImplementedError("the large_batch_init EF21 path is not implemented by the "
-                                  "MI355X codec")
+        # (sparse_hook.py:172-175, sparse_hook_c4.py:201-204)
+        if state.iter < state.start_compress_iter:
+            logger.info("Using large batch initialization in EF21!!")
+        return _large_batch_ef21(state, bucket, c4)
     state.maybe_accumulate_momentum_on_bucket(bucket)
     group = state.process_group if state.process_group is not None else dist.group.WORLD
     world_size = group.size()
     input_tensor = bucket.buffer()
-    tensors = bucket.gradients()
 
     if state.iter < state.start_compress_iter:  # (:190-193)
         state.maybe_increase_iter(bucket)
         return default_hooks._allreduce_fut(group, input_tensor, state)
 
     state._on_compression_start()
-    if state.sparse_type != "tensor":  # the reference crashes for row/column (:96)
-        raise ValueError(f"not enough values to unpack (sparse_type={state.sparse_type!r}: only "
-                         "'tensor' is functional in the reference)")
-    if not input_tensor.is_cuda or input_tensor.dtype not in N.DTYPE_CODE:
-        raise RuntimeError("sparse HIP codec needs a float32 or bfloat16 bucket on a GPU")
+    _check_compressible(state, input_tensor)
     L = N.lib()
     device = input_tensor.device
     dtype = input_tensor.dtype
@@ -164,8 +158,38 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
     if state.random:  # shared reseed so every rank draws the same indices (:230-235)
         seed = torch.randint(0, 1_000_000_000, (1,), generator=state.rng).item()
         torch.manual_seed(seed)
+    _compress_exchange(state, bucket, group, world_size, ef, state._call_ratio(), seed,
+                       e_decay=decay, g_decay=decay, count_bits=True)
+    state.maybe_increase_iter(bucket)
+    fut = torch.futures.Future()
+    fut.set_result(input_tensor)
+    return fut
 
-    ratio = state._call_ratio()
+
+def _check_compressible(state: SparseState, input_tensor: torch.Tensor) -> None:
+    if state.sparse_type != "tensor":  # the reference crashes for row/column (:96)
+        raise ValueError(f"not enough values to unpack (sparse_type={state.sparse_type!r}: only "
+                         "'tensor' is functional in the reference)")
+    if not input_tensor.is_cuda or input_tensor.dtype not in N.DTYPE_CODE:
+        raise RuntimeError("sparse HIP codec needs a float32 or bfloat16 bucket on a GPU")
+
+
+def _compress_exchange(state: SparseState, bucket, group, world_size: int, ef: int, ratio: float,
+                       seed, e_decay: float, g_decay: float, count_bits: bool, on_values=None) -> None:
+    """The compressed call after the EF pre-apply, on the caller's stream: select (TopK) or draw
+    (RandK) the indices, gather the values, persist the residual (EF14: E[idx] = 0; EF21:
+    E[idx] += e_decay * values), exchange (RandK: all-reduce; TopK: all-gather of values and
+    indices) and decode into the bucket (EF21: gE += g_decay * out, out = gE).
+    Reference: sparse_hook.py:237-297 (and :363-410 for the large-batch hook)."""
+    L = N.lib()
+    input_tensor = bucket.buffer()
+    tensors = bucket.gradients()
+    device = input_tensor.device
+    dtype = input_tensor.dtype
+    b = bucket.index()
+    total = input_tensor.shape[0]
+    stream = torch.cuda.current_stream(device).cuda_stream
+    dt = N.DTYPE_CODE[dtype]
     numels = [t.numel() for t in tensors]
     ks = [max(1, int(n * ratio)) for n in numels]
     offsets: List[int] = []
@@ -218,21 +242,25 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
     # the call's selection, for inspection and tests (int32 indices per tensor, concatenated
     # in bucket order at the k offsets; TopK: ascending within a tensor)
     state.last_indices, state.last_k = indices, ks
+    if on_values is not None:
+        on_values(values)
     if ef != N.EF_NONE and not (fold14 and not state.random):  # residual persistence (:257-267)
         N.check(L.arctopk_sparse_residual(state.error_dict[b].data_ptr(), nt, a_off, a_k, a_ko,
-                                          indices.data_ptr(), values.data_ptr(), ef, decay, dt, stream),
+                                          indices.data_ptr(), values.data_ptr(), ef, e_decay, dt, stream),
                 "arctopk_sparse_residual")
     gerr = state.global_error_dict[b].data_ptr() if ef == N.EF21 else None
 
     if state.random:
-        state.comm_bits_this_round += 2 * (world_size - 1) * bits_sum
+        if count_bits:
+            state.comm_bits_this_round += 2 * (world_size - 1) * bits_sum
         if world_size > 1:
             dist.all_reduce(values, group=group, async_op=False)
         N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, indices.data_ptr(),
-                                        values.data_ptr(), 1, world_size, 0, gerr, decay, dt, stream),
+                                        values.data_ptr(), 1, world_size, 0, gerr, g_decay, dt, stream),
                 "arctopk_sparse_decode")
     else:
-        state.comm_bits_this_round += (world_size - 1) * world_size * bits_sum
+        if count_bits:
+            state.comm_bits_this_round += (world_size - 1) * world_size * bits_sum
         if world_size > 1:
             all_vals = torch.empty(world_size * sum_k, dtype=dtype, device=device)
             all_idx = torch.empty(world_size * sum_k, dtype=torch.int32, device=device)
@@ -242,8 +270,74 @@ def _sparse_hook_impl(state: SparseState, bucket) -> "torch.futures.Future[torch
             all_vals, all_idx = values, indices
         N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, all_idx.data_ptr(),
                                         all_vals.data_ptr(), world_size, world_size, 1, gerr,
-                                        decay, dt, stream), "arctopk_sparse_decode")
+                                        g_decay, dt, stream), "arctopk_sparse_decode")
 
+
+def _large_batch_ef21(state: SparseState, bucket, c4: bool) -> "torch.futures.Future[torch.Tensor]":
+    """EF21 with large-batch initialisation (reference sparse_hook.py:307-416; the registered
+    copy sparse_hook_c4.py:353-457), reached when ``state.large_batch_init`` is set by hand:
+
+    - iteration 0: the reference calls ``default_hooks._allreduce_fut`` without its required
+      ``hook_state`` argument, so it raises TypeError (after advancing ``iter``); so does this;
+    - 1 <= iter < start_compress_iter: E += G; the bucket is all-reduced and averaged; gE += it;
+    - iter == start_compress_iter: E and gE are divided by start_compress_iter - 1;
+    - compressed calls: D = G - E, C(D) at ``compress_ratio`` (never the gradual ratio),
+      E += C(D) (alpha 1), the exchange, gE += error_decay * out, out = gE.  No communication
+      bits are counted (the reference counts none in this hook).  The registered copy then
+      fails in the reference (its ``cal_k(state, tensor)`` is called as ``cal_k(tensor,
+      ratio)``: AttributeError, sparse_hook_c4.py:421); with ``c4`` so does this, at the same
+      point (after the residual division, the pre-apply and the reseed)."""
+    assert state.use_error_feedback == "ef21", "This hook is only for EF21"
+    assert state.large_batch_init, "This hook is only for large batch initialization"
+    state.maybe_accumulate_momentum_on_bucket(bucket)
+    group = state.process_group if state.process_group is not None else dist.group.WORLD
+    world_size = group.size()
+    input_tensor = bucket.buffer()
+    b = bucket.index()
+    total = input_tensor.shape[0]
+    if state.iter < 1:
+        state.maybe_increase_iter(bucket)
+        raise TypeError("_allreduce_fut() missing 1 required positional argument: 'hook_state'")
+    if state.iter < state.start_compress_iter:
+        if b not in state.error_dict:
+            logger.info("A tensor of length %s that represents local/global error is created.", total)
+            state.error_dict[b] = torch.zeros(total, device=input_tensor.device, dtype=input_tensor.dtype)
+            state.global_error_dict[b] = torch.zeros(total, device=input_tensor.device, dtype=input_tensor.dtype)
+        state.error_dict[b].add_(input_tensor, alpha=1.0)
+        dist.all_reduce(input_tensor, group=group, async_op=False)
+        input_tensor.div_(world_size)
+        state.global_error_dict[b].add_(input_tensor, alpha=1.0)
+        state.maybe_increase_iter(bucket)
+        fut = torch.futures.Future()
+        fut.set_result(input_tensor)
+        return fut
+    if state.iter == state.start_compress_iter:
+        state.error_dict[b].div_(state.start_compress_iter - 1)
+        state.global_error_dict[b].div_(state.start_compress_iter - 1)
+    _check_compressible(state, input_tensor)
+    err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
+    _residual_on(state.global_error_dict, b, input_tensor, "global_error_dict")
+    L = N.lib()
+    stream = torch.cuda.current_stream(input_tensor.device).cuda_stream
+    N.check(L.arctopk_ef_apply(input_tensor.data_ptr(), err.data_ptr(), total, N.EF21, 1,
+                               N.DTYPE_CODE[input_tensor.dtype], stream), "arctopk_ef_apply")
+    seed = None
+    if state.random:
+        seed = torch.randint(0, 1_000_000_000, (1,), generator=state.rng).item()
+        torch.manual_seed(seed)
+    if c4:
+        raise AttributeError("'Tensor' object has no attribute 'get_current_compress_ratio'")
+    log_diff = bucket.is_last() and dist.get_rank() == 0 and logger.isEnabledFor(logging.INFO)
+    sq = [None]
+    if log_diff:  # |D - C(D)| = sqrt(|D|^2 - |values|^2): only computed when the log is on
+        dn = input_tensor.float().pow(2).sum()
+        sq[0] = lambda v: float((dn - v.float().pow(2).sum()).clamp_min(0).sqrt())
+    vals_seen = []
+    _compress_exchange(state, bucket, group, world_size, N.EF21, state.compress_ratio, seed,
+                       e_decay=1.0, g_decay=float(state.error_decay), count_bits=False,
+                       on_values=vals_seen.append if log_diff else None)
+    if log_diff:
+        logger.info(f"Rank[{dist.get_rank()}] Iter[{state.iter}], Diff error{sq[0](vals_seen[0])}")
     state.maybe_increase_iter(bucket)
     fut = torch.futures.Future()
     fut.set_result(input_tensor)

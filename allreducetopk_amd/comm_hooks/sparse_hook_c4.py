@@ -62,4 +62,4 @@ def cal_k(state, tensor):
 
 def sparse_hook_sync(state: SparseState, bucket: dist.GradBucket
                      ) -> torch.futures.Future[torch.Tensor]:
-    return _base._sparse_hook_impl(state, bucket)
+    return _base._sparse_hook_impl(state, bucket, c4=True)

@@ -123,14 +123,16 @@ def decode_topk(all_vals: List[torch.Tensor], all_idx: List[torch.Tensor], shape
 
 
 def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed: Optional[int],
-                  indices_override=None, error_decay: float = 1.0):
+                  indices_override=None, error_decay: float = 1.0, residual_decay: Optional[float] = None):
     """One steady-state compressed call on len(Gs) ranks in one process.
 
     ``indices_override``: per rank, a list of per-tensor index tensors (RandK draws
     made elsewhere, e.g. by the device generator).  ``error_decay``: EF21's residual scaling
     (``E.add_(C, alpha=error_decay)``, ``gE.add_(out, alpha=error_decay)``, sparse_hook.py:265,
-    :296; sparse_hook_c4.py:311, :342).
+    :296; sparse_hook_c4.py:311, :342).  ``residual_decay`` overrides the local residual's
+    factor (the large-batch hook adds C with alpha 1.0 but scales gE: sparse_hook.py:386, :410).
     """
+    e_decay = error_decay if residual_decay is None else residual_decay
     ws = len(Gs)
     Xs, packs = [], []
     for q, (G, E) in enumerate(zip(Gs, Es)):
@@ -152,7 +154,7 @@ def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed:
         if ef == "ef14":
             E_new.append(X.clone())
         elif ef == "ef21":  # X holds C(D): zero except the selection (:265)
-            E_new.append(E.clone().add_(X, alpha=error_decay))
+            E_new.append(E.clone().add_(X, alpha=e_decay))
         else:
             E_new.append(None)
     gE_new = None
@@ -161,3 +163,67 @@ def simulate_step(Gs, Es, gE, shapes, ratio: float, ef: str, random: bool, seed:
         out = gE_new.clone()
     return dict(X=Xs, values=[p[0] for p in packs], indices=[p[1] for p in packs], ks=ks,
                 bits=packs[0][3], out=out, E_new=E_new, gE_new=gE_new)
+
+
+@dataclass
+class LargeBatchState:
+    """The EF21 large-batch-initialisation hook's state (sparse_hook.py:307-416, reached when
+    ``state.large_batch_init`` is set by hand), for ``ws`` ranks simulated in one process."""
+    ws: int
+    shapes: list
+    ratio: float
+    random: bool
+    start: int
+    seed: int = 0
+    error_decay: float = 1.0
+    iter: int = 0
+    Es: Optional[List[torch.Tensor]] = None
+    gE: Optional[torch.Tensor] = None
+    rng: torch.Generator = field(default=None)
+
+    def __post_init__(self):
+        if self.rng is None:
+            self.rng = torch.Generator().manual_seed(int(self.seed))
+
+
+def large_batch_call(st: LargeBatchState, Gs: List[torch.Tensor]) -> dict:
+    """One call of sparse_hook_sync_large_batch_ef21 on every rank (one bucket, iter advancing
+    as for the last bucket).  Returns dict(out, E, gE, seed, indices) after the call.
+
+      iter < 1            : TypeError (the reference calls default_hooks._allreduce_fut without
+                            its required hook_state, :336-338), after iter += 1
+      1 <= iter < start   : E += G; out = all_reduce(G) / ws; gE += out            (:339-353)
+      iter == start       : E /= start - 1; gE /= start - 1                         (:354-356)
+      iter >= start       : D = G - E; C = sparsify(D) (compress_ratio, not the gradual one);
+                            E += C; out = mean of C over ranks (RandK: all_reduce / ws;
+                            TopK: rank-ordered scatter-add / ws); gE += error_decay * out;
+                            out = gE                                                 (:358-410)
+    The hook counts no communication bits."""
+    ws = st.ws
+    if st.iter < 1:
+        st.iter += 1
+        raise TypeError("_allreduce_fut() missing 1 required positional argument: 'hook_state'")
+    if st.iter < st.start:
+        if st.Es is None:
+            st.Es = [torch.zeros_like(G) for G in Gs]
+            st.gE = torch.zeros_like(Gs[0])
+        for E, G in zip(st.Es, Gs):
+            E.add_(G, alpha=1.0)
+        acc = Gs[0].clone()
+        for q in range(1, ws):
+            acc = acc + Gs[q]
+        acc.div_(ws)
+        st.gE.add_(acc, alpha=1.0)
+        st.iter += 1
+        return dict(out=acc, E=[E.clone() for E in st.Es], gE=st.gE.clone(), seed=None, indices=None)
+    if st.iter == st.start:
+        for E in st.Es:
+            E.div_(st.start - 1)
+        st.gE.div_(st.start - 1)
+    seed = int(torch.randint(0, 1_000_000_000, (1,), generator=st.rng).item()) if st.random else None
+    res = simulate_step(Gs, st.Es, st.gE, st.shapes, st.ratio, "ef21", st.random, seed,
+                        error_decay=st.error_decay, residual_decay=1.0)
+    st.Es, st.gE = res["E_new"], res["gE_new"]
+    st.iter += 1
+    return dict(out=res["out"], E=[E.clone() for E in st.Es], gE=st.gE.clone(), seed=seed,
+                indices=res["indices"])

@@ -95,6 +95,19 @@ CASES += [
          ratio=0.2, ef="ef21", ws=2, iters=3, start=0, seed=5, error_decay=0.7),
     dict(name="topk_c4_gradual_ef21_decay09_ws1", hook="sparse_c4", random=False, shapes=SPARSE_MIX,
          ratio=0.2, ef="ef21", ws=1, iters=3, start=1, seed=5, error_decay=0.9),
+    # EF21 with large-batch initialisation (state.large_batch_init, set by hand: both
+    # constructors fix False; sparse_hook.py:172-175 -> :307-416).  Its iteration-0 branch calls
+    # default_hooks._allreduce_fut without the required hook_state and raises TypeError, and the
+    # registered copy (sparse_hook_c4.py:353-457) also fails at its first compressed call
+    # (large_batch_errors.json), so these runs use sparse_hook and start at iteration 1 (iter0):
+    # two accumulating dense iterations, then the averaged residuals and compressed calls.
+    dict(name="topk_largebatch_ef21_ws1", hook="sparse", random=False, shapes=SPARSE_MIX,
+         ratio=0.2, ef="ef21", ws=1, iters=4, start=3, seed=5, large_batch=True, iter0=1),
+    dict(name="topk_largebatch_ef21_decay07_ws2", hook="sparse", random=False, shapes=SPARSE_MIX,
+         ratio=0.2, ef="ef21", ws=2, iters=4, start=3, seed=5, large_batch=True, iter0=1,
+         error_decay=0.7),
+    dict(name="randk_largebatch_ef21_ws2", hook="sparse", random=True, shapes=SPARSE_MIX,
+         ratio=0.2, ef="ef21", ws=2, iters=4, start=3, seed=9, large_batch=True, iter0=1),
 ]
 
 
@@ -171,6 +184,9 @@ def make_state(case):
     st, hook = _make_state(case)
     if "error_decay" in case:
         st.error_decay = case["error_decay"]
+    if case.get("large_batch"):
+        st.large_batch_init = True
+    st.iter = case.get("iter0", 0)
     return st, hook
 
 
@@ -260,6 +276,35 @@ def make_error_case():
     return "no-error"
 
 
+def large_batch_errors(rank, port, outdir):
+    """How the large-batch EF21 hooks fail (sparse_hook.py:336-338, sparse_hook_c4.py:384-386 at
+    iteration 0; sparse_hook_c4.py:421 at the first compressed call): exception, message, and
+    the iteration counter afterwards."""
+    sys.path.insert(0, REFERENCE)
+    sys.dont_write_bytecode = True
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    out = {}
+    for tag, hook_name, iter0 in (("sparse_iter0", "sparse", 0), ("sparse_c4_iter0", "sparse_c4", 0),
+                                  ("sparse_c4_compressed", "sparse_c4", 3)):
+        case = dict(hook=hook_name, random=False, ratio=0.2, start=3, ef="ef21", seed=5, large_batch=True,
+                    iter0=iter0)
+        state, hook = make_state(case)
+        if iter0 >= 3:  # residuals as the accumulating iterations leave them
+            state.error_dict[0] = torch.zeros(bucket_numel(SPARSE_MIX))
+            state.global_error_dict[0] = torch.zeros(bucket_numel(SPARSE_MIX))
+        bucket = SyntheticBucket(torch.randn(bucket_numel(SPARSE_MIX)), SPARSE_MIX, index=0, is_last=True)
+        try:
+            hook(state, bucket)
+            res = dict(raises="no-error")
+        except Exception as e:  # noqa: BLE001 -- recorded as the reference's behaviour
+            res = dict(raises=type(e).__name__, message=str(e))
+        res["iter_after"] = int(state.iter)
+        out[tag] = res
+    with open(os.path.join(outdir, "err.json"), "w") as f:
+        json.dump(out, f)
+    dist.destroy_process_group()
+
+
 def main():
     meta_common = dict(torch=torch.__version__, cpu_capability=torch.backends.cpu.get_cpu_capability(),
                        reference="Aris-ma/AllreduceTopK @ /root/reference (read-only)")
@@ -282,6 +327,13 @@ def main():
     err = make_error_case()
     with open(os.path.join(HERE, "nd_indivisible_error.json"), "w") as f:
         json.dump(dict(meta_common, shape=[3, 5, 2], r=4, ratio=0.2, raises=err), f, indent=1)
+    with tempfile.TemporaryDirectory() as td:
+        port = free_port()
+        mp.spawn(large_batch_errors, args=(port, td), nprocs=1, join=True)
+        with open(os.path.join(td, "err.json")) as f:
+            res = json.load(f)
+    with open(os.path.join(HERE, "large_batch_errors.json"), "w") as f:
+        json.dump(dict(meta_common, cases=res), f, indent=1)
 
 
 if __name__ == "__main__":

@@ -419,6 +419,8 @@ def _golden_ws2_worker(rank, ws, port, name):
                              random_seed=m["seed"])
         st.index_source = "host"  # RandK: the reference's CPU randperm draws (the fixtures')
         st.error_decay = m.get("error_decay", 1.0)
+        if m.get("large_batch"):  # EF21 large-batch initialisation, from iteration iter0
+            st.large_batch_init, st.iter = True, m["iter0"]
         hook = mod.sparse_hook_sync
     bf16 = m.get("dtype") == "bf16"
     from oracle import arctopk as A
@@ -464,7 +466,8 @@ def _golden_ws2_worker(rank, ws, port, name):
 
 @pytest.mark.parametrize("name", ["arc_mix_ef14_ws2", "arc_mix_ef21_ws2", "arc_warmup_ef21_ws2",
                                   "arc_mix_noef_bf16_ws2", "topk_mix_ef14_ws2", "topk_mix_ef21_ws2",
-                                  "topk_mix_ef21_decay07_ws2", "randk_mix_noef_ws2"])
+                                  "topk_mix_ef21_decay07_ws2", "randk_mix_noef_ws2",
+                                  "topk_largebatch_ef21_decay07_ws2", "randk_largebatch_ef21_ws2"])
 def test_reference_ws2_golden_through_hip_hook(name):
     """Every ws=2 fixture of the reference, RandK included (index_source="host": its CPU
     torch.randperm draws, sparse_hook_c4.py:20)."""

@@ -180,6 +180,8 @@ def test_topk_golden_on_gpu(name):
                          sparse_type="tensor", random=False, use_error_feedback=m["ef"],
                          random_seed=m["seed"])
     st.error_decay = m.get("error_decay", 1.0)  # EF21 residual scaling (set by hand, as a driver would)
+    if m.get("large_batch"):  # EF21 large-batch initialisation (set by hand; from iteration iter0)
+        st.large_batch_init, st.iter = True, m["iter0"]
     shapes = [tuple(s) for s in m["shapes"]]
     for it in range(m["iters"]):
         out = mod.sparse_hook_sync(st, SyntheticBucket(g.t(0, it, "G").to(DEV), shapes)).wait()
@@ -190,6 +192,7 @@ def test_topk_golden_on_gpu(name):
         if g.has(0, it, "gE"):
             assert_bitwise(st.global_error_dict[0], g.t(0, it, "gE"), f"{name} it{it} gE")
         assert st.comm_bits_this_round == int(g.np(0, it, "bits"))
+        assert st.iter == int(g.np(0, it, "iter_after"))
 
 
 @pytest.mark.parametrize("name", [n for n in case_names("randk_") if n.endswith("ws1")])
@@ -312,3 +315,37 @@ def test_randk_hook_bf16_vs_oracle(ef):
         if ef == "ef21":
             assert_bitwise(st.global_error_dict[0], res["gE_new"], f"it{it} gE")
             gE = res["gE_new"]
+
+
+@pytest.mark.parametrize("c4", [False, True])
+def test_large_batch_ef21_failures_match_reference(c4):
+    """The reference's large-batch EF21 hook raises TypeError at iteration 0 (its
+    default_hooks._allreduce_fut call lacks the required hook_state), and its registered copy
+    raises AttributeError at the first compressed call (cal_k(state, tensor) called as
+    cal_k(tensor, ratio)): the same exceptions at the same points (tests/golden/
+    large_batch_errors.json)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large_batch_errors.json")) as f:
+        cases = json.load(f)["cases"]
+    mod = sparse_hook_c4 if c4 else sparse_hook
+    shapes = [(10,), (40, 16), (4, 3, 3, 3), (96, 40)]
+    st = mod.SparseState(None, compress_ratio=0.2, start_compress_iter=3, sparse_type="tensor",
+                         use_error_feedback="ef21")
+    st.large_batch_init = True
+    mk = lambda: SyntheticBucket(_rand(shapes, 3).to(DEV), shapes)  # noqa: E731
+    ref = cases["sparse_c4_iter0" if c4 else "sparse_iter0"]
+    with pytest.raises(TypeError) as ei:
+        mod.sparse_hook_sync(st, mk())
+    assert str(ei.value) == ref["message"] and st.iter == ref["iter_after"]
+    mod.sparse_hook_sync(st, mk()).wait()  # iterations 1, 2: accumulate
+    mod.sparse_hook_sync(st, mk()).wait()
+    if c4:
+        ref = cases["sparse_c4_compressed"]
+        with pytest.raises(AttributeError) as ei:
+            mod.sparse_hook_sync(st, mk())
+        assert str(ei.value) == ref["message"] and st.iter == ref["iter_after"]
+    else:
+        mod.sparse_hook_sync(st, mk()).wait()
+        assert st.iter == 4
+    torch.cuda.synchronize()

@@ -92,7 +92,10 @@ def test_arc_oracle_matches_reference(name):
             assert int(g.np(q, it, "bits")) == bits, f"{name} it{it} comm bits"
 
 
-@pytest.mark.parametrize("name", case_names("topk_") + case_names("randk_"))
+SPARSE_CASES = [n for n in case_names("topk_") + case_names("randk_") if "largebatch" not in n]
+
+
+@pytest.mark.parametrize("name", SPARSE_CASES)
 def test_sparse_oracle_matches_reference(name):
     g = Golden(name)
     m = g.meta
@@ -184,3 +187,37 @@ def test_projection_stream_equals_global_reseed():
     mine = A.draw_projections(424242, segs, 4)
     for a, b in zip(ref, mine):
         assert (a is None and b is None) or torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name", [n for n in case_names() if "largebatch" in n])
+def test_large_batch_oracle_matches_reference(name):
+    """EF21 with large-batch initialisation (sparse_hook.py:307-416), iterations 1 .. 4 of the
+    reference's own run: accumulating dense calls, the averaged residuals, compressed calls."""
+    g = Golden(name)
+    m = g.meta
+    ws = m["ws"]
+    st = S.LargeBatchState(ws=ws, shapes=[tuple(s) for s in m["shapes"]], ratio=m["ratio"], random=m["random"],
+                           start=m["start"], seed=m["seed"], error_decay=m.get("error_decay", 1.0),
+                           iter=m["iter0"])
+    for it in range(m["iters"]):
+        Gs = [g.t(q, it, "G") for q in range(ws)]
+        res = S.large_batch_call(st, Gs)
+        if res["seed"] is not None:
+            assert int(g.np(0, it, "seed")[0]) == res["seed"]
+        for q in range(ws):
+            _eq(res["out"], g.t(q, it, "out"), f"{name} it{it} r{q} out")
+            _eq(res["E"][q], g.t(q, it, "E"), f"{name} it{it} r{q} E")
+            _eq(res["gE"], g.t(q, it, "gE"), f"{name} it{it} r{q} gE")
+            assert int(g.np(q, it, "bits")) == 0, "the large-batch hook counts no bits"
+            assert int(g.np(q, it, "iter_after")) == st.iter
+
+
+def test_large_batch_errors_match_reference():
+    with open(os.path.join(GOLDEN, "large_batch_errors.json")) as f:
+        cases = json.load(f)["cases"]
+    st = S.LargeBatchState(ws=1, shapes=[(10,)], ratio=0.2, random=False, start=3)
+    with pytest.raises(TypeError) as ei:
+        S.large_batch_call(st, [torch.zeros(10)])
+    assert (type(ei.value).__name__, str(ei.value), st.iter) == (
+        cases["sparse_iter0"]["raises"], cases["sparse_iter0"]["message"], cases["sparse_iter0"]["iter_after"])
+    assert cases["sparse_c4_compressed"]["raises"] == "AttributeError"
