@@ -276,7 +276,7 @@ class BucketPlan:
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h is not None and N._lib is not None:
+        if h is not None and N is not None and N._lib is not None:
             try:
                 N._lib.arctopk_plan_destroy(h)
             except Exception:  # interpreter shutdown
@@ -369,7 +369,7 @@ class GroupPlan:
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h is not None and N._lib is not None:
+        if h is not None and N is not None and N._lib is not None:
             try:
                 N._lib.arctopk_plan_destroy(h)
             except Exception:  # interpreter shutdown

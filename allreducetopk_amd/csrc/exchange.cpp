@@ -245,20 +245,22 @@ class Watchdog {
                 }
             }
             if (fail) {
-                fail_all_locked(fail);
                 if (teardown_on_failure()) {
                     // as ProcessGroupNCCL's async error handling: work queued behind the failed
                     // collective (decode, copy-back, optimizer step) would run on partially
-                    // reduced buffers once the aborted kernels exit, so the process ends here
+                    // reduced buffers once the aborted kernels exit, so the process ends here,
+                    // before any abort (ncclCommAbort may wait for the device; exiting releases
+                    // the communicators and the peers' own watchdogs see this rank gone)
                     std::fprintf(stderr,
                                  "[arctopk] exchange watchdog: a collective failed or stayed pending past the "
-                                 "timeout (status %d); communicators aborted, ending the process so that no "
-                                 "partially reduced update is applied (ARCTOPK_ASYNC_ERROR_HANDLING=0 or 2: "
-                                 "raise from the hook instead)\n",
+                                 "timeout (status %d); ending the process so that no partially reduced "
+                                 "update is applied (ARCTOPK_ASYNC_ERROR_HANDLING=0 or 2: abort the "
+                                 "communicators and raise from the hook instead)\n",
                                  fail);
                     std::fflush(stderr);
                     std::_Exit(1);
                 }
+                fail_all_locked(fail);
             }
         }
     }

@@ -219,8 +219,8 @@ int arctopk_comm_init_rccl(const char* rccl_path, const void* id, int32_t nranks
  * arctopk_comm_status returns it, and every later exchange step on the communicator returns
  * it instead of enqueueing work.  Work already queued behind the failed collective (the decode,
  * the caller's copy-back and optimizer step) would then run on partially reduced buffers, so,
- * as ProcessGroupNCCL's async error handling does by default, the watchdog then ends the
- * process (stderr message, exit status 1).  ARCTOPK_ASYNC_ERROR_HANDLING (else torch's
+ * as ProcessGroupNCCL's async error handling does by default, the watchdog ends the process
+ * instead of aborting (stderr message, exit status 1).  ARCTOPK_ASYNC_ERROR_HANDLING (else torch's
  * TORCH_NCCL_ASYNC_ERROR_HANDLING) = 0 or 2 keeps it alive: the error is then raised by the
  * next exchange step.  arctopk_comm_init_rccl = timeout 0: blocking creation, no watchdog.  The
  * device current on the calling thread is left unchanged.

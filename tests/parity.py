@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import os
 import socket
+import tempfile
 
 import torch
 import torch.distributed as dist
@@ -16,13 +17,21 @@ def free_port() -> int:
     return p
 
 
+def rendezvous() -> str:
+    """A file:// rendezvous for a new process group: no TCP port to race for (a port from
+    free_port() can be taken by another process before the store listens on it)."""
+    fd, path = tempfile.mkstemp(prefix="arctopk_rdzv_")
+    os.close(fd)
+    os.unlink(path)  # (the FileStore creates it)
+    return "file://" + path
+
+
 def ensure_group(backend: str) -> None:
     """A world_size-1 process group (the hooks call torch.distributed collectives)."""
     if dist.is_initialized():
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(free_port())
-    dist.init_process_group(backend, rank=0, world_size=1)
+    dist.init_process_group(backend, init_method=rendezvous(), rank=0, world_size=1)
 
 
 def check_rows_tie_aware(rows, energy_ref: torch.Tensor, k: int, band: float = 0.0):

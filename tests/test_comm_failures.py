@@ -26,7 +26,7 @@ REPO = os.path.dirname(HERE)
 def _callback_worker(rank, ws, port, td):
     sys.path.insert(0, REPO)
     sys.path.insert(0, HERE)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws,
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=ws,
                             timeout=datetime.timedelta(seconds=3))
     from allreducetopk_amd import _native as N
     from allreducetopk_amd import exchange as X
@@ -50,8 +50,8 @@ def _callback_worker(rank, ws, port, td):
 
 
 def test_callback_comm_peer_never_answers_raises_runtime_error():
-    from parity import free_port
-    port = free_port()
+    from parity import rendezvous
+    port = rendezvous()
     with tempfile.TemporaryDirectory() as td:
         mp.spawn(_callback_worker, args=(2, port, td), nprocs=2, join=True)
         assert os.path.exists(os.path.join(td, "r0_raised"))
@@ -76,12 +76,11 @@ def test_store_keys_are_group_deterministic():
 
 def test_group_timeout_is_read_from_the_process_group():
     from allreducetopk_amd import exchange as X
-    from parity import free_port
+    from parity import rendezvous
     if dist.is_initialized():
         pytest.skip("a process group is already initialised in this process")
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(free_port())
-    dist.init_process_group("gloo", rank=0, world_size=1, timeout=datetime.timedelta(seconds=42))
+    dist.init_process_group("gloo", init_method=rendezvous(), rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=42))
     try:
         assert X.group_timeout_s(dist.group.WORLD) == 42.0
         g = dist.new_group([0], timeout=datetime.timedelta(seconds=7))

@@ -24,13 +24,13 @@ def _setup(rank, ws, port):
     sys.path.insert(0, REPO)
     sys.path.insert(0, HERE)
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+    dist.init_process_group("gloo", init_method=port, rank=rank,
                             world_size=ws)
 
 
 def _spawn(fn, *args, ws=2):
-    from parity import free_port
-    port = free_port()
+    from parity import rendezvous
+    port = rendezvous()
     with tempfile.TemporaryDirectory() as td:
         mp.spawn(fn, args=(ws, port, td) + args, nprocs=ws, join=True)
 

@@ -134,11 +134,12 @@ def test_emulated_wire_leaves_results_unchanged(ef):
 
 
 _WATCHDOG_CHILD = r"""
-import os, sys, time
+import ctypes, os, sys, time
 sys.path.insert(0, os.getcwd()); sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
 import torch
 from parity import ensure_group
 ensure_group("nccl")
+from allreducetopk_amd import _native as N
 from allreducetopk_amd.bucket import SyntheticBucket
 from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
 st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback="ef14")
@@ -149,29 +150,35 @@ def call(last):
     x = torch.randn(256 * 512 + 96 * 40 + 10, device="cuda:0")
     return G.group_topk_hook(st, SyntheticBucket(x, shapes, index=0, is_last=last))
 call(True).wait(); torch.cuda.synchronize()
-assert st._comms[3].timeout_s == 0.2
-torch.cuda._sleep(3_000_000_000)  # the next collectives queue behind ~1 s of GPU time
+assert st._comms[3].timeout_s == 2.0
+# a GPU "sleep" of exactly 6 s on the hook's stream (the emulated-wire kernel paced by the
+# constant-rate clock), so the next collectives stay pending past the 2 s timeout
+w = ctypes.c_void_p()
+N.check(N.lib().arctopk_comm_init_wire(2, 1.0, 6.0e6, 1, 0, ctypes.byref(w)), "wire")
+buf = torch.zeros(64, device="cuda:0")
+N.check(N.lib().arctopk_comm_allreduce(w, buf.data_ptr(), 64, N.F32, torch.cuda.current_stream().cuda_stream), "sleep")
 call(False)
-time.sleep(3.0)  # the watchdog sees them pending past 0.2 s
+time.sleep(4.5)  # the watchdog sees them pending past 2 s
 print("ALIVE", flush=True)
 try:
     call(True)
 except RuntimeError as e:
     print("RAISED", e, flush=True)
 torch.cuda.synchronize()
+N.lib().arctopk_comm_destroy(w)
 """
 
 
 @pytest.mark.parametrize("handling", ["default", "0"])
 def test_watchdog_timeout_tears_down_or_raises(handling, tmp_path):
-    """A collective pending past the communicator's timeout (one-rank RCCL behind a GPU sleep,
-    ARCTOPK_COMM_TIMEOUT_S=0.2): by default the watchdog ends the process before any partially
+    """A collective pending past the communicator's timeout (one-rank RCCL behind a 6 s GPU
+    sleep, ARCTOPK_COMM_TIMEOUT_S=2): by default the watchdog ends the process before any partially
     reduced update can be applied (ProcessGroupNCCL's async error handling); with
     ARCTOPK_ASYNC_ERROR_HANDLING=0 the process lives and the next hook call raises."""
     import os
     import subprocess
     import sys
-    env = dict(os.environ, ARCTOPK_COMM_TIMEOUT_S="0.2", MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, ARCTOPK_COMM_TIMEOUT_S="2.0", MASTER_ADDR="127.0.0.1")
     env.pop("ARCTOPK_ASYNC_ERROR_HANDLING", None)
     env.pop("TORCH_NCCL_ASYNC_ERROR_HANDLING", None)
     if handling != "default":

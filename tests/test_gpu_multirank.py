@@ -28,7 +28,7 @@ def _worker(rank, ws, port, td, ef, kind):
     sys.path.insert(0, REPO)
     sys.path.insert(0, HERE)
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+    dist.init_process_group("gloo", init_method=port, rank=rank,
                             world_size=ws)
     from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
@@ -106,8 +106,8 @@ def _worker(rank, ws, port, td, ef, kind):
                                      ("arc_sync", "ef14"), ("arc_sync", "ef21"),
                                      ("topk", "ef14"), ("topk", "ef21"), ("randk", "ef14")])
 def test_two_ranks_one_gpu(kind, ef):
-    from parity import free_port
-    port = free_port()
+    from parity import rendezvous
+    port = rendezvous()
     with tempfile.TemporaryDirectory() as td:
         mp.spawn(_worker, args=(2, port, td, ef, kind), nprocs=2, join=True)
 
@@ -128,7 +128,7 @@ def _worker_multi(rank, ws, port, ef, sketch_comm, steps):
     sys.path.insert(0, HERE)
     os.environ["ARCTOPK_SKETCH_COMM"] = sketch_comm
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+    dist.init_process_group("gloo", init_method=port, rank=rank,
                             world_size=ws)
     from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
@@ -191,8 +191,8 @@ def _worker_multi(rank, ws, port, ef, sketch_comm, steps):
 @pytest.mark.parametrize("ef,sketch_comm", [("ef14", "separate"), ("ef21", "separate"),
                                             ("noef", "shared"), ("ef14", "shared")])
 def test_two_ranks_buckets_in_flight(ef, sketch_comm):
-    from parity import free_port
-    mp.spawn(_worker_multi, args=(2, free_port(), ef, sketch_comm, 3), nprocs=2, join=True)
+    from parity import rendezvous
+    mp.spawn(_worker_multi, args=(2, rendezvous(), ef, sketch_comm, 3), nprocs=2, join=True)
 
 
 class _DdpNet(torch.nn.Module):
@@ -309,7 +309,7 @@ def _ddp_two_ranks_worker(rank, ws, port, ef):
     sys.path.insert(0, REPO)
     sys.path.insert(0, HERE)
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=ws)
     from torch.nn.parallel import DistributedDataParallel as DDP
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
     from oracle import arctopk as A
@@ -329,8 +329,8 @@ def test_hook_inside_ddp_two_ranks(ef):
     """Two DDP ranks on cuda:0 (gloo): the exchange step with its exchange-stream decode
     and device-aware Future through the Reducer's finalize, every parameter gradient vs the
     two-rank oracle."""
-    from parity import free_port
-    mp.spawn(_ddp_two_ranks_worker, args=(2, free_port(), ef), nprocs=2, join=True)
+    from parity import rendezvous
+    mp.spawn(_ddp_two_ranks_worker, args=(2, rendezvous(), ef), nprocs=2, join=True)
 
 
 @pytest.mark.parametrize("ef,sketch_comm", [("ef14", "separate"), ("ef21", "separate"),
@@ -397,7 +397,7 @@ def _golden_ws2_worker(rank, ws, port, name):
     sys.path.insert(0, REPO)
     sys.path.insert(0, HERE)
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=ws)
     from allreducetopk_amd.bucket import SyntheticBucket
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
     from allreducetopk_amd.comm_hooks import sparse_hook, sparse_hook_c4
@@ -471,5 +471,5 @@ def _golden_ws2_worker(rank, ws, port, name):
 def test_reference_ws2_golden_through_hip_hook(name):
     """Every ws=2 fixture of the reference, RandK included (index_source="host": its CPU
     torch.randperm draws, sparse_hook_c4.py:20)."""
-    from parity import free_port
-    mp.spawn(_golden_ws2_worker, args=(2, free_port(), name), nprocs=2, join=True)
+    from parity import rendezvous
+    mp.spawn(_golden_ws2_worker, args=(2, rendezvous(), name), nprocs=2, join=True)
