@@ -458,7 +458,7 @@ class GroupTopKState(HookState):
         self.exchange_groups = os.environ.get("ARCTOPK_EXCHANGE_GROUPS", "auto")
         if self.exchange_groups not in ("auto", "all", "off"):
             raise ValueError("ARCTOPK_EXCHANGE_GROUPS must be 'auto', 'all' or 'off'")
-        self.group_bytes = int(float(os.environ.get("ARCTOPK_GROUP_MIB", "64")) * (1 << 20))
+        self.group_bytes = int(float(os.environ.get("ARCTOPK_GROUP_MIB", "128")) * (1 << 20))
         # The plan of a bucket is found by its buffer's identity (no gradients() walk per
         # call).  DDP rebuilds its buckets once, after the first iteration, and the caching
         # allocator may hand a rebuilt bucket the same block: for the first
@@ -1064,7 +1064,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         # finish, so the select is not held back waiting for it)
         depth = 2 if comms else 1
         ars = None
-        if comms and (defer or grouped):
+        if comms:
             ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
             if pk.kind == "callback" and ars.cuda_stream not in pk._streams:
                 pk.known_stream(ars)
@@ -1112,7 +1112,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             st_ = L.arctopk_exchange_step(u.handle, u_x, u_e, u_g, ef, int(err_in), int(u_draw), seed,
                                           u_next.handle if u_next is not None else None, u_nseed,
                                           sk.handle if comms else None, pk.handle if comms else None, sid,
-                                          ars.cuda_stream if (ars is not None and u_defer) else None,
+                                          ars.cuda_stream if ars is not None else None,
                                           int(u_defer), ride[0].handle if ride is not None else None,
                                           ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
                                           u_vptr, marks)

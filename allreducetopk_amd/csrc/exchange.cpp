@@ -621,7 +621,11 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // with collectives the pack kernel completes x_ev_packed itself (no marker packet on the
     // caller's stream, where one idles the GPU several us): the all-reduce stream waits for it,
     // and the watchdog sees the sketch all-reduce before it complete
-    const bool async_ar = defer && packed_comm;
+    // the packed all-reduce goes on the all-reduce stream whenever the caller gave one: a
+    // deferred step's, and the backward's last step's too (its decode then waits for it on the
+    // caller's stream, while the earlier steps' decodes run beside it on the wire); inline only
+    // without that stream or with markers (the marker pass times the phases in stream order)
+    const bool async_ar = packed_comm && ar_stream && ar_stream != stream && (defer || !marks);
     if (packed_comm) {
         if ((e = ensure_event(&p->x_ev_packed, 0)) ||
             (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
@@ -647,7 +651,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // the backward's last step (no deferral): the last deferred decode it finishes shares one
     // launch with its own decode, after its own packed all-reduce (unless markers were asked for)
     arctopk_plan* pair = nullptr;
-    if (!defer && nfinish > 0 && finish[nfinish - 1] && finish[nfinish - 1] != p &&
+    if (!defer && !async_ar && nfinish > 0 && finish[nfinish - 1] && finish[nfinish - 1] != p &&
         finish[nfinish - 1]->x_deferred && !(finish_marks && finish_marks[nfinish - 1]) && !marks)
         pair = finish[nfinish - 1];
     // earlier buckets' deferred decodes the caller wants done now (in its order)
@@ -664,7 +668,11 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         p->x_ws = ws;
         return 0;
     }
-    if (packed_comm) e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
+    if (async_ar) {  // this step's own packed all-reduce, on the all-reduce stream
+        if ((e = (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0))) return e;
+    } else if (packed_comm) {
+        e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
+    }
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
     if (e) return e;
     if (pair) {

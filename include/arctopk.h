@@ -255,7 +255,10 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   later step's `ride` / `finish`); with communicators its packed all-reduce runs on
  *   `ar_stream` after the pack kernel, which completes the event that stream waits for (no
  *   marker packet on `stream`), so the caller's stream encodes the next bucket while these
- *   packed values are on the wire.  defer = 0: all-reduce and decode inline on `stream`.
+ *   packed values are on the wire.  defer = 0: the decode follows on `stream`; given an
+ *   `ar_stream` (and no markers), the packed all-reduce runs there too and `stream` waits for
+ *   it just before the decode, so the `finish` steps' decodes run beside it on the wire;
+ *   otherwise the all-reduce is inline on `stream`.
  * ride: an earlier step's deferred decode, run inside this step's select launch (extra blocks of
  *   the single-block select launch, or of the multi-block select's last, fused write launch: the
  *   select's latency then hides behind the decode's HBM stream), else right after the select;
