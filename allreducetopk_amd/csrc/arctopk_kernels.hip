@@ -90,12 +90,39 @@ __device__ __forceinline__ float4 ef_combine4(float4 x, float4 e) {
 //  ENC_TILE       : m < 64 (ND convs, m = 2*t^2): the tile's rows are loaded coalesced
 //                   into LDS, then one thread per row forms its R dot products.
 //  ENC_RAW        : 1-D tensors: the sketch is the (EF-applied) values themselves.
+// Order key: energies are >= +0 or NaN; as uint32 the non-negative floats are
+// ordered, and every NaN (either sign) maps above +inf, as torch.topk ranks NaN largest.
+__device__ __forceinline__ uint32_t energy_key(float e) {
+    uint32_t u = __float_as_uint(e);
+    if (e != e) u = 0x7FFFFFFFu;  // NaN largest (above +inf 0x7F800000; bit 31 stays clear)
+    return u & 0x7FFFFFFFu ? u : 0u;  // -0 cannot occur; keep +0 = 0
+}
+
+// The energy of a row from its R fp32 sketch sums in registers, exactly as row_energy forms it
+// from the stored sketch at world size 1: each sum rounded to T as it is stored, divided by 1
+// (exact), squared and summed in order (keys mode of the encode).
+template <typename T, int R>
+__device__ __forceinline__ float energy_regs(const float (&acc)[R]) {
+    const float a = rnd<T>(acc[0]);
+    float s = rnd<T>(__fmul_rn(a, a));
+#pragma unroll
+    for (int j = 1; j < R; ++j) {
+        const float b = rnd<T>(acc[j]);
+        s = __fadd_rn(s, rnd<T>(__fmul_rn(b, b)));
+    }
+    return rnd<T>(s);
+}
+
 template <typename T, int R, int EF, bool ERR_IN>
 __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, const EncTile t,
                                             const T* __restrict__ G, T* __restrict__ E,
                                             const T* __restrict__ V, T* __restrict__ sketch,
-                                            float* __restrict__ part_buf, float* __restrict__ lds) {
+                                            float* __restrict__ part_buf, uint32_t* __restrict__ keys,
+                                            float* __restrict__ lds) {
     const SegDev s = segs[t.seg];
+    // keys mode (world size 1, multi-block select items): the row's energy key instead of its
+    // sketch -- the key the select's key pass would form from the sketch (k_arc_keys)
+    uint32_t* const kout = (keys && s.keyed) ? keys + s.row_off : nullptr;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -199,6 +226,10 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
                 const float x = row[c];
 #pragma unroll
                 for (int j = 0; j < R; ++j) acc[j] = fmaf(x, vl[c * R + j], acc[j]);
+            }
+            if (kout) {
+                kout[t.row0 + rr] = energy_key(energy_regs<T, R>(acc));
+                continue;
             }
             T* out = sketch + s.sketch_off + (t.row0 + rr) * R;
             if constexpr (R == 4 && sizeof(T) == 4) {
@@ -312,7 +343,9 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
                 if (st_ == steps - 1) {
 #pragma unroll
                     for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
-                    if (lane < R) {
+                    if (kout) {
+                        if (lane == 0) kout[r_] = energy_key(energy_regs<T, R>(acc));
+                    } else if (lane < R) {
                         float v = acc[0];
 #pragma unroll
                         for (int j = 1; j < R; ++j)
@@ -437,7 +470,9 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
                 // makes the pick a dynamically indexed private array, i.e. a few bytes of
                 // scratch per row; the alternative, lane 0 storing all R, measured 10 us
                 // slower per headline encode, 148 vs 138 us.)
-                if (lane < R) {
+                if (kout) {
+                    if (lane == 0) kout[r_] = energy_key(energy_regs<T, R>(acc));
+                } else if (lane < R) {
                     float v = acc[0];
 #pragma unroll
                     for (int j = 1; j < R; ++j)
@@ -482,8 +517,12 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
             if (lane == 0) {
+                if (kout) {
+                    kout[row] = energy_key(energy_regs<T, R>(acc));
+                } else {
 #pragma unroll
-                for (int j = 0; j < R; ++j) put(row * R + j, acc[j]);
+                    for (int j = 0; j < R; ++j) put(row * R + j, acc[j]);
+                }
             }
         }
     }
@@ -496,9 +535,10 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                                                 const T* __restrict__ G, T* __restrict__ E,
                                                 const T* __restrict__ V,
                                                 T* __restrict__ sketch,
-                                                float* __restrict__ part_buf) {
+                                                float* __restrict__ part_buf,
+                                                uint32_t* __restrict__ keys) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    encode_tile<T, R, EF, ERR_IN>(segs, tiles[blockIdx.x], G, E, V, sketch, part_buf, lds);
+    encode_tile<T, R, EF, ERR_IN>(segs, tiles[blockIdx.x], G, E, V, sketch, part_buf, keys, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -547,14 +587,6 @@ __device__ __forceinline__ float row_energy(const T* __restrict__ p, int R, cons
         s = __fadd_rn(s, rnd<T>(__fmul_rn(b, b)));
     }
     return rnd<T>(s);
-}
-
-// Order key: energies are >= +0 or NaN; as uint32 the non-negative floats are
-// ordered, and every NaN (either sign) maps above +inf, as torch.topk ranks NaN largest.
-__device__ __forceinline__ uint32_t energy_key(float e) {
-    uint32_t u = __float_as_uint(e);
-    if (e != e) u = 0x7FFFFFFFu;  // NaN largest (above +inf 0x7F800000; bit 31 stays clear)
-    return u & 0x7FFFFFFFu ? u : 0u;  // -0 cannot occur; keep +0 = 0
 }
 
 template <typename T>
@@ -1784,7 +1816,7 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
                                                   const int32_t* __restrict__ ids, int first,
                                                   const T* __restrict__ sketch, int R, Scale sc,
                                                   uint32_t* __restrict__ keys, MWorkspace* ws,
-                                                  KeysGrid kg) {
+                                                  KeysGrid kg, int from_keys) {
     // one 16 KiB histogram (the compacted (bin, count) list is packed into it in place):
     // LDS sets the occupancy, and every block of the grid must be resident in one round
     __shared__ uint32_t h[kMBins];
@@ -1812,6 +1844,17 @@ __global__ void __launch_bounds__(KT) k_arc_keys(const SegDev* __restrict__ segs
         else if (dg == (uint32_t)kMBins - 1u) ++c_hi;
         else atomicAdd(&h[dg], 1u);
     };
+    if (from_keys && s.keyed) {  // the encode wrote the keys (keys mode): histogram only
+        constexpr int UK = 8;
+        for (; row < s.n; row += UK * gs) {
+            uint32_t kv[UK];
+#pragma unroll
+            for (int u = 0; u < UK; ++u) kv[u] = kout[min(row + u * gs, s.n - 1)];
+#pragma unroll
+            for (int u = 0; u < UK; ++u)
+                if (row + u * gs < s.n) count(kv[u]);
+        }
+    }
     if (stride == 4 && (s.sketch_off & 3) == 0) {  // r = 4: one quad load per row, UK rows in flight
         constexpr int UK = 8;
         for (; row < s.n; row += UK * gs) {
@@ -2816,7 +2859,7 @@ __global__ void __launch_bounds__(256) k_sketch_combine(const SegDev* __restrict
 // column-split tensors
 template <typename T, int R>
 int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
-                    hipStream_t st) {
+                    uint32_t* keys, hipStream_t st) {
     if (p->n_enc > 0) {
         const bool use_e = p->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
         const int nt = use_e ? p->n_enc_e : p->n_enc;
@@ -2825,13 +2868,13 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
         const EncTile* tiles = use_e ? p->d_enc_e : p->d_enc;
         float* pb = p->d_part;
         if (ef == ARCTOPK_EF_NONE)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
         else if (ef == ARCTOPK_EF14 && err_in)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
         else if (ef == ARCTOPK_EF14)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
         else
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
         const int e = (int)hipGetLastError();
         if (e) return e;
     }
@@ -2844,20 +2887,20 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
 
 template <typename T>
 int launch_encode(const arctopk_plan* p, const void* grad, void* err, int ef, int err_in, const void* V,
-                  void* sketch, hipStream_t st) {
+                  void* sketch, uint32_t* keys, hipStream_t st) {
     const T* G = static_cast<const T*>(grad);
     T* E = static_cast<T*>(err);
     const T* Vt = static_cast<const T*>(V);
     T* sk = static_cast<T*>(sketch);
     switch (p->r) {
-        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, st);
-        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, st);
-        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, st);
-        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, st);
-        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, st);
-        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, st);
-        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, st);
-        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, st);
+        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, keys, st);
     }
     return ARCTOPK_EINVAL;
 }
@@ -2926,7 +2969,8 @@ int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int nsm, const 
 // ride: a deferred decode that may run in the last select launch (*rode = true if it did)
 template <typename T>
 int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_t* rowlist, int32_t* slotmap,
-                  VDrawJob job, bool* drawn, hipStream_t st, const RideArgs* ride = nullptr, bool* rode = nullptr) {
+                  VDrawJob job, bool* drawn, hipStream_t st, const RideArgs* ride = nullptr, bool* rode = nullptr,
+                  bool keyed = false) {
     *drawn = false;
     if (rode) *rode = false;
     const T* sketch = static_cast<const T*>(sketch_);
@@ -2978,10 +3022,12 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
                 1, std::min<int64_t>(kMHistBlocks, (b.it[i].n + rpb - 1) / rpb));
         if (keys_threads == 256)
             hipLaunchKernelGGL((k_arc_keys<T, 256>), dim3(kg.first[b.cnt]), dim3(256), 0, st, p->d_segs,
-                               p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg);
+                               p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg,
+                               keyed ? 1 : 0);
         else
             hipLaunchKernelGGL((k_arc_keys<T, 1024>), dim3(kg.first[b.cnt]), dim3(1024), 0, st, p->d_segs,
-                               p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg);
+                               p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg,
+                               keyed ? 1 : 0);
         int e = ms_arc_compact(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, st);
         if (e) return e;
         const int nsm = bi == 0 ? p->n_small : 0;
@@ -3157,9 +3203,27 @@ extern "C" int arctopk_encode(const arctopk_plan* p, const void* grad, void* err
     if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
     if (p->info.v_len > 0 && !V) return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    if (p->dtype == ARCTOPK_BF16) return launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, st);
-    return launch_encode<float>(p, grad, err, ef, err_in, V, sketch, st);
+    if (p->dtype == ARCTOPK_BF16) return launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, nullptr, st);
+    return launch_encode<float>(p, grad, err, ef, err_in, V, sketch, nullptr, st);
 }
+
+namespace arctopk {
+// arctopk_encode at world size 1 for this plan's own select (keys mode): multi-block select
+// items get their energy keys written into the plan's key buffer instead of their sketch rows
+// (the sketch all-reduce is the identity, so the keys are the select's; its key pass then only
+// builds the histograms).  Every other segment's sketch is written as arctopk_encode writes it.
+int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef, int32_t err_in, const void* V,
+                 void* sketch, void* stream) {
+    if (!p || !grad || !sketch) return ARCTOPK_EINVAL;
+    if (ef != ARCTOPK_EF_NONE && !err) return ARCTOPK_EINVAL;
+    if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
+    if (p->info.v_len > 0 && !V) return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t* keys = p->any_keyed ? p->d_keys : nullptr;
+    if (p->dtype == ARCTOPK_BF16) return launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, keys, st);
+    return launch_encode<float>(p, grad, err, ef, err_in, V, sketch, keys, st);
+}
+}  // namespace arctopk
 
 extern "C" int arctopk_row_energy(const arctopk_plan* p, const void* sketch, int32_t ws,
                                   float* energy, void* stream) {
@@ -3169,10 +3233,23 @@ extern "C" int arctopk_row_energy(const arctopk_plan* p, const void* sketch, int
     return launch_energy<float>(p, sketch, ws, nullptr, energy, st);
 }
 
+namespace arctopk {
+// arctopk_select_draw; keyed: the encode of this call ran in keys mode (arctopk::encode_keyed),
+// so the multi-block items' keys are in place (world size 1 only)
+int select_draw_keyed(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
+                      const arctopk_plan* next, uint64_t next_seed, void* next_V, bool keyed, void* stream);
+}  // namespace arctopk
+
 extern "C" int arctopk_select_draw(const arctopk_plan* p, const void* sketch, int32_t ws,
                                    int32_t* rowlist, int32_t* slotmap, const arctopk_plan* next,
                                    uint64_t next_seed, void* next_V, void* stream) {
-    if (!p || !sketch || !rowlist || !slotmap || ws < 1) return ARCTOPK_EINVAL;
+    return arctopk::select_draw_keyed(p, sketch, ws, rowlist, slotmap, next, next_seed, next_V, false, stream);
+}
+
+int arctopk::select_draw_keyed(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist,
+                               int32_t* slotmap, const arctopk_plan* next, uint64_t next_seed, void* next_V,
+                               bool keyed, void* stream) {
+    if (!p || !sketch || !rowlist || !slotmap || ws < 1 || (keyed && ws != 1)) return ARCTOPK_EINVAL;
     if (next && (!next_V || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     VDrawJob job{};
@@ -3185,8 +3262,8 @@ extern "C" int arctopk_select_draw(const arctopk_plan* p, const void* sketch, in
     }
     bool drawn = false;
     const int e = p->dtype == ARCTOPK_BF16
-                      ? launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, job, &drawn, st)
-                      : launch_select<float>(p, sketch, ws, rowlist, slotmap, job, &drawn, st);
+                      ? launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, nullptr, nullptr, keyed)
+                      : launch_select<float>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, nullptr, nullptr, keyed);
     if (e) return e;
     if (job.n && !drawn) return arctopk_draw_projections(next, next_seed, next_V, stream);
     return 0;
@@ -3242,8 +3319,9 @@ namespace arctopk {
 // caller decodes rp itself).
 int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
                 const arctopk_plan* next, uint64_t next_seed, void* next_V, const arctopk_plan* rp,
-                int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream) {
+                int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream, bool keyed) {
     *rode = 0;
+    if (keyed && ws != 1) return ARCTOPK_EINVAL;
     constexpr int64_t big_rows = ARCTOPK_SEL_BIG_ROWS;
     const bool rideable = rp && rp->dtype == p->dtype && rp->device == p->device && rp->n_dec > 0 &&
                           rp->b_packed && rp->b_slotmap && rp_out && (rp_ef != ARCTOPK_EF21 || rp_gerr) &&
@@ -3265,14 +3343,14 @@ int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* 
         bool drawn = false, took = false;
         hipStream_t st = (hipStream_t)stream;
         const int e = p->dtype == ARCTOPK_BF16
-                          ? launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, &ra, &took)
-                          : launch_select<float>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, &ra, &took);
+                          ? launch_select<bf16_t>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, &ra, &took, keyed)
+                          : launch_select<float>(p, sketch, ws, rowlist, slotmap, job, &drawn, st, &ra, &took, keyed);
         if (e) return e;
         *rode = took ? 1 : 0;
         if (job.n && !drawn) return arctopk_draw_projections(next, next_seed, next_V, stream);
         return 0;
     }
-    if (!fusable) return arctopk_select_draw(p, sketch, ws, rowlist, slotmap, next, next_seed, next_V, stream);
+    if (!fusable) return select_draw_keyed(p, sketch, ws, rowlist, slotmap, next, next_seed, next_V, keyed, stream);
     if (!p || !sketch || !rowlist || !slotmap || ws < 1 || rp_ws < 1) return ARCTOPK_EINVAL;
     if (next && (!next_V || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
     VDrawJob job{};
@@ -3529,11 +3607,11 @@ extern "C" int arctopk_step(const arctopk_plan* p, void* bucket, void* err, void
     int e = step_mark(marks, ARCTOPK_MARK_START, st);
     if (!e && draw && p->info.v_len > 0) e = arctopk_draw_projections(p, seed, p->b_V, stream);
     if (!e) e = step_mark(marks, ARCTOPK_MARK_DRAW, st);
-    if (!e) e = arctopk_encode(p, bucket, err, ef, err_in, p->b_V, p->b_sketch, st);
+    if (!e) e = arctopk::encode_keyed(p, bucket, err, ef, err_in, p->b_V, p->b_sketch, st);
     if (!e) e = step_mark(marks, ARCTOPK_MARK_ENCODE, st);
     if (!e)
-        e = arctopk_select_draw(p, p->b_sketch, 1, p->b_rowlist, p->b_slotmap, next, next_seed,
-                                next ? next->b_V : nullptr, st);
+        e = arctopk::select_draw_keyed(p, p->b_sketch, 1, p->b_rowlist, p->b_slotmap, next, next_seed,
+                                       next ? next->b_V : nullptr, true, st);
     if (!e) e = step_mark(marks, ARCTOPK_MARK_SELECT, st);
     if (!e) e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, st);
     if (!e) e = step_mark(marks, ARCTOPK_MARK_PACK, st);

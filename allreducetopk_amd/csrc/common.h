@@ -60,9 +60,6 @@
 #define ARCTOPK_ENC_MIN_TILE 2048      // fewest elements per wave-per-row encode tile
                                        // (A/B: ResNet-18 DDP buckets 292 -> 304 GB/s vs 8192)
 #endif
-#ifndef ARCTOPK_ENC_ROWS_MULT
-#define ARCTOPK_ENC_ROWS_MULT 1        // rows per wave-per-row encode tile rounded up to a multiple
-#endif
 #ifndef ARCTOPK_ENC_UNITS_G_ONLY
 #define ARCTOPK_ENC_UNITS_G_ONLY 4     // fp32 encode without E loads: 16-B units per lane per step
 #endif
@@ -126,6 +123,8 @@ struct SegDev {
     int64_t part_off;  // nparts > 1: partial sketches at part_buf[part_off + (p * n + row) * r]
     int32_t dchunk0;      // decode mode 3 (short rows): global index of the segment's first decode
     int32_t dchunk_rows;  // chunk, and rows per chunk (0: the segment has no mode-3 chunks)
+    int32_t keyed;        // multi-block select item whose encode can emit its energy keys directly
+    int32_t pad_k;        // (at world size 1: the sketch all-reduce is the identity)
 };
 
 __device__ __forceinline__ uint32_t div32(uint32_t x, uint32_t magic) { return __umulhi(x, magic); }
@@ -375,6 +374,7 @@ struct arctopk_plan {
     int32_t* d_m3;                // segments with mode-3 decode chunks, and their number
     int n_m3;
     uint32_t* d_keys;             // select workspace: one key per row
+    int any_keyed;                // some segment is `keyed` (SegDev)
     int32_t* d_small;             // segments selected by the fused one-block kernel
     int n_small;
     int small_lds;                // bytes of LDS keys for the largest small segment
@@ -406,9 +406,15 @@ struct arctopk_plan {
     void* x_ev_dec;                     // completed by an inline decode after a collective
 };
 namespace arctopk {
+// keyed: the call's encode ran in keys mode (encode_keyed; world size 1 only)
 int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
                 const arctopk_plan* next, uint64_t next_seed, void* next_V, const arctopk_plan* rp,
-                int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream);
+                int32_t rp_ws, int32_t rp_ef, void* rp_gerr, void* rp_out, int* rode, void* stream,
+                bool keyed = false);
+int select_draw_keyed(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
+                      const arctopk_plan* next, uint64_t next_seed, void* next_V, bool keyed, void* stream);
+int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef, int32_t err_in, const void* V,
+                 void* sketch, void* stream);
 int decode_pair(const arctopk_plan* pa, int32_t ws_a, int32_t ef_a, void* gerr_a, void* out_a,
                 const arctopk_plan* pb, int32_t ws_b, int32_t ef_b, void* gerr_b, void* out_b, void* stream,
                 void* done);

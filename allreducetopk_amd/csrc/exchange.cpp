@@ -585,7 +585,11 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (!e && draw && p->info.v_len > 0) e = arctopk_draw_projections(p, seed, const_cast<void*>(V), stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_DRAW, st);
     ht.lap(0);
-    if (!e) e = arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
+    // world size 1 (no communicators): the sketch is not all-reduced, so the multi-block select
+    // items' encode writes their energy keys directly (keys mode)
+    const bool keyed = !sketch_comm;
+    if (!e) e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream)
+                      : arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_ENCODE, st);
     ht.lap(1);
     // one all-reduce for every tensor's sketch (the reference: one per tensor, :33, :58, :88)
@@ -600,7 +604,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         if ((e = wait_ar(ride, st)) || (e = mark(ride_marks, ARCTOPK_MARK_PACKED_AR, st))) return e;
         e = arctopk::select_ride(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
                                  next ? next->b_V : nullptr, ride, ride->x_ws, ride->x_ef, ride->x_gerr,
-                                 ride->x_bucket, &rode, stream);
+                                 ride->x_bucket, &rode, stream, keyed);
         if (!e && rode) {
             ride->x_deferred = 0;
             e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
@@ -612,8 +616,8 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
             if (!e) e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
         }
     } else {
-        e = arctopk_select_draw(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
-                                next ? next->b_V : nullptr, stream);
+        e = arctopk::select_draw_keyed(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
+                                       next ? next->b_V : nullptr, keyed, stream);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_SELECT, st);
     if (e) return e;

@@ -3,6 +3,7 @@
 // Built once per bucket layout; nothing here runs per call.
 #include <algorithm>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <numeric>
@@ -122,6 +123,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     // (small buckets: tiles down to ARCTOPK_ENC_MIN_TILE elements -- at least one row per wave --
     // so a bucket of a few rows spreads them over waves instead of walking them in sequence)
     const int64_t tile_elems = std::min<int64_t>(65536, std::max<int64_t>(ARCTOPK_ENC_MIN_TILE, row_work / target));
+    static_assert(ARCTOPK_ENC_MIN_TILE <= 65536, "encode tiles hold at most 64 Ki elements");
     // a second table for the fp32 kernels that also stream E (EF14 after the first call, EF21):
     // tensors of at least ARCTOPK_ENC_E_MIN_ROWS rows (embeddings) get tiles sized for twice the
     // block target (A/B: Llama-1B embedding bucket 1,072 -> 1,137 GB/s, RoBERTa 994 -> 1,008;
@@ -186,18 +188,21 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 split_ids.push_back((int32_t)i);
                 split_rows_max = std::max<int64_t>(split_rows_max, s.n);
             }
-            // rows per tile: a multiple of ARCTOPK_ENC_ROWS_MULT (4: every wave of the block the
-            // same number of rows)
-            constexpr int64_t rm = ARCTOPK_ENC_ROWS_MULT;
             for (int tab = 0; tab < 2; ++tab)
             for (int part = 0; part < nparts; ++part) {
                 const bool big = s.n >= (int64_t)ARCTOPK_ENC_E_MIN_ROWS;
                 any_e = any_e || (tab && big);
                 const int64_t te = tab && big ? tile_elems_e : tile_elems;
-                const int64_t per = std::max<int64_t>(4, (te / std::min<int64_t>(clen, s.m) + rm - 1) / rm * rm);
-                const int64_t ntiles = (s.n + per - 1) / per;
                 const int64_t c0 = part * clen;
                 const int64_t cl = std::min<int64_t>(clen, s.m - c0);
+                // tiles: this part's share of the block target, rounded to nearest (a bucket of
+                // equal tensors gets exactly the target: a whole number of resident rounds, no
+                // partial last round), within [te / 64 Ki-element, one per 4 rows]
+                const double work = (double)s.n * (double)cl;
+                int64_t ntiles = std::llround(work / (double)te);
+                ntiles = std::max<int64_t>(ntiles, (int64_t)std::ceil(work / 65536.0));
+                ntiles = std::min<int64_t>(ntiles, std::max<int64_t>(1, s.n / 4));
+                ntiles = std::max<int64_t>(ntiles, 1);
                 std::vector<EncTile>& dst = tab ? enc_e : enc;
                 // tile ti holds rows ti, ti + ntiles, ...: consecutive blocks read adjacent rows
                 for (int64_t ti = 0; ti < ntiles; ++ti)
@@ -206,6 +211,10 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
                 lds = std::max<int>(lds, (int)(cl * r * 4));
             }
         }
+        // keys mode (world size 1): a multi-block select item's encode writes the energy keys its
+        // key pass would form from the sketch (unsplit 2-D / ND tensors)
+        g.keyed = (s.n > small_cap && s.kind == ARCTOPK_SEG_SKETCH && g.nparts == 1) ? 1 : 0;
+        g.pad_k = 0;
         // ---- pack chunks: selected rows, ~kChunkElems elements each (small m: at most
         //      kSmallTileRows rows, the size of the kernels' LDS row/slot table)
         pack_begin.push_back((int32_t)pack.size());
@@ -282,6 +291,7 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     p->enc_lds_bytes = lds;
     p->dec_lds_bytes = (int)dec_lds;
     p->n_small = (int)small_ids.size();
+    for (const SegDev& g : dsegs) p->any_keyed = p->any_keyed || g.keyed;
     p->n_large = (int)large_ids.size();
     p->small_lds = (int)(((small_rows + 3) & ~3) * 4 + 16);
 #define ALLOC_COPY(dst, vec)                                                                  \
