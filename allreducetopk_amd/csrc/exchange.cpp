@@ -44,6 +44,7 @@ struct Rccl {
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*comm_init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_finalize)(ncclComm_t) = nullptr;
     ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
     ncclResult_t (*get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
@@ -75,6 +76,7 @@ int rccl_load(const char* path, const Rccl** out) {
     r.comm_init_rank_config =
         reinterpret_cast<decltype(r.comm_init_rank_config)>(dlsym(h, "ncclCommInitRankConfig"));
     r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.comm_finalize = reinterpret_cast<decltype(r.comm_finalize)>(dlsym(h, "ncclCommFinalize"));
     r.comm_abort = reinterpret_cast<decltype(r.comm_abort)>(dlsym(h, "ncclCommAbort"));
     r.get_async_error = reinterpret_cast<decltype(r.get_async_error)>(dlsym(h, "ncclCommGetAsyncError"));
     r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
@@ -419,9 +421,36 @@ extern "C" int arctopk_comm_destroy(arctopk_comm* c) {
         if (c->timeout_ms > 0) Watchdog::get().remove(c);
         std::lock_guard<std::mutex> lc(c->mu);
         if (c->nccl) {
-            const ncclResult_t r = c->rccl->comm_destroy(c->nccl);
-            e = (r == ncclInProgress) ? 0 : rccl_status(r);
-            c->nccl = nullptr;
+            const Rccl* R = c->rccl;
+            // a non-blocking communicator is finalized first and polled until its pending
+            // operations have flushed (bounded by its timeout: past it, abort), then destroyed
+            if (c->nonblocking && R->comm_finalize) {
+                ncclResult_t st = R->comm_finalize(c->nccl);
+                const int64_t t_end = now_ms() + (c->timeout_ms > 0 ? c->timeout_ms : 60000);
+                while (st == ncclInProgress || st == ncclSuccess) {
+                    ncclResult_t a = ncclSuccess;
+                    if (R->get_async_error(c->nccl, &a) != ncclSuccess) a = ncclInternalError;
+                    if (a != ncclInProgress) {
+                        st = a;
+                        break;
+                    }
+                    if (now_ms() > t_end) {
+                        st = ncclInProgress;
+                        break;
+                    }
+                    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                }
+                if (st != ncclSuccess) {
+                    (void)R->comm_abort(c->nccl);
+                    c->nccl = nullptr;
+                    e = st == ncclInProgress ? ARCTOPK_ETIMEOUT : rccl_status(st);
+                }
+            }
+            if (c->nccl) {
+                const ncclResult_t r = R->comm_destroy(c->nccl);
+                e = (r == ncclInProgress) ? 0 : rccl_status(r);
+                c->nccl = nullptr;
+            }
         }
     }
     if (c->wire_ev) (void)hipEventDestroy(c->wire_ev);

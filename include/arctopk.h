@@ -241,6 +241,10 @@ int arctopk_comm_init_callback(arctopk_allreduce_fn fn, void* ctx, int32_t nrank
  */
 int arctopk_comm_init_wire(int32_t emul_ranks, double busbw_gbs, double latency_us, int32_t blocks,
                            int32_t device, arctopk_comm** out);
+/* Destroy a communicator.  An RCCL communicator created non-blocking is finalized first
+ * (ncclCommFinalize, polled until its pending operations have flushed, at most its timeout;
+ * past it, or on an error, it is aborted and ARCTOPK_ETIMEOUT / the RCCL error is returned),
+ * then destroyed. */
 int arctopk_comm_destroy(arctopk_comm* comm);
 int arctopk_comm_size(const arctopk_comm* comm);
 /* in-place SUM all-reduce of `count` elements (ARCTOPK_F32 / ARCTOPK_BF16), stream-ordered */
