@@ -41,22 +41,35 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s meas
 PHASES = ["encode", "sketch_allreduce", "select", "pack", "packed_allreduce", "decode"]
 
 
-def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4):
+# the plan's select rules (csrc/common.h): single-block selects up to 15,360 rows, or 4,096 beside
+# multi-block items; V^T slices of at most 64 KiB per encode part
+SMALL_SEL_ROWS, SMALL_SEL_ROWS_MIXED, V_LDS_MAX_BYTES = 15360, 4096, 64 * 1024
+
+
+def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4, keyed: bool = False):
     """Minimum HBM bytes per call, per phase (element size eb, fused design).
 
     1-D tensors are their own sketch (written by encode, read by select); 2-D/ND
-    tensors add an [n, r] sketch and read an [m, r] projection.
+    tensors add an [n, r] sketch and read an [m, r] projection.  keyed (world size 1, the step
+    path): the multi-block select items' encode writes a 4-B energy key per row instead of
+    their sketch rows, and the select reads those keys (keys mode).
     """
     from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import _geometry
     n_el = bucket_numel(shapes)
+    geo = [(_geometry(s_), len(s_)) for s_ in shapes]
+    any_large = any(n > SMALL_SEL_ROWS for (_, n, _), _nd in geo)
+    small_cap = SMALL_SEL_ROWS_MIXED if any_large else SMALL_SEL_ROWS
     k_el = sk = vbytes = rows = k_rows = 0
-    for s_ in shapes:
-        kind, n, m = _geometry(s_)
+    for (kind, n, m), nd in geo:
         k_el += max(1, int(n * ratio)) * m
         rows += n
         k_rows += max(1, int(n * ratio))
-        sk += eb * n * (1 if m == 1 and len(s_) == 1 else r)
-        vbytes += 0 if len(s_) == 1 else m * r * eb
+        va = 8 if eb == 2 else 4  # (the plan's column-part rule: unsplit rows only)
+        if keyed and nd > 1 and n > small_cap and m <= V_LDS_MAX_BYTES // (4 * r) // va * va:
+            sk += 4 * n  # the row's energy key instead of its sketch
+        else:
+            sk += eb * n * (1 if m == 1 and nd == 1 else r)
+        vbytes += 0 if nd == 1 else m * r * eb
     if ef == "noef":
         enc = eb * n_el + sk + vbytes
         pack = 2 * eb * k_el
@@ -486,7 +499,8 @@ def main():
         hook_path = "exchange" if (world > 1 or args.force_exchange) else "step"
     value = world * args.steps * bytes_per_step / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
-    per_bucket = [algorithmic_bytes(args.ef, sh, args.ratio, args.r, eb) for sh in layouts]
+    per_bucket = [algorithmic_bytes(args.ef, sh, args.ratio, args.r, eb, keyed=(hook_path == "step"))
+                  for sh in layouts]
     alg = {k: sum(d[k] for d in per_bucket) / nb for k in per_bucket[0]}  # mean over the step's buckets
     roof = None
     if light:

@@ -122,6 +122,34 @@ __global__ void __launch_bounds__(256) k_rows_sweep(const float4* __restrict__ a
     }
 }
 
+// the same sweep with each wave's U loads of a step spread over the row (unit u of lane l at
+// quad u * MU / U + st * 64 + l: 1 KiB pieces 2 KiB apart) instead of one contiguous 4 KiB
+// piece -- the flat kernel's per-wave pattern (its waves' pieces are 4 KiB apart)
+template <int U>
+__global__ void __launch_bounds__(256) k_rows_sweep_il(const float4* __restrict__ a, float4* __restrict__ b,
+                                                      int total_rows) {
+    constexpr int MU = 512;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int W = gridDim.x * 4;
+    for (int r = blockIdx.x * 4 + wave; r < total_rows; r += W) {
+        const size_t row = (size_t)r * MU;
+        for (int st = 0; st < MU / (64 * U); ++st) {
+            float4 x[U], y[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t j = row + u * (MU / U) + st * 64 + lane;
+                x[u] = ld_nt(a + j);
+                y[u] = ld_nt(b + j);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t j = row + u * (MU / U) + st * 64 + lane;
+                st_nt(b + j, make_float4(x[u].x + y[u].x, x[u].y + y[u].y, x[u].z + y[u].z, x[u].w + y[u].w));
+            }
+        }
+    }
+}
+
 template <typename F>
 float time_it(F f, int reps) {
     hipEvent_t e0, e1;
@@ -175,6 +203,11 @@ int main(int argc, char** argv) {
                                        (float4*)B[pick(i)], 16 * 2048); }, reps);
                 std::printf("%s rows in sweep order, %5d blocks: in-place add (nt) %5.0f GB/s  %6.1f us\n",
                             cold ? "cold" : "warm", g, 3 * bytes / tw / 1e6, tw * 1e3);
+                const float ti = time_it([&](int i) {
+                    hipLaunchKernelGGL(k_rows_sweep_il<4>, dim3(g), dim3(256), 0, 0, (const float4*)A[pick(i)],
+                                       (float4*)B[pick(i)], 16 * 2048); }, reps);
+                std::printf("%s rows in sweep order, spread units, %5d blocks: in-place add (nt) %5.0f GB/s  %6.1f us\n",
+                            cold ? "cold" : "warm", g, 3 * bytes / ti / 1e6, ti * 1e3);
             }
             for (int ntiles : {64, 80, 128, 160, 256, 512}) {
                 const float tw = time_it([&](int i) {

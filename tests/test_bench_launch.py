@@ -63,3 +63,21 @@ def test_sparse_algorithmic_bytes_follow_the_survey_formula():
 
 def test_pmc_traffic_is_never_the_n1_file_at_n_gt_1():
     assert bench.pmc_traffic("headline", "ef14", "k_encode", 2) == (None, None, None)
+
+
+def test_keys_mode_algorithmic_bytes():
+    """At world size 1 the multi-block items' encode writes 4-B keys instead of their sketch rows
+    (keys mode): the encode and select bytes drop by (4 r - 4) B per such row, nothing else."""
+    import bench
+    conv = [[512, 512, 3, 3]] * 2  # ND: m = 18, n = 131,072 rows each (multi-block items)
+    a, b = bench.algorithmic_bytes("ef14", conv, 0.2, 4), bench.algorithmic_bytes("ef14", conv, 0.2, 4, keyed=True)
+    rows = 2 * 131072
+    assert a["encode"] - b["encode"] == (16 - 4) * rows
+    assert a["select"] - b["select"] == (16 - 4) * rows
+    assert a["pack"] == b["pack"] and a["decode"] == b["decode"]
+    head = [[2048, 2048]] * 16  # single-block items: keys mode does not apply
+    assert bench.algorithmic_bytes("ef14", head, 0.2, 4) == bench.algorithmic_bytes("ef14", head, 0.2, 4, keyed=True)
+    # a tensor beside a multi-block item joins the multi-block batch past 4,096 rows
+    mixed = [[20000, 8], [5000, 8], [100, 8]]
+    c, d = bench.algorithmic_bytes("noef", mixed, 0.2, 4), bench.algorithmic_bytes("noef", mixed, 0.2, 4, keyed=True)
+    assert c["encode"] - d["encode"] == 12 * (20000 + 5000)
