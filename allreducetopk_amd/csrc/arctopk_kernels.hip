@@ -113,7 +113,7 @@ __device__ __forceinline__ float energy_regs(const float (&acc)[R]) {
     return rnd<T>(s);
 }
 
-template <typename T, int R, int EF, bool ERR_IN>
+template <typename T, int R, int EF, bool ERR_IN, bool ROWS = true>
 __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, const EncTile t,
                                             const T* __restrict__ G, T* __restrict__ E,
                                             const T* __restrict__ V, T* __restrict__ sketch,
@@ -243,6 +243,8 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
         }
         return;
     }
+    if constexpr (!ROWS) return;  // k_encode_short: a table without wave-per-row tiles
+    else {
 
     // wave-per-row modes over the tile's columns [c0, c0 + cl): stage that slice of V^T
     // ([R][cl]) in LDS (conflict-free writes: consecutive lanes take consecutive columns
@@ -526,9 +528,34 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
             }
         }
     }
+    }  // ROWS
 }
 
-// One tile per block.
+// The previous bucket's pack riding in this bucket's encode launch (world size 1: nothing waits
+// for the packed values before the next call's select, whose launch carries their decode): its
+// chunks are the launch's FIRST blocks, so the gathers run beside the encode's stream instead of
+// after it.  Same dtype and EF mode as the encode; the buffers are the previous call's.
+template <typename T>
+struct PackRide {
+    const SegDev* segs;
+    const Chunk* chunks;
+    const T* G;
+    T* E;
+    const int32_t* rowlist;
+    const int32_t* slotmap;
+    T* packed;
+    int32_t* dfirst;
+    int32_t n;  // chunks (blocks); 0: none
+};
+template <typename T, int EF>
+__device__ __forceinline__ void pack_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                           const T* __restrict__ G, T* __restrict__ E,
+                                           const int32_t* __restrict__ rowlist,
+                                           const int32_t* __restrict__ slotmap,
+                                           T* __restrict__ packed, int32_t* __restrict__ dfirst,
+                                           int32_t* __restrict__ rs);
+
+// One tile per block (after the riding pack's chunks).
 template <typename T, int R, int EF, bool ERR_IN>
 __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                                                 const EncTile* __restrict__ tiles, int ntiles,
@@ -536,9 +563,33 @@ __global__ void __launch_bounds__(256) k_encode(const SegDev* __restrict__ segs,
                                                 const T* __restrict__ V,
                                                 T* __restrict__ sketch,
                                                 float* __restrict__ part_buf,
-                                                uint32_t* __restrict__ keys) {
+                                                uint32_t* __restrict__ keys, PackRide<T> pr) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    encode_tile<T, R, EF, ERR_IN>(segs, tiles[blockIdx.x], G, E, V, sketch, part_buf, keys, lds);
+    if ((int)blockIdx.x < pr.n) {
+        pack_chunk<T, EF>(pr.segs, pr.chunks[blockIdx.x], pr.G, pr.E, pr.rowlist, pr.slotmap, pr.packed,
+                          pr.dfirst, reinterpret_cast<int32_t*>(lds));
+        return;
+    }
+    encode_tile<T, R, EF, ERR_IN>(segs, tiles[blockIdx.x - pr.n], G, E, V, sketch, part_buf, keys, lds);
+}
+
+// The same for a tile table without wave-per-row tiles (only 1-D tensors and rows of m < 64:
+// conv stacks, BatchNorm vectors): the row paths compiled out, so the kernel needs far fewer
+// registers than k_encode and more of its short-lived blocks are resident at once.
+template <typename T, int R, int EF, bool ERR_IN>
+__global__ void __launch_bounds__(256) k_encode_short(const SegDev* __restrict__ segs,
+                                                      const EncTile* __restrict__ tiles, int ntiles,
+                                                      const T* __restrict__ G, T* __restrict__ E,
+                                                      const T* __restrict__ V, T* __restrict__ sketch,
+                                                      float* __restrict__ part_buf, uint32_t* __restrict__ keys,
+                                                      PackRide<T> pr) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if ((int)blockIdx.x < pr.n) {
+        pack_chunk<T, EF>(pr.segs, pr.chunks[blockIdx.x], pr.G, pr.E, pr.rowlist, pr.slotmap, pr.packed,
+                          pr.dfirst, reinterpret_cast<int32_t*>(lds));
+        return;
+    }
+    encode_tile<T, R, EF, ERR_IN, false>(segs, tiles[blockIdx.x - pr.n], G, E, V, sketch, part_buf, keys, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -2039,14 +2090,15 @@ __device__ __forceinline__ void pack_stream_small(const SegDev& s, const Chunk& 
     }
 }
 
+// One pack chunk (256 threads): k_pack's block, or a block of the next bucket's encode launch
+// that this bucket's pack rides in (world size 1, PackRide).  rs: LDS for kSmallTileRows rows.
 template <typename T, int EF>
-__global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
-                                              const Chunk* __restrict__ chunks,
-                                              const T* __restrict__ G, T* __restrict__ E,
-                                              const int32_t* __restrict__ rowlist,
-                                              const int32_t* __restrict__ slotmap,
-                                              T* __restrict__ packed, int32_t* __restrict__ dfirst) {
-    const Chunk ch = chunks[blockIdx.x];
+__device__ __forceinline__ void pack_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                           const T* __restrict__ G, T* __restrict__ E,
+                                           const int32_t* __restrict__ rowlist,
+                                           const int32_t* __restrict__ slotmap,
+                                           T* __restrict__ packed, int32_t* __restrict__ dfirst,
+                                           int32_t* __restrict__ rs) {
     const SegDev s = segs[ch.seg];
     const int m = (int)s.m;
     if constexpr (sizeof(T) == 4) {
@@ -2097,7 +2149,6 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
         return;
     }
     if (m >= 4 && m < 256) {  // small-m: row list staged in LDS, 32-bit mulhi division
-        __shared__ int32_t rs[kSmallTileRows];
         const int nr = (int)ch.nrows;
         const int32_t before = (threadIdx.x == 0 && ch.row0 > 0) ? rl[-1] : -1;  // the previous slot's row
         for (int r = threadIdx.x; r < nr; r += 256) rs[r] = rl[r];
@@ -2306,6 +2357,17 @@ __global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
             st1<T>(dst + e, v);
         }
     }
+}
+
+template <typename T, int EF>
+__global__ void __launch_bounds__(256) k_pack(const SegDev* __restrict__ segs,
+                                              const Chunk* __restrict__ chunks,
+                                              const T* __restrict__ G, T* __restrict__ E,
+                                              const int32_t* __restrict__ rowlist,
+                                              const int32_t* __restrict__ slotmap,
+                                              T* __restrict__ packed, int32_t* __restrict__ dfirst) {
+    __shared__ int32_t rs[kSmallTileRows];
+    pack_chunk<T, EF>(segs, chunks[blockIdx.x], G, E, rowlist, slotmap, packed, dfirst, rs);
 }
 
 // ---------------------------------------------------------------------------
@@ -2859,22 +2921,32 @@ __global__ void __launch_bounds__(256) k_sketch_combine(const SegDev* __restrict
 // column-split tensors
 template <typename T, int R>
 int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
-                    uint32_t* keys, hipStream_t st) {
-    if (p->n_enc > 0) {
+                    uint32_t* keys, hipStream_t st, PackRide<T> pr) {
+    if (p->n_enc > 0 || pr.n > 0) {
         const bool use_e = p->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
         const int nt = use_e ? p->n_enc_e : p->n_enc;
-        dim3 grid(nt), block(256);
-        const size_t lds = (size_t)p->enc_lds_bytes;
+        dim3 grid(nt + pr.n), block(256);
+        // (a riding pack chunk stages up to kSmallTileRows rows of its row list in the same LDS)
+        const size_t lds = std::max<size_t>((size_t)p->enc_lds_bytes, pr.n ? (size_t)kSmallTileRows * 4 : 0);
         const EncTile* tiles = use_e ? p->d_enc_e : p->d_enc;
         float* pb = p->d_part;
-        if (ef == ARCTOPK_EF_NONE)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
+        if (p->enc_short) {  // no wave-per-row tile: the lean kernel
+            if (ef == ARCTOPK_EF_NONE)
+                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+            else if (ef == ARCTOPK_EF14 && err_in)
+                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+            else if (ef == ARCTOPK_EF14)
+                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+            else
+                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+        } else if (ef == ARCTOPK_EF_NONE)
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         else if (ef == ARCTOPK_EF14 && err_in)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         else if (ef == ARCTOPK_EF14)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         else
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys);
+            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         const int e = (int)hipGetLastError();
         if (e) return e;
     }
@@ -2887,20 +2959,20 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
 
 template <typename T>
 int launch_encode(const arctopk_plan* p, const void* grad, void* err, int ef, int err_in, const void* V,
-                  void* sketch, uint32_t* keys, hipStream_t st) {
+                  void* sketch, uint32_t* keys, hipStream_t st, PackRide<T> pr = PackRide<T>{}) {
     const T* G = static_cast<const T*>(grad);
     T* E = static_cast<T*>(err);
     const T* Vt = static_cast<const T*>(V);
     T* sk = static_cast<T*>(sketch);
     switch (p->r) {
-        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, keys, st);
-        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, keys, st);
-        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, keys, st);
-        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, keys, st);
-        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, keys, st);
-        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, keys, st);
-        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, keys, st);
-        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, keys, st);
+        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
     }
     return ARCTOPK_EINVAL;
 }
@@ -3213,15 +3285,35 @@ namespace arctopk {
 // (the sketch all-reduce is the identity, so the keys are the select's; its key pass then only
 // builds the histograms).  Every other segment's sketch is written as arctopk_encode writes it.
 int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef, int32_t err_in, const void* V,
-                 void* sketch, void* stream) {
+                 void* sketch, void* stream, const arctopk_plan* rp, const void* rp_grad, void* rp_err, int* rode) {
+    if (rode) *rode = 0;
     if (!p || !grad || !sketch) return ARCTOPK_EINVAL;
     if (ef != ARCTOPK_EF_NONE && !err) return ARCTOPK_EINVAL;
     if (ef < 0 || ef > 2) return ARCTOPK_EINVAL;
     if (p->info.v_len > 0 && !V) return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     uint32_t* keys = p->any_keyed ? p->d_keys : nullptr;
-    if (p->dtype == ARCTOPK_BF16) return launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, keys, st);
-    return launch_encode<float>(p, grad, err, ef, err_in, V, sketch, keys, st);
+    // the ride: rp's pack (its bound row list, slot map and packed buffer; its bucket and residual)
+    // as the launch's first blocks -- same dtype, and buffers distinct from this call's
+    const bool take = rp && rode && rp->dtype == p->dtype && rp->device == p->device && rp->n_pack > 0 &&
+                      rp->b_rowlist && rp->b_slotmap && rp->b_packed && (ef == ARCTOPK_EF14 ? rp_err : rp_grad) &&
+                      (ef != ARCTOPK_EF21 || rp_err) && rp_grad != grad && (!rp_err || rp_err != err);
+    if (p->dtype == ARCTOPK_BF16) {
+        PackRide<bf16_t> pr{};
+        if (take)
+            pr = PackRide<bf16_t>{rp->d_segs, rp->d_pack, static_cast<const bf16_t*>(rp_grad), static_cast<bf16_t*>(rp_err),
+                                  rp->b_rowlist, rp->b_slotmap, static_cast<bf16_t*>(rp->b_packed), rp->d_dfirst, rp->n_pack};
+        const int e = launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, keys, st, pr);
+        if (!e && take) *rode = 1;
+        return e;
+    }
+    PackRide<float> pr{};
+    if (take)
+        pr = PackRide<float>{rp->d_segs, rp->d_pack, static_cast<const float*>(rp_grad), static_cast<float*>(rp_err),
+                             rp->b_rowlist, rp->b_slotmap, static_cast<float*>(rp->b_packed), rp->d_dfirst, rp->n_pack};
+    const int e = launch_encode<float>(p, grad, err, ef, err_in, V, sketch, keys, st, pr);
+    if (!e && take) *rode = 1;
+    return e;
 }
 }  // namespace arctopk
 

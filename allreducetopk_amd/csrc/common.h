@@ -7,6 +7,9 @@
 
 // Build-time tuning constants (build(defines=[...]) makes A/B variants; the product library
 // has no run-time tuning knobs and one code path per feature).  Selects:
+#ifndef ARCTOPK_ENC_SHORT_MAX_TILES
+#define ARCTOPK_ENC_SHORT_MAX_TILES 8192  // largest tile table of the lean short-row encode kernel
+#endif
 #ifndef ARCTOPK_SEL_BIG_ROWS
 #define ARCTOPK_SEL_BIG_ROWS 4096      // single-block select: 1024 threads above this many rows
 #endif
@@ -355,6 +358,7 @@ struct arctopk_plan {
     arctopk::EncTile* d_enc_e;    // encode tiles of the fp32 kernels that also stream E (0: use d_enc)
     int n_enc_e;
     int enc_lds_bytes;            // dynamic LDS of the encode launch
+    int enc_short;                // no wave-per-row tile in the tables: k_encode_short
     float* d_part;                // partial sketches of column-split segments
     int32_t* d_split;             // ids of column-split segments
     int n_split;
@@ -403,6 +407,9 @@ struct arctopk_plan {
     void* x_bucket;                     //   the bucket,
     void* x_gerr;                       //   the global residual (EF21),
     int x_ef, x_ws;                     //   the EF mode and world size of that call
+    int x_pack;                         // its pack is deferred too (world size 1): enqueued in the
+    void* x_err;                        //   next call's encode launch, or by exchange_finish; the
+                                        //   residual it gathers from
     void* x_ev_dec;                     // completed by an inline decode after a collective
 };
 namespace arctopk {
@@ -413,8 +420,11 @@ int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* 
                 bool keyed = false);
 int select_draw_keyed(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
                       const arctopk_plan* next, uint64_t next_seed, void* next_V, bool keyed, void* stream);
+// keyed encode; rp (may be null): a plan whose deferred pack (its bound buffers, bucket rp_grad
+// and residual rp_err, the same EF mode and dtype) rides in the launch: *rode = 1 when it did
 int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef, int32_t err_in, const void* V,
-                 void* sketch, void* stream);
+                 void* sketch, void* stream, const arctopk_plan* rp = nullptr, const void* rp_grad = nullptr,
+                 void* rp_err = nullptr, int* rode = nullptr);
 int decode_pair(const arctopk_plan* pa, int32_t ws_a, int32_t ef_a, void* gerr_a, void* out_a,
                 const arctopk_plan* pb, int32_t ws_b, int32_t ef_b, void* gerr_b, void* out_b, void* stream,
                 void* done);

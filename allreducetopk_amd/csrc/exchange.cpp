@@ -574,11 +574,22 @@ int wait_ar(arctopk_plan* p, hipStream_t st) {
 }
 }  // namespace
 
+namespace {
+// a deferred pack (world size 1) that no encode launch took: its own launch
+int pack_now(arctopk_plan* p, void* stream) {
+    if (!p->x_pack) return 0;
+    const int e = arctopk_pack(p, p->x_bucket, p->x_err, p->x_ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
+    if (!e) p->x_pack = 0;
+    return e;
+}
+}  // namespace
+
 extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* const* marks) {
     if (!p) return ARCTOPK_EINVAL;
     if (!p->x_deferred) return 0;
     hipStream_t st = (hipStream_t)stream;
-    int e = wait_ar(p, st);
+    int e = pack_now(p, stream);
+    if (!e) e = wait_ar(p, st);
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
     if (!e) e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, stream, nullptr);
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
@@ -609,6 +620,8 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (ht.on) g_ht_calls.fetch_add(1, std::memory_order_relaxed);
     // this bucket's own deferred decode, if a caller never finished it (the hook always does)
     int e = arctopk_exchange_finish(p, stream, nullptr);
+    // a step with markers times its own encode: the ride's deferred pack goes first, unmarked
+    if (!e && marks && ride) e = pack_now(ride, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_START, st);
     if (!V) V = p->b_V;
     if (!e && draw && p->info.v_len > 0) e = arctopk_draw_projections(p, seed, const_cast<void*>(V), stream);
@@ -617,8 +630,27 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // world size 1 (no communicators): the sketch is not all-reduced, so the multi-block select
     // items' encode writes their energy keys directly (keys mode)
     const bool keyed = !sketch_comm;
-    if (!e) e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream)
-                      : arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
+    // the ride's deferred pack (world size 1) runs as the first blocks of this encode launch when
+    // it can: same EF mode and dtype, other buffers (a bucket hooked twice in a row reads the
+    // residual the pack rewrites: then the pack goes first, in its own launch)
+    if (!e && ride && ride->x_pack) {
+        const bool fits = keyed && ride->x_ef == ef && ride->dtype == p->dtype && ride->x_bucket != bucket &&
+                          (!err || ride->x_err != err);
+        int prode = 0;
+        if (fits) {
+            e = arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream, ride, ride->x_bucket,
+                                      ride->x_err, &prode);
+            if (!e && prode) ride->x_pack = 0;
+            if (!e) e = pack_now(ride, stream);  // (not taken: nothing of this call's touches it)
+        } else {
+            e = pack_now(ride, stream);
+            if (!e) e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream)
+                              : arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
+        }
+    } else if (!e) {
+        e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream)
+                  : arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
+    }
     if (!e) e = mark(marks, ARCTOPK_MARK_ENCODE, st);
     ht.lap(1);
     // one all-reduce for every tensor's sketch (the reference: one per tensor, :33, :58, :88)
@@ -666,6 +698,11 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
                                  p->x_ev_packed);
         if (!e) Watchdog::get().watch(sketch_comm, p->x_ev_packed);
+    } else if (defer && !marks) {
+        // world size 1, deferred: nothing reads the packed values before the next call's select
+        // (the decode rides there), so the pack rides in the next call's encode launch
+        p->x_pack = 1;
+        p->x_err = err;
     } else {
         e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
     }
@@ -710,7 +747,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (e) return e;
     if (pair) {
         if (packed_comm && (e = ensure_event(&p->x_ev_dec, hipEventDisableTiming | hipEventReleaseToDevice))) return e;
-        if ((e = wait_ar(pair, st))) return e;
+        if ((e = pack_now(pair, stream)) || (e = wait_ar(pair, st))) return e;
         e = arctopk::decode_pair(pair, pair->x_ws, pair->x_ef, pair->x_gerr, pair->x_bucket, p, ws, ef, gerr, bucket,
                                  stream, packed_comm ? p->x_ev_dec : nullptr);
         if (!e) {

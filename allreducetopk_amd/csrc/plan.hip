@@ -289,6 +289,11 @@ extern "C" int arctopk_plan_create(const int64_t* dims, const int32_t* ndims, in
     std::copy(pack_begin.begin(), pack_begin.end(), p->h_pack_begin);
     std::copy(dec_begin.begin(), dec_begin.end(), p->h_dec_begin);
     p->enc_lds_bytes = lds;
+    // the lean encode kernel for tables of short rows (its blocks are latency-bound: more of them
+    // resident at once), up to a few rounds of blocks -- a large bucket streams faster at
+    // k_encode's occupancy (28 x [512, 512, 3, 3]: 14,336 tiles, 134 -> 139 us lean)
+    p->enc_short = (int)enc.size() <= ARCTOPK_ENC_SHORT_MAX_TILES;
+    for (const EncTile& et : enc) p->enc_short = p->enc_short && (et.mode == ENC_RAW || et.mode == ENC_TILE);
     p->dec_lds_bytes = (int)dec_lds;
     p->n_small = (int)small_ids.size();
     for (const SegDev& g : dsegs) p->any_keyed = p->any_keyed || g.keyed;

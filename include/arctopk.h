@@ -263,6 +263,11 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   `ar_stream` (and no markers), the packed all-reduce runs there too and `stream` waits for
  *   it just before the decode, so the `finish` steps' decodes run beside it on the wire;
  *   otherwise the all-reduce is inline on `stream`.
+ *   Without communicators (world size 1) and markers, defer = 1 defers the pack as well: nothing
+ *   reads the packed values before the decode, so they are packed by the first blocks of the next
+ *   step's encode launch (that step's `ride`; same EF mode and dtype, other bucket and residual
+ *   buffers) or by arctopk_exchange_finish.  Until then the plan's packed buffer and the residual's
+ *   selected rows are not yet final.
  * ride: an earlier step's deferred decode, run inside this step's select launch (extra blocks of
  *   the single-block select launch, or of the multi-block select's last, fused write launch: the
  *   select's latency then hides behind the decode's HBM stream), else right after the select;
@@ -280,7 +285,7 @@ int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* ger
                           void* const* const* finish_marks, int32_t nfinish, const void* V,
                           void* const* marks);
 /* The deferred decode of `plan`'s last deferred exchange step, on `stream` (no-op if none):
- * after that step's packed all-reduce. */
+ * after that step's packed all-reduce (and, at world size 1, its deferred pack). */
 int arctopk_exchange_finish(arctopk_plan* plan, void* stream, void* const* marks);
 
 /*
