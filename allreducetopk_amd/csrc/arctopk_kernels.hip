@@ -1810,8 +1810,116 @@ struct DecodeRide {
     T* gE;
     T* out;
     Scale sc;
-    int32_t n;  // chunks (blocks); 0: none
+    int32_t n;    // chunks (blocks); 0: none
+    int32_t fin;  // world size 1, pack and decode fused (finalize_chunk): 1 EF14, 2 noef; 0: decode
+    T* E;         // (fin) the residual the selected rows are taken from
 };
+
+// World size 1, pack + decode in one pass (no packed buffer): the all-reduce is the identity, so
+// the decoded bucket is the selected rows' values (x / 1, exact) and zero elsewhere.  EF14: out :=
+// E on selected rows, 0 elsewhere, and the selected rows of E := 0 (what k_pack then k_decode
+// leave); noef: out is the bucket itself (G, in place), whose unselected elements become 0.  One
+// decode chunk (its row range) per 256-thread block.
+template <typename T>
+__device__ __forceinline__ void finalize_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                               const int32_t* __restrict__ slotmap, T* __restrict__ E,
+                                               T* __restrict__ out, int fin, Scale sc) {
+    // the decode's own arithmetic on the selected values (x / 1, rounded to T: bit-identical to
+    // k_decode's output from the packed copy, NaNs included)
+    auto mean4 = [&](float4 v) { return rnd4<T>(sc(v)); };
+    auto mean1 = [&](float v) { return rnd<T>(sc(v)); };
+    const SegDev s = segs[ch.seg];
+    const int m = (int)s.m;
+    const int64_t base = s.offset + ch.row0 * m;
+    const int32_t* sm = slotmap + s.row_off + ch.row0;
+    const int nr = (int)ch.nrows;
+    const bool ef14 = fin == 1;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (s.vec && m >= 256) {  // wave per row, 16-B quads: a selected row is copied, the rest zeroed
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m4 = m >> 2;
+        constexpr int U = 4;
+        for (int j = wave; j < nr; j += 4) {
+            const bool sel = sm[j] >= 0;
+            T* op = out + base + (int64_t)j * m;
+            T* ep = E + base + (int64_t)j * m;
+            if (ef14 && sel) {
+                for (int c0 = 0; c0 < m4; c0 += 64 * U) {
+                    float4 v[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) v[u] = ldq<T, kNtDecode>(ep, min(c0 + u * 64 + lane, m4 - 1));
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int c = c0 + u * 64 + lane;
+                        if (c < m4) {
+                            stq<T, kNtDecode>(op, c, mean4(v[u]));
+                            stq<T, kNtDecode>(ep, c, z4);
+                        }
+                    }
+                }
+            } else if (!sel) {
+                for (int c = lane; c < m4; c += 64) stq<T, kNtDecode>(op, c, z4);
+            }
+        }
+        return;
+    }
+    // other rows: the chunk's elements as 16-B quads (scalar edges), each element's row from the
+    // slot map
+    const int64_t cnt = (int64_t)nr * m;
+    auto row_of = [&](int64_t e) -> int { return m == 1 ? (int)e : (int)div32((uint32_t)e, s.magic32); };
+    auto one = [&](int64_t e) {
+        const bool sel = sm[row_of(e)] >= 0;
+        if (ef14) {
+            float v = 0.f;
+            if (sel) {
+                v = mean1(ld1<T>(E + base + e));
+                st1<T>(E + base + e, 0.f);
+            }
+            st1<T>(out + base + e, v);
+        } else if (!sel) {
+            st1<T>(out + base + e, 0.f);
+        }
+    };
+    const int64_t pre = min<int64_t>(cnt, (4 - (base & 3)) & 3);
+    for (int64_t e = threadIdx.x; e < pre; e += 256) one(e);
+    const int64_t nq = (cnt - pre) >> 2;
+    constexpr int UQ = 4;
+    for (int64_t q0 = threadIdx.x; q0 < nq; q0 += 256 * UQ) {
+        bool sl[UQ][4];
+        float4 ev[UQ];
+#pragma unroll
+        for (int u = 0; u < UQ; ++u) {
+            const int64_t e = pre + 4 * min<int64_t>(q0 + u * 256, nq - 1);
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sl[u][j] = sm[row_of(e + j)] >= 0;
+                any = any || sl[u][j];
+            }
+            // EF14: the residual quad when any element is selected; noef: the bucket's own quad
+            // when it is partly selected (its unselected elements are zeroed in place)
+            const bool all = sl[u][0] && sl[u][1] && sl[u][2] && sl[u][3];
+            ev[u] = (ef14 ? any : (any && !all)) ? ldq<T, false>((ef14 ? E : out) + base + e, 0) : z4;
+        }
+#pragma unroll
+        for (int u = 0; u < UQ; ++u) {
+            if (q0 + u * 256 >= nq) break;
+            const int64_t e = pre + 4 * (q0 + u * 256);
+            const bool* q = sl[u];
+            const bool any = q[0] || q[1] || q[2] || q[3], all = q[0] && q[1] && q[2] && q[3];
+            const float4 v = make_float4(q[0] ? ev[u].x : 0.f, q[1] ? ev[u].y : 0.f, q[2] ? ev[u].z : 0.f,
+                                         q[3] ? ev[u].w : 0.f);
+            if (ef14) {
+                stq<T, kNtDecode>(out + base + e, 0, mean4(v));
+                if (any)
+                    stq<T, false>(E + base + e, 0, make_float4(q[0] ? 0.f : ev[u].x, q[1] ? 0.f : ev[u].y,
+                                                               q[2] ? 0.f : ev[u].z, q[3] ? 0.f : ev[u].w));
+            } else if (!all) {
+                stq<T, false>(out + base + e, 0, v);
+            }
+        }
+    }
+    for (int64_t e = pre + 4 * nq + threadIdx.x; e < cnt; e += 256) one(e);
+}
 template <typename T, int EF>
 __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, const Chunk ch,
                                              const int32_t* __restrict__ dfc,
@@ -1819,6 +1927,17 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
                                              const int32_t* __restrict__ slotmap, Scale sc,
                                              T* __restrict__ gE, T* __restrict__ out,
                                              float* __restrict__ dlds);
+// chunk c of a ride: its decode, or (world size 1, fin) the fused pack + decode
+template <typename T, int EF>
+__device__ __forceinline__ void ride_chunk(const DecodeRide<T>& d, int c, float* __restrict__ dlds) {
+    if constexpr (EF != ARCTOPK_EF21) {
+        if (d.fin) {
+            finalize_chunk<T>(d.segs, d.chunks[c], d.slotmap, d.E, d.out, d.fin, d.sc);
+            return;
+        }
+    }
+    decode_chunk<T, EF>(d.segs, d.chunks[c], d.dfirst + c, d.packed, d.slotmap, d.sc, d.gE, d.out, dlds);
+}
 
 // grid: [write ranges (nflat)] [small selects] [ride decode chunks (dr.n)] [V draw (job.n)]
 template <typename T, int EF>
@@ -1835,8 +1954,7 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     const int rb = (int)blockIdx.x - ((int)gridDim.x - job.n - dr.n);
     if (rb >= 0) {  // the ride's decode chunks
-        decode_chunk<T, EF>(dr.segs, dr.chunks[rb], dr.dfirst + rb, dr.packed, dr.slotmap, dr.sc, dr.gE, dr.out,
-                            reinterpret_cast<float*>(dyn));
+        ride_chunk<T, EF>(dr, rb, reinterpret_cast<float*>(dyn));
         return;
     }
     if ((int)blockIdx.x >= nflat) {  // the small segments' single-block selects
@@ -2802,14 +2920,9 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
 }
 
 template <typename T, int EF>
-__global__ void __launch_bounds__(256) k_decode(const SegDev* __restrict__ segs,
-                                                const Chunk* __restrict__ chunks,
-                                                const int32_t* __restrict__ dfirst,
-                                                const T* __restrict__ packed,
-                                                const int32_t* __restrict__ slotmap, Scale sc,
-                                                T* __restrict__ gE, T* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_decode(DecodeRide<T> d) {
     extern __shared__ __attribute__((aligned(16))) float dlds[];  // small-m chunk tile
-    decode_chunk<T, EF>(segs, chunks[blockIdx.x], dfirst + blockIdx.x, packed, slotmap, sc, gE, out, dlds);
+    ride_chunk<T, EF>(d, (int)blockIdx.x, dlds);
 }
 
 // Two buckets' decodes in one launch (the backward's last exchange step: the previous bucket's
@@ -2820,7 +2933,7 @@ __global__ void __launch_bounds__(256) k_decode2(DecodeRide<T> a, DecodeRide<T> 
     const int i = (int)blockIdx.x;
     const DecodeRide<T>& d = i < a.n ? a : b;
     const int c = i < a.n ? i : i - a.n;
-    decode_chunk<T, EF>(d.segs, d.chunks[c], d.dfirst + c, d.packed, d.slotmap, d.sc, d.gE, d.out, dlds);
+    ride_chunk<T, EF>(d, c, dlds);
 }
 
 // A deferred decode (an earlier bucket's, arctopk_exchange_step's `ride`) riding in the
@@ -2840,9 +2953,7 @@ __global__ void __launch_bounds__(kST) k_select_small_dec(const SegDev* __restri
         select_small_seg<T, kST>(segs, seg_ids[blockIdx.x], sketch, R, sc, rowlist, slotmap, dyn);
         return;
     }
-    decode_chunk<T, EF>(dr.segs, dr.chunks[blockIdx.x - nsel], dr.dfirst + (blockIdx.x - nsel), dr.packed,
-                        dr.slotmap, dr.sc, dr.gE, dr.out,
-                        reinterpret_cast<float*>(dyn));
+    ride_chunk<T, EF>(dr, (int)blockIdx.x - nsel, reinterpret_cast<float*>(dyn));
 }
 
 // WRITE_X = false (EF14 fold): E := x + E only; the caller reads the pre-compression
@@ -3004,6 +3115,10 @@ struct RideArgs {
     void* gerr;
     void* out;
 };
+// the fused pack + decode of plan rp's deferred step (exchange.cpp sets x_fin at world size 1)
+inline int ride_fin(const arctopk_plan* rp, int32_t ef) {
+    return rp->x_fin ? (ef == ARCTOPK_EF14 ? 1 : 2) : 0;
+}
 
 template <typename T>
 DecodeRide<T> make_ride(const RideArgs* ra) {
@@ -3019,6 +3134,8 @@ DecodeRide<T> make_ride(const RideArgs* ra) {
     dr.out = static_cast<T*>(ra->out);
     dr.sc = make_scale(ra->ws);
     dr.n = rp->n_dec;
+    dr.fin = ride_fin(rp, ra->ef);
+    dr.E = static_cast<T*>(rp->x_err);
     return dr;
 }
 
@@ -3234,33 +3351,36 @@ __global__ void __launch_bounds__(256) k_dfirst(const SegDev* __restrict__ segs,
 
 // `done` as in pack_launch (the decode after an inline all-reduce, watched by exchange.cpp)
 template <typename T, int EF>
-void decode_launch(dim3 grid, size_t lds, hipStream_t st, hipEvent_t done, const SegDev* segs, const Chunk* ch,
-                   const int32_t* dfirst, const T* packed, const int32_t* slotmap, Scale sc, T* gerr, T* out) {
+void decode_launch(dim3 grid, size_t lds, hipStream_t st, hipEvent_t done, const DecodeRide<T>& d) {
     if (done)
-        hipExtLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, nullptr, done, 0, segs, ch, dfirst,
-                              packed, slotmap, sc, gerr, out);
+        hipExtLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, nullptr, done, 0, d);
     else
-        hipLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, segs, ch, dfirst, packed, slotmap, sc,
-                           gerr, out);
+        hipLaunchKernelGGL((k_decode<T, EF>), grid, dim3(256), lds, st, d);
 }
 
+// decode chunks [c0, c1) of plan p; fin (world size 1): the fused pack + decode from residual E
 template <typename T>
 int launch_decode(const arctopk_plan* p, int c0, int c1, const int32_t* dfirst, const void* packed_,
                   const int32_t* slotmap, int32_t ws, int32_t ef, void* gerr_, void* out_, hipStream_t st,
-                  hipEvent_t done = nullptr) {
-    const T* packed = static_cast<const T*>(packed_);
-    T* gerr = static_cast<T*>(gerr_);
-    T* out = static_cast<T*>(out_);
-    dim3 grid(c1 - c0);
-    const Chunk* ch = p->d_dec + c0;
-    const Scale sc = make_scale(ws);
+                  hipEvent_t done = nullptr, int fin = 0, void* E = nullptr) {
+    DecodeRide<T> d{};
+    d.segs = p->d_segs;
+    d.chunks = p->d_dec + c0;
+    d.dfirst = dfirst + c0;
+    d.packed = static_cast<const T*>(packed_);
+    d.slotmap = slotmap;
+    d.gE = static_cast<T*>(gerr_);
+    d.out = static_cast<T*>(out_);
+    d.sc = make_scale(ws);
+    d.n = c1 - c0;
+    d.fin = fin;
+    d.E = static_cast<T*>(E);
+    const dim3 grid(c1 - c0);
     const size_t lds = (size_t)p->dec_lds_bytes;
-    if (ef == ARCTOPK_EF21)
-        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, p->d_segs, ch, dfirst + c0, packed, slotmap, sc, gerr,
-                                       out);
+    if (ef == ARCTOPK_EF21 && !fin)
+        decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, d);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
-        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, p->d_segs, ch, dfirst + c0, packed, slotmap, sc,
-                                          gerr, out);
+        decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, d);
     else
         return ARCTOPK_EINVAL;
     return (int)hipGetLastError();
@@ -3376,6 +3496,8 @@ int launch_select_ride(const arctopk_plan* p, const void* sketch_, int32_t ws, i
     dr.out = static_cast<T*>(rp_out);
     dr.sc = make_scale(rp_ws);
     dr.n = rp->n_dec;
+    dr.fin = ride_fin(rp, rp_ef);
+    dr.E = static_cast<T*>(rp->x_err);
     const size_t shm = (size_t)std::max(p->small_lds, rp->dec_lds_bytes);
     const dim3 grid(p->n_small + dr.n + job.n);
     const T* sketch = static_cast<const T*>(sketch_);
@@ -3585,9 +3707,12 @@ int decode_signal(const arctopk_plan* p, const void* packed, const int32_t* slot
     const int c0 = p->h_dec_begin[0], c1 = p->h_dec_begin[p->nseg];
     hipStream_t st = (hipStream_t)stream;
     if (c1 == c0) return done ? (int)hipEventRecord((hipEvent_t)done, st) : 0;
+    const int fin = ride_fin(p, ef);
     if (p->dtype == ARCTOPK_BF16)
-        return launch_decode<bf16_t>(p, c0, c1, p->d_dfirst, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
-    return launch_decode<float>(p, c0, c1, p->d_dfirst, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done);
+        return launch_decode<bf16_t>(p, c0, c1, p->d_dfirst, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done,
+                                     fin, p->x_err);
+    return launch_decode<float>(p, c0, c1, p->d_dfirst, packed, slotmap, ws, ef, gerr, out, st, (hipEvent_t)done,
+                                fin, p->x_err);
 }
 }  // namespace arctopk
 

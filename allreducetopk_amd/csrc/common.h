@@ -407,6 +407,8 @@ struct arctopk_plan {
     void* x_bucket;                     //   the bucket,
     void* x_gerr;                       //   the global residual (EF21),
     int x_ef, x_ws;                     //   the EF mode and world size of that call
+    int x_fin;                          // world size 1, EF14 / noef: no pack; the decode is the
+                                        //   fused pack + decode from the residual x_err (finalize)
     int x_pack;                         // its pack is deferred too (world size 1): enqueued in the
     void* x_err;                        //   next call's encode launch, or by exchange_finish; the
                                         //   residual it gathers from

@@ -593,7 +593,7 @@ extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* cons
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
     if (!e) e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, stream, nullptr);
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
-    if (!e) p->x_deferred = 0;
+    if (!e) p->x_deferred = p->x_fin = 0;
     return e;
 }
 
@@ -667,13 +667,13 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
                                  next ? next->b_V : nullptr, ride, ride->x_ws, ride->x_ef, ride->x_gerr,
                                  ride->x_bucket, &rode, stream, keyed);
         if (!e && rode) {
-            ride->x_deferred = 0;
+            ride->x_deferred = ride->x_fin = 0;
             e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
         }
         if (!e && !rode) {  // a separate decode launch after the select
             e = arctopk::decode_signal(ride, ride->b_packed, ride->b_slotmap, ride->x_ws, ride->x_ef, ride->x_gerr,
                                        ride->x_bucket, stream, nullptr);
-            if (!e) ride->x_deferred = 0;
+            if (!e) ride->x_deferred = ride->x_fin = 0;
             if (!e) e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
         }
     } else {
@@ -698,9 +698,16 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
                                  p->x_ev_packed);
         if (!e) Watchdog::get().watch(sketch_comm, p->x_ev_packed);
+    } else if (!marks && ef != ARCTOPK_EF21 && p->dtype == ARCTOPK_F32) {
+        // world size 1 (fp32, EF14 / noef): the all-reduce is the identity, so no packed buffer
+        // is needed -- the decode (riding in a later select launch, or inline below) takes the
+        // selected rows from E / the bucket itself and zeroes the rest (finalize_chunk; bf16
+        // measured 2 % slower this way and keeps pack + decode)
+        p->x_fin = 1;
+        p->x_err = err;
     } else if (defer && !marks) {
-        // world size 1, deferred: nothing reads the packed values before the next call's select
-        // (the decode rides there), so the pack rides in the next call's encode launch
+        // world size 1, deferred (EF21): nothing reads the packed values before the next call's
+        // select (the decode rides there), so the pack rides in the next call's encode launch
         p->x_pack = 1;
         p->x_err = err;
     } else {
@@ -751,7 +758,8 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk::decode_pair(pair, pair->x_ws, pair->x_ef, pair->x_gerr, pair->x_bucket, p, ws, ef, gerr, bucket,
                                  stream, packed_comm ? p->x_ev_dec : nullptr);
         if (!e) {
-            pair->x_deferred = 0;
+            pair->x_deferred = pair->x_fin = 0;
+            p->x_fin = 0;
             if (packed_comm) Watchdog::get().watch(packed_comm, p->x_ev_dec);
             ht.lap(7);
             return 0;
@@ -766,6 +774,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         if (!e) Watchdog::get().watch(packed_comm, p->x_ev_dec);
     } else {
         e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream, nullptr);
+        p->x_fin = 0;
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
     ht.lap(7);

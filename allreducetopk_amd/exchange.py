@@ -168,9 +168,15 @@ class Comm:
         return obj
 
     def register(self, t: torch.Tensor) -> None:
-        """A buffer the native step may all-reduce through the callback (by its address)."""
+        """A buffer the native step may all-reduce through the callback (by its address).  An
+        exchange group's sketch / packed buffers are slices of its bucket's, and the first group's
+        start at the bucket's own address: the longest buffer registered at an address is kept
+        (every shorter one is its prefix), so both the group's and the whole bucket's all-reduce
+        find theirs."""
         if self._fn is not None:
-            self._views[t.data_ptr()] = t
+            old = self._views.get(t.data_ptr())
+            if old is None or t.numel() > old.numel() or t.dtype != old.dtype:
+                self._views[t.data_ptr()] = t
 
     def known_stream(self, s: "torch.cuda.Stream") -> None:
         """A stream the native step may hand the callback (found by its raw handle)."""

@@ -52,7 +52,9 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4, keyed:
     1-D tensors are their own sketch (written by encode, read by select); 2-D/ND
     tensors add an [n, r] sketch and read an [m, r] projection.  keyed (world size 1, the step
     path): the multi-block select items' encode writes a 4-B energy key per row instead of
-    their sketch rows, and the select reads those keys (keys mode).
+    their sketch rows, and the select reads those keys (keys mode); and for
+    EF14 / noef the pack and the decode are one pass with no packed copy (the all-reduce is the
+    identity: DESIGN.md section 4, finalize).
     """
     from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import _geometry
     n_el = bucket_numel(shapes)
@@ -70,11 +72,21 @@ def algorithmic_bytes(ef: str, shapes, ratio: float, r: int, eb: int = 4, keyed:
         else:
             sk += eb * n * (1 if m == 1 and nd == 1 else r)
         vbytes += 0 if nd == 1 else m * r * eb
-    if ef == "noef":
+    if ef == "noef" and keyed:  # world size 1: no packed copy; the unselected elements are zeroed
+        enc = eb * n_el + sk + vbytes
+        pack = 0
+        dec = eb * (n_el - k_el)
+        read = eb * n_el + vbytes + sk
+    elif ef == "noef":
         enc = eb * n_el + sk + vbytes
         pack = 2 * eb * k_el
         dec = eb * (k_el + n_el)
         read = eb * n_el + vbytes + sk + eb * k_el + eb * k_el
+    elif ef == "ef14" and keyed:  # world size 1: decode := the selected rows of E, which are zeroed
+        enc = 3 * eb * n_el + sk + vbytes
+        pack = 0
+        dec = eb * (n_el + 2 * k_el)  # write out; read E rows, zero E rows
+        read = 2 * eb * n_el + vbytes + sk + eb * k_el
     elif ef == "ef14":
         enc = 3 * eb * n_el + sk + vbytes          # read G, E; write E := G + E
         pack = 3 * eb * k_el  # read E rows, write packed, zero E rows

@@ -70,14 +70,21 @@ def test_keys_mode_algorithmic_bytes():
     (keys mode): the encode and select bytes drop by (4 r - 4) B per such row, nothing else."""
     import bench
     conv = [[512, 512, 3, 3]] * 2  # ND: m = 18, n = 131,072 rows each (multi-block items)
-    a, b = bench.algorithmic_bytes("ef14", conv, 0.2, 4), bench.algorithmic_bytes("ef14", conv, 0.2, 4, keyed=True)
+    a, b = bench.algorithmic_bytes("ef21", conv, 0.2, 4), bench.algorithmic_bytes("ef21", conv, 0.2, 4, keyed=True)
     rows = 2 * 131072
     assert a["encode"] - b["encode"] == (16 - 4) * rows
     assert a["select"] - b["select"] == (16 - 4) * rows
     assert a["pack"] == b["pack"] and a["decode"] == b["decode"]
+    # EF14 / noef at world size 1: no packed copy -- the decode takes the selected rows from E
+    # (read and zeroed) and writes the bucket: (4 + 8 rho) B per element instead of (4 + 16 rho)
+    n_el, k_el = 2 * 512 * 512 * 9, 2 * int(131072 * 0.2) * 18
+    c = bench.algorithmic_bytes("ef14", conv, 0.2, 4, keyed=True)
+    assert c["pack"] == 0 and c["decode"] == 4 * (n_el + 2 * k_el)
+    assert bench.algorithmic_bytes("noef", conv, 0.2, 4, keyed=True)["decode"] == 4 * (n_el - k_el)
     head = [[2048, 2048]] * 16  # single-block items: keys mode does not apply
-    assert bench.algorithmic_bytes("ef14", head, 0.2, 4) == bench.algorithmic_bytes("ef14", head, 0.2, 4, keyed=True)
+    h0, h1 = bench.algorithmic_bytes("ef14", head, 0.2, 4), bench.algorithmic_bytes("ef14", head, 0.2, 4, keyed=True)
+    assert h0["encode"] == h1["encode"] and h0["select"] == h1["select"]
     # a tensor beside a multi-block item joins the multi-block batch past 4,096 rows
     mixed = [[20000, 8], [5000, 8], [100, 8]]
-    c, d = bench.algorithmic_bytes("noef", mixed, 0.2, 4), bench.algorithmic_bytes("noef", mixed, 0.2, 4, keyed=True)
+    c, d = bench.algorithmic_bytes("ef21", mixed, 0.2, 4), bench.algorithmic_bytes("ef21", mixed, 0.2, 4, keyed=True)
     assert c["encode"] - d["encode"] == 12 * (20000 + 5000)

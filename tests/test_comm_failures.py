@@ -118,3 +118,27 @@ def test_comm_status_abort_and_bad_wire_params_without_gpu():
     assert L.arctopk_comm_init_wire(8, 350.0, 10.0, 32, 0, ctypes.byref(w)) == 0
     assert L.arctopk_comm_size(w) == 1  # results of a one-rank all-reduce
     assert L.arctopk_comm_destroy(w) == 0
+
+
+def test_callback_registry_keeps_the_longest_view_at_an_address():
+    """An exchange group's buffers are prefixes of its bucket's (the first group starts at the
+    bucket's address): registering the group's view must not hide the bucket's (the N = 2 gloo
+    rehearsal failed with 'exchange all-reduce of an unregistered view' before)."""
+    from allreducetopk_amd import _native as N
+    from allreducetopk_amd import exchange as X
+    from parity import rendezvous
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    dist.init_process_group("gloo", init_method=rendezvous(), rank=0, world_size=1)
+    try:
+        c = X.Comm.callback(dist.group.WORLD)
+        bucket = torch.ones(100)
+        c.register(bucket)
+        c.register(bucket[:40])  # the first group's slice, registered later
+        for n in (100, 40):
+            c.check(N.lib().arctopk_comm_allreduce(c.handle, bucket.data_ptr(), n, N.F32, None), "allreduce")
+        c.register(bucket[60:])  # another group's slice: its own address
+        c.check(N.lib().arctopk_comm_allreduce(c.handle, bucket[60:].data_ptr(), 40, N.F32, None), "allreduce")
+        assert torch.equal(bucket, torch.ones(100))  # one rank: the sum is the value
+    finally:
+        dist.destroy_process_group()

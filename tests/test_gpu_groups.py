@@ -23,10 +23,10 @@ def _grad(b, step, dtype):
     return g.to(dtype)
 
 
-def _run(groups, ef, defer=True, wire=None, projections="device", dtype=torch.float32, steps=3):
+def _run(groups, ef, defer=True, wire=None, projections="device", dtype=torch.float32, steps=3, pg=None):
     from allreducetopk_amd.bucket import SyntheticBucket
     from allreducetopk_amd.comm_hooks import group_topk_hook_no_reshape as G
-    st = G.GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback=ef,
+    st = G.GroupTopKState(pg, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback=ef,
                           seed=23)
     st.force_exchange = True
     st.defer_decode = defer
@@ -91,3 +91,16 @@ def test_grouped_exchange_direct_caller_futures_complete_on_return():
                                                   is_last=False)) for b in (2, 1, 0)]
     assert all(f.done() for f in futs) and not st._x_pend
     torch.cuda.synchronize()
+
+
+def test_grouped_exchange_over_callback_communicators():
+    """The same through callback communicators (a gloo group: the path every non-NCCL backend and
+    the two-ranks-on-one-GPU tests take).  The first group's buffers start at the bucket's own
+    address, so the callback's buffer registry must keep both (an N = 2 gloo rehearsal of
+    bench.py failed there)."""
+    import torch.distributed as dist
+    ensure_group("nccl")
+    ref = _run("off", "ef14")
+    g = dist.new_group([0], backend="gloo")
+    _same(ref, _run("auto", "ef14", pg=g), "groups over a gloo callback communicator")
+    _same(ref, _run("off", "ef14", pg=g), "whole buckets over a gloo callback communicator")
