@@ -1835,29 +1835,35 @@ __device__ __forceinline__ void finalize_chunk(const SegDev* __restrict__ segs, 
     const int nr = (int)ch.nrows;
     const bool ef14 = fin == 1;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (s.vec && m >= 256) {  // wave per row, 16-B quads: a selected row is copied, the rest zeroed
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m4 = m >> 2;
+    if (s.vec && m >= 256) {  // wave per row, 16-B units: a selected row is copied, the rest zeroed
+        constexpr int PQ = kQuadsPer16<T>;  // quads per 16-B unit (fp32 1, bf16 2)
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, mu = m / (4 * PQ);
         constexpr int U = 4;
+        float4 zu[PQ];
+#pragma unroll
+        for (int h = 0; h < PQ; ++h) zu[h] = z4;
         for (int j = wave; j < nr; j += 4) {
             const bool sel = sm[j] >= 0;
             T* op = out + base + (int64_t)j * m;
             T* ep = E + base + (int64_t)j * m;
             if (ef14 && sel) {
-                for (int c0 = 0; c0 < m4; c0 += 64 * U) {
-                    float4 v[U];
+                for (int c0 = 0; c0 < mu; c0 += 64 * U) {
+                    float4 v[U][PQ];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) v[u] = ldq<T, kNtDecode>(ep, min(c0 + u * 64 + lane, m4 - 1));
+                    for (int u = 0; u < U; ++u) ld16<T, kNtDecode>(ep, min(c0 + u * 64 + lane, mu - 1), v[u]);
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const int c = c0 + u * 64 + lane;
-                        if (c < m4) {
-                            stq<T, kNtDecode>(op, c, mean4(v[u]));
-                            stq<T, kNtDecode>(ep, c, z4);
+                        if (c < mu) {
+#pragma unroll
+                            for (int h = 0; h < PQ; ++h) v[u][h] = mean4(v[u][h]);
+                            st16<T, kNtDecode>(op, c, v[u]);
+                            st16<T, kNtDecode>(ep, c, zu);
                         }
                     }
                 }
             } else if (!sel) {
-                for (int c = lane; c < m4; c += 64) stq<T, kNtDecode>(op, c, z4);
+                for (int c = lane; c < mu; c += 64) st16<T, kNtDecode>(op, c, zu);
             }
         }
         return;

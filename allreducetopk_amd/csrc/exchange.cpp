@@ -698,11 +698,10 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
                                  p->x_ev_packed);
         if (!e) Watchdog::get().watch(sketch_comm, p->x_ev_packed);
-    } else if (!marks && ef != ARCTOPK_EF21 && p->dtype == ARCTOPK_F32) {
-        // world size 1 (fp32, EF14 / noef): the all-reduce is the identity, so no packed buffer
-        // is needed -- the decode (riding in a later select launch, or inline below) takes the
-        // selected rows from E / the bucket itself and zeroes the rest (finalize_chunk; bf16
-        // measured 2 % slower this way and keeps pack + decode)
+    } else if (!marks && ef != ARCTOPK_EF21) {
+        // world size 1 (EF14 / noef): the all-reduce is the identity, so no packed buffer is
+        // needed -- the decode (riding in a later select launch, or inline below) takes the
+        // selected rows from E / the bucket itself and zeroes the rest (finalize_chunk)
         p->x_fin = 1;
         p->x_err = err;
     } else if (defer && !marks) {

@@ -263,10 +263,10 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   `ar_stream` (and no markers), the packed all-reduce runs there too and `stream` waits for
  *   it just before the decode, so the `finish` steps' decodes run beside it on the wire;
  *   otherwise the all-reduce is inline on `stream`.
- *   Without communicators (world size 1) and markers the all-reduces are identities: for fp32
- *   EF14 / noef no packed values are formed at all -- the decode (deferred or inline) takes the
+ *   Without communicators (world size 1) and markers the all-reduces are identities: for EF14 /
+ *   noef no packed values are formed at all -- the decode (deferred or inline) takes the
  *   selected rows from the residual / the bucket and zeroes the rest, the same bits as pack then
- *   decode; otherwise (EF21, bf16) defer = 1 defers the pack as well, to the first blocks of the
+ *   decode; for EF21, defer = 1 defers the pack as well, to the first blocks of the
  *   next step's encode launch (that step's `ride`; same EF mode and dtype, other bucket and
  *   residual buffers) or arctopk_exchange_finish.  Until the decode the plan's packed buffer and
  *   the residual's selected rows are not final.
