@@ -32,7 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel  # noqa: E402
-from workloads import HEADLINE, WORKLOADS, ddp_buckets, resnet18_cifar_shapes  # noqa: E402,F401
+from workloads import DDP_MODELS, HEADLINE, WORKLOADS, ddp_buckets, resnet18_cifar_shapes  # noqa: E402,F401
 from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import (GroupTopKState,  # noqa: E402
                                                                       group_topk_hook)
 
@@ -259,7 +259,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ef", default="ef14", choices=["noef", "ef14", "ef21"])
-    ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS) + ["resnet18_ddp"],
+    ap.add_argument("--workload", default="headline", choices=sorted(WORKLOADS) + sorted(DDP_MODELS),
                     help="bucket shape set (headline = the BASELINE metric's bucket)")
     ap.add_argument("--hook", default="arc", choices=["arc", "topk", "randk"],
                     help="arc = ARC-TopK (the metric's codec); topk / randk = the reference's "
@@ -322,9 +322,9 @@ def main():
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    if args.workload == "resnet18_ddp":  # configs[1]'s model, as its DDP buckets
-        label = "resnet18_cifar_ddp_buckets_fp32_44.7MB"
-        layouts = ddp_buckets(resnet18_cifar_shapes())
+    if args.workload in DDP_MODELS:  # configs[1] / configs[3]'s model, as its DDP buckets
+        label, model_shapes = DDP_MODELS[args.workload]
+        layouts = ddp_buckets(model_shapes())
         shapes = layouts[0]
     else:
         label, shapes = WORKLOADS[args.workload]

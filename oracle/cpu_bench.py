@@ -29,15 +29,15 @@ def _rank(rank: int, args, port: int, out_q) -> None:
     import torch.distributed as dist
 
     from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
-    from workloads import WORKLOADS
+    from workloads import DDP_MODELS, WORKLOADS
     from oracle import arctopk as A
 
     torch.set_num_threads(args.threads)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=args.ws)
-    if args.workload == "resnet18_ddp":  # configs[1]: the first of the model's DDP buckets
-        from workloads import ddp_buckets, resnet18_cifar_shapes
-        shapes = ddp_buckets(resnet18_cifar_shapes())[0]
+    if args.workload in DDP_MODELS:  # configs[1] / configs[3]: the first of the model's DDP buckets
+        from workloads import ddp_buckets
+        shapes = ddp_buckets(DDP_MODELS[args.workload][1]())[0]
     else:
         shapes = WORKLOADS[args.workload][1]
     n = bucket_numel(shapes)

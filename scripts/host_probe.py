@@ -36,8 +36,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    if args.workload == "resnet18_ddp":
-        layouts = bench.ddp_buckets(bench.resnet18_cifar_shapes())
+    if args.workload in bench.DDP_MODELS:
+        layouts = bench.ddp_buckets(bench.DDP_MODELS[args.workload][1]())
     else:
         layouts = [bench.WORKLOADS[args.workload][1]] * 4
     g = torch.Generator(device=dev).manual_seed(1000)

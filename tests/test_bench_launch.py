@@ -88,3 +88,21 @@ def test_keys_mode_algorithmic_bytes():
     mixed = [[20000, 8], [5000, 8], [100, 8]]
     c, d = bench.algorithmic_bytes("ef21", mixed, 0.2, 4), bench.algorithmic_bytes("ef21", mixed, 0.2, 4, keyed=True)
     assert c["encode"] - d["encode"] == 12 * (20000 + 5000)
+
+
+def test_ddp_model_workloads_match_the_reference_models():
+    """configs[1] / configs[3] as DDP buckets: ResNet-18 62 tensors,
+    11,173,962 parameters, 3 buckets; CIFAR-100 ResNet-50 161 tensors, 23,705,252 parameters,
+    5 buckets of at most 26 MiB; every ND tensor divides into rows of 2 t^2 (cal_k's reshape)."""
+    from allreducetopk_amd.bucket import bucket_numel
+    from workloads import DDP_MODELS, ddp_buckets
+    expect = {"resnet18_ddp": (62, 11_173_962, 3), "resnet50_ddp": (161, 23_705_252, 5)}
+    for name, (label, fn) in DDP_MODELS.items():
+        shapes = fn()
+        layouts = ddp_buckets(shapes)
+        assert (len(shapes), bucket_numel(shapes), len(layouts)) == expect[name], name
+        assert sorted(map(tuple, (s for b in layouts for s in b))) == sorted(map(tuple, shapes))
+        assert max(bucket_numel(b) * 4 for b in layouts) <= 26 << 20
+        for s in shapes:
+            if len(s) > 2:
+                assert bucket_numel([s]) % (2 * s[-1] ** 2) == 0, s

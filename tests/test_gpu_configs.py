@@ -34,7 +34,7 @@ from allreducetopk_amd import _native as N
 from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
 from allreducetopk_amd.comm_hooks import sparse_hook
 from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import GroupTopKState, group_topk_hook
-from workloads import WORKLOADS, ddp_buckets, resnet18_cifar_shapes
+from workloads import WORKLOADS, ddp_buckets, resnet18_cifar_shapes, resnet50_cifar_shapes
 from oracle import arctopk as A
 from oracle import sparse as S
 from parity import assert_bitwise, check_rows_tie_aware, ensure_group
@@ -181,6 +181,46 @@ def test_resnet18_ddp_buckets_ef14(force_exchange):
     for it in range(3):
         run.step({b: (sh, _randn(bucket_numel(sh), 900 + 10 * it + b)) for b, sh in enumerate(layouts)})
     assert run.checked == 9
+
+
+@pytest.mark.parametrize("force_exchange", [False, True])
+def test_resnet50_ddp_buckets_ef14(force_exchange):
+    """configs[3]'s model as DDP hooks it: the CIFAR-100 ResNet-50's five DDP buckets (161
+    tensors: 1x1 convs of m = 2, 3x3 convs of m = 18, BatchNorm vectors, the [100, 2048]
+    classifier), hooked in bucket order over two backwards on one state."""
+    layouts = ddp_buckets(resnet50_cifar_shapes())
+    assert len(layouts) == 5 and sum(bucket_numel(sh) for sh in layouts) == 23_705_252
+    run = ArcRun("ef14", seed=13, force_exchange=force_exchange)
+    for it in range(2):
+        run.step({b: (sh, _randn(bucket_numel(sh), 1700 + 10 * it + b)) for b, sh in enumerate(layouts)})
+    assert run.checked == 10
+
+
+def test_resnet50_ddp_buckets_topk_ef14():
+    """configs[3]'s TopK baseline (topk_sync, sparse_hook.py:163-304) on the model's five DDP
+    buckets, hooked in order on one state over two backwards: indices satisfy the exact tie
+    rule against the oracle's |X|, and given them every output and residual is bit-exact."""
+    layouts = ddp_buckets(resnet50_cifar_shapes())
+    st = sparse_hook.SparseState(None, compress_ratio=0.2, start_compress_iter=0,
+                                 sparse_type="tensor", random=False, use_error_feedback="ef14")
+    E = {}
+    for it in range(2):
+        for b, sh in enumerate(layouts):
+            G = _randn(bucket_numel(sh), 1800 + 10 * it + b)
+            out = sparse_hook.sparse_hook_sync(st, SyntheticBucket(G.to(DEV), sh, index=b,
+                                                                   is_last=(b == len(layouts) - 1))).wait()
+            torch.cuda.synchronize()
+            X = S.encode(G, E.get(b), "ef14")
+            idx = _split(st.last_indices.cpu(), st.last_k)
+            off = 0
+            for t, s_ in zip(idx, sh):
+                nel = bucket_numel([s_])
+                assert check_rows_tie_aware(t, X[off:off + nel].abs(), t.numel(), band=0.0) == 0
+                off += nel
+            res = S.simulate_step([G], [E.get(b)], None, sh, 0.2, "ef14", False, None, indices_override=[idx])
+            assert_bitwise(out, res["out"], f"it{it} bucket {b} out")
+            assert_bitwise(st.error_dict[b], res["E_new"][0], f"it{it} bucket {b} E")
+            E[b] = res["E_new"][0]
 
 
 RESNET50 = WORKLOADS["resnet50_mixed"][1]

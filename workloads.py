@@ -40,6 +40,25 @@ def resnet18_cifar_shapes():
     return shapes + [[10, 512], [10]]
 
 
+def resnet50_cifar_shapes(num_classes=100):
+    """Parameter shapes of the CIFAR-100 ResNet-50 of configs[3] in definition order (the
+    reference's cifar10/resnet.py:40-112 Bottleneck [3, 4, 6, 3]: 1x1 -> 3x3 -> 1x1 (x4), each
+    conv followed by BatchNorm weight + bias, a 1x1 conv + BN shortcut on each layer's first
+    block; run_cifar100_resnet50.py:155 ResNet50(num_classes=100)); 161 tensors, 23.71 M
+    parameters."""
+    shapes = [[64, 3, 3, 3], [64], [64]]
+    cin = 64
+    for planes, nblocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        for b in range(nblocks):
+            s_ = stride if b == 0 else 1
+            shapes += [[planes, cin, 1, 1], [planes], [planes], [planes, planes, 3, 3], [planes], [planes],
+                       [4 * planes, planes, 1, 1], [4 * planes], [4 * planes]]
+            if s_ != 1 or cin != 4 * planes:
+                shapes += [[4 * planes, cin, 1, 1], [4 * planes], [4 * planes]]
+            cin = 4 * planes
+    return shapes + [[num_classes, 2048], [num_classes]]
+
+
 def ddp_buckets(shapes, first_cap=1 << 20, cap=25 << 20, elem_bytes=4):
     """DDP's bucketing as the Reducer sees it: parameters in reverse definition order (the
     order gradients become ready), a first bucket of <= 1 MiB, then <= 25 MiB buckets
@@ -56,3 +75,10 @@ def ddp_buckets(shapes, first_cap=1 << 20, cap=25 << 20, elem_bytes=4):
     if cur:
         out.append(cur)
     return out
+
+
+# whole models as their DDP buckets (bench.py --workload; one step = one backward's buckets)
+DDP_MODELS = {
+    "resnet18_ddp": ("resnet18_cifar_ddp_buckets_fp32_44.7MB", resnet18_cifar_shapes),      # configs[1]
+    "resnet50_ddp": ("resnet50_cifar100_ddp_buckets_fp32_94.8MB", resnet50_cifar_shapes),   # configs[3]
+}
