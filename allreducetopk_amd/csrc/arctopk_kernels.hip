@@ -1531,7 +1531,8 @@ __device__ __forceinline__ void arc_refine_item(const MBatch& b, int t, MWorkspa
 // overlap instead of running back to back.  Trailing blocks may draw the next call's
 // projections (VDrawJob).
 template <typename T>
-__global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __restrict__ bp, MWorkspace* ws,
+__global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __restrict__ bp, int nitems,
+                                                               MWorkspace* ws,
                                                                const uint32_t* __restrict__ ckey,
                                                                const SegDev* __restrict__ segs,
                                                                const int32_t* __restrict__ small_ids,
@@ -1543,12 +1544,11 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __r
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-    const MBatch& b = *bp;
-    if ((int)blockIdx.x < b.cnt) {
-        arc_refine_item(b, (int)blockIdx.x, ws, ckey, dyn);
+    if ((int)blockIdx.x < nitems) {
+        arc_refine_item(*bp, (int)blockIdx.x, ws, ckey, dyn);
     }
     else
-        select_small_seg<T, kRefineThreads>(segs, small_ids[blockIdx.x - b.cnt], sketch, R, sc, rowlist,
+        select_small_seg<T, kRefineThreads>(segs, small_ids[blockIdx.x - nitems], sketch, R, sc, rowlist,
                                             slotmap, dyn);
 }
 
@@ -1947,7 +1947,8 @@ __device__ __forceinline__ void ride_chunk(const DecodeRide<T>& d, int c, float*
 
 // grid: [write ranges (nflat)] [small selects] [ride decode chunks (dr.n)] [V draw (job.n)]
 template <typename T, int EF>
-__global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, int nflat,
+__global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __restrict__ bp, const RangeGrid g,
+                                                             int nflat,
                                                              const uint32_t* __restrict__ keys, MWorkspace* ws,
                                                              const uint32_t* __restrict__ ckey,
                                                              const SegDev* __restrict__ segs,
@@ -1967,13 +1968,9 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
         select_small_seg<T, kFuseNT>(segs, small_ids[blockIdx.x - nflat], sketch, R, sc, rowlist, slotmap, dyn);
         return;
     }
-    const MBatch& b = *bp;
-    int t = 0, r = (int)blockIdx.x;  // flat grid: the ranges of the batch's items back to back
-    while (t + 1 < b.cnt && r >= b.it[t].nranges) {
-        r -= b.it[t].nranges;
-        ++t;
-    }
-    arc_write_fused_range(b.it[t], t, r, keys, ws, ckey, rowlist, slotmap, dyn);
+    int t, r;  // flat grid: the ranges of the batch's items back to back
+    if (!ms_locate(g, &t, &r)) return;
+    arc_write_fused_range(bp->it[t], t, r, keys, ws, ckey, rowlist, slotmap, dyn);
 }
 
 struct KeysGrid {
@@ -3155,7 +3152,8 @@ int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int nsm, const 
         if (ok != hipSuccess) return (int)ok;
     }
     launch_job_kernel(&k_arc_write_fused<T, EF>, dim3(nflat + nsm + dr.n + bj.n), dim3(kFuseNT), shm, st,
-                      (const MBatch*)(p->d_large_batches + bi), nflat, (const uint32_t*)p->d_keys, p->d_mws, ckey,
+                      (const MBatch*)(p->d_large_batches + bi), ms_range_grid(p->h_large_batches[bi]), nflat,
+                      (const uint32_t*)p->d_keys, p->d_mws, ckey,
                       (const SegDev*)p->d_segs, (const int32_t*)p->d_small, sketch, (int)p->r, make_scale(ws),
                       rowlist, slotmap, dr, bj);
     return (int)hipGetLastError();
@@ -3265,12 +3263,14 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         if (lds_ok != hipSuccess) return (int)lds_ok;
         if (bi == 0)
             launch_job_kernel(&k_arc_refine<T>, dim3(b.cnt + nsm + bj.n), dim3(kRefineThreads),
-                              (size_t)kRefineLdsCap * 4, st, (const MBatch*)(p->d_large_batches + bi), p->d_mws,
+                              (size_t)kRefineLdsCap * 4, st, (const MBatch*)(p->d_large_batches + bi), (int)b.cnt,
+                              p->d_mws,
                               (const uint32_t*)ckey, (const SegDev*)p->d_segs, (const int32_t*)p->d_small,
                               sketch, (int)p->r, make_scale(ws), rowlist, slotmap, bj);
         else
             hipLaunchKernelGGL(k_arc_refine<T>, dim3(b.cnt + nsm + bj.n), dim3(kRefineThreads),
-                               (size_t)kRefineLdsCap * 4, st, p->d_large_batches + bi, p->d_mws, ckey, p->d_segs,
+                               (size_t)kRefineLdsCap * 4, st, p->d_large_batches + bi, (int)b.cnt, p->d_mws, ckey,
+                               p->d_segs,
                                p->d_small, sketch, p->r, make_scale(ws), rowlist, slotmap, bj);
         if (bi == 0) *drawn = true;
         e = (int)hipGetLastError();

@@ -44,6 +44,14 @@ struct MBatch {
     int32_t cnt;
 };
 
+// Where each item's ranges start in a flat per-range grid (block x = range r of item t),
+// passed by value: a block finds its item from kernel arguments instead of walking the
+// plan-resident batch's items one dependent load at a time
+struct RangeGrid {
+    int32_t cnt;             // items
+    int32_t first[kMB + 1];  // first block of each item; first[cnt] = blocks
+};
+
 struct MState {
     uint32_t prefix, mask;  // decided leading bits
     int32_t bit;            // bits [bit-1 .. 0] still undecided
@@ -255,6 +263,23 @@ int ms_arc_compact(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWo
                    hipStream_t st);
 int ms_arc_write(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWorkspace* ws, int64_t cap_total,
                  int32_t* out_idx, int32_t* out_slot, hipStream_t st);
+// the flat per-range grid of a batch (host)
+RangeGrid ms_range_grid(const MBatch& b);
+
+// block x of a flat per-range grid -> (item t, range r); false past the last range
+__device__ __forceinline__ bool ms_locate(const RangeGrid& g, int* t, int* r) {
+    const int x = (int)blockIdx.x;
+    if (x >= g.first[g.cnt]) return false;
+    int lo = 0, hi = g.cnt - 1;  // last item with first <= x (binary search over kernel arguments)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (g.first[mid] <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    *t = lo;
+    *r = x - g.first[lo];
+    return true;
+}
 // candidate keys the ARC refine stages in LDS (more are read from their ranges' regions)
 constexpr int kRefineLdsCap = 32768;
 

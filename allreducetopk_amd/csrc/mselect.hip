@@ -259,14 +259,13 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
 // ARC: one block per range, no atomics: the keys above the first-pass bin are counted and
 // the bin's keys are copied (in index order) into the range's own candidate region;
 // cnt_gt / cnt_cand per range for the refine.
-__global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ bp,
+__global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ bp, const RangeGrid g,
                                                      const uint32_t* __restrict__ keys, MWorkspace* ws,
                                                      uint32_t* __restrict__ ckey) {
-    const MBatch& b = *bp;
     __shared__ uint32_t lds[4], s_cnt[4], s_and[4];
     int t, r;
-    if (!ms_locate(b, &t, &r)) return;
-    const MItem it = b.it[t];
+    if (!ms_locate(g, &t, &r)) return;
+    const MItem it = bp->it[t];
     uint32_t d;  // the first-pass bin (keys above it are selected; its keys are the candidates)
     {
         __shared__ uint32_t lds_d[256 + 128];
@@ -451,7 +450,7 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
 // ballot compaction in index order.  ARC: rows[out_off + slot] = i and the slot map for
 // every key; TopK: idx[out_off + slot] = i, vals[out_off + slot] = x[key_off + i].
 template <int SRC, bool ARC>
-__device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
+__device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, const uint32_t* __restrict__ keys,
                                               const void* __restrict__ x, MWorkspace* ws,
                                               int32_t* __restrict__ out_idx, void* __restrict__ out_val,
                                               int32_t* __restrict__ out_slot, void* zero_x);
@@ -462,27 +461,29 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
                                                   int32_t* __restrict__ out_idx,
                                                   void* __restrict__ out_val,
                                                   int32_t* __restrict__ out_slot, void* zero_x) {
-    ms_write_body<SRC, ARC>(b, keys, x, ws, out_idx, out_val, out_slot, zero_x);
+    int t, r;
+    if (!ms_locate(b, &t, &r)) return;
+    ms_write_body<SRC, ARC>(b, t, r, keys, x, ws, out_idx, out_val, out_slot, zero_x);
 }
 
 // ARC: the batch from device memory (plan-resident)
-__global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp, const uint32_t* __restrict__ keys,
-                                                   MWorkspace* ws, int32_t* __restrict__ out_idx,
-                                                   int32_t* __restrict__ out_slot) {
-    ms_write_body<0, true>(*bp, keys, nullptr, ws, out_idx, nullptr, out_slot, nullptr);
+__global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp, const RangeGrid g,
+                                                   const uint32_t* __restrict__ keys, MWorkspace* ws,
+                                                   int32_t* __restrict__ out_idx, int32_t* __restrict__ out_slot) {
+    int t, r;
+    if (!ms_locate(g, &t, &r)) return;
+    ms_write_body<0, true>(*bp, t, r, keys, nullptr, ws, out_idx, nullptr, out_slot, nullptr);
 }
 
 // TopK (!ARC) with zero_x (= x): the tile is rewritten with its selected elements zeroed,
 // whole tiles, so no line is left partially dirty -- EF14's `tensor.view(-1)[indices] = 0`
 // (sparse_hook.py:104) fused into the pass that already reads every element
 template <int SRC, bool ARC>
-__device__ __forceinline__ void ms_write_body(const MBatch& b, const uint32_t* __restrict__ keys,
+__device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, const uint32_t* __restrict__ keys,
                                               const void* __restrict__ x, MWorkspace* ws,
                                               int32_t* __restrict__ out_idx, void* __restrict__ out_val,
                                               int32_t* __restrict__ out_slot, void* zero_x) {
     __shared__ uint32_t s_eq[4], s_gt[4];
-    int t, r;
-    if (!ms_locate(b, &t, &r)) return;
     const MItem it = b.it[t];
     const uint32_t T = ws->st[t].prefix;
     uint32_t take_left = ws->take_eq[t][r];
@@ -566,6 +567,14 @@ void ms_item_geometry(MItem& it) {
     it.pad_ = 0;
 }
 
+RangeGrid ms_range_grid(const MBatch& b) {
+    RangeGrid g{};
+    g.cnt = b.cnt;
+    g.first[0] = 0;
+    for (int i = 0; i < b.cnt; ++i) g.first[i + 1] = g.first[i] + b.it[i].nranges;
+    return g;
+}
+
 int64_t ms_workspace_bytes(int64_t cap_total) {
     return (int64_t)sizeof(MWorkspace) + 8 * cap_total;
 }
@@ -630,7 +639,8 @@ int ms_arc_compact(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWo
     int gr;
     if (int e = arc_batch_check(b, cap_total, &gr)) return e;
     uint32_t* ckey = reinterpret_cast<uint32_t*>(ws + 1);
-    hipLaunchKernelGGL(k_arc_compact, dim3(total_ranges(b)), dim3(256), 0, st, d_b, keys, ws, ckey);
+    hipLaunchKernelGGL(k_arc_compact, dim3(total_ranges(b)), dim3(256), 0, st, d_b, ms_range_grid(b), keys, ws,
+                       ckey);
     return (int)hipGetLastError();
 }
 
@@ -639,7 +649,8 @@ int ms_arc_write(const MBatch& b, const MBatch* d_b, const uint32_t* keys, MWork
     if (b.cnt < 1) return 0;
     int gr;
     if (int e = arc_batch_check(b, cap_total, &gr)) return e;
-    hipLaunchKernelGGL(k_arc_write, dim3(total_ranges(b)), dim3(256), 0, st, d_b, keys, ws, out_idx, out_slot);
+    hipLaunchKernelGGL(k_arc_write, dim3(total_ranges(b)), dim3(256), 0, st, d_b, ms_range_grid(b), keys, ws,
+                       out_idx, out_slot);
     return (int)hipGetLastError();
 }
 
