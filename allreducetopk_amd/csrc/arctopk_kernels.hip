@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "mselect.h"
+#include "mselect_dev.h"
 #include "vdraw.h"  // (fast contraction inside, for rocrand only)
 
 using namespace arctopk;
@@ -1973,6 +1974,26 @@ __global__ void __launch_bounds__(kFuseNT) k_arc_write_fused(const MBatch* __res
     arc_write_fused_range(bp->it[t], t, r, keys, ws, ckey, rowlist, slotmap, dyn);
 }
 
+// The write pass of the refine path (ms_arc_write's body, one block per range) with a deferred
+// decode riding in the same launch: grid [write ranges] [ride decode chunks (dr.n)].  The write
+// blocks are few and latency-bound; the decode's chunks stream beside them instead of in a
+// launch of their own after the select.
+template <typename T, int EF>
+__global__ void __launch_bounds__(256) k_arc_write_ride(const MBatch* __restrict__ bp, const RangeGrid g,
+                                                        const uint32_t* __restrict__ keys, MWorkspace* ws,
+                                                        int32_t* __restrict__ out_idx, int32_t* __restrict__ out_slot,
+                                                        DecodeRide<T> dr) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    const int nflat = g.first[g.cnt];
+    if ((int)blockIdx.x >= nflat) {
+        ride_chunk<T, EF>(dr, (int)blockIdx.x - nflat, reinterpret_cast<float*>(dyn));
+        return;
+    }
+    int t, r;
+    if (!ms_locate(g, &t, &r)) return;
+    ms_write_body<0, true>(*bp, t, r, keys, nullptr, ws, out_idx, nullptr, out_slot, nullptr);
+}
+
 struct KeysGrid {
     int32_t first[kMB + 1];  // first block of each item in the flat key-pass grid
 };
@@ -3159,6 +3180,21 @@ int launch_write_fused(const arctopk_plan* p, int bi, int nflat, int nsm, const 
     return (int)hipGetLastError();
 }
 
+template <typename T, int EF>
+int launch_write_ride(const arctopk_plan* p, int bi, int32_t* rowlist, int32_t* slotmap, DecodeRide<T> dr,
+                      size_t shm, hipStream_t st) {
+    if (shm > 48 * 1024) {
+        static const hipError_t ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_arc_write_ride<T, EF>),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        if (ok != hipSuccess) return (int)ok;
+    }
+    const RangeGrid g = ms_range_grid(p->h_large_batches[bi]);
+    hipLaunchKernelGGL((k_arc_write_ride<T, EF>), dim3(g.first[g.cnt] + dr.n), dim3(256), shm, st,
+                       (const MBatch*)(p->d_large_batches + bi), g, (const uint32_t*)p->d_keys, p->d_mws, rowlist,
+                       slotmap, dr);
+    return (int)hipGetLastError();
+}
+
 // ride: a deferred decode that may run in the last select launch (*rode = true if it did)
 template <typename T>
 int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_t* rowlist, int32_t* slotmap,
@@ -3275,6 +3311,18 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
         if (bi == 0) *drawn = true;
         e = (int)hipGetLastError();
         if (e) return e;
+        // the last batch's write pass carries the deferred decode, as the fused write does
+        const bool take = ride && bi == p->n_large_batches - 1 && ride->rp->n_dec > 0 &&
+                          ride->rp->dtype == p->dtype && ride->rp->dec_lds_bytes <= 64 * 1024;
+        if (take) {
+            const DecodeRide<T> dr = make_ride<T>(ride);
+            const size_t shm = (size_t)ride->rp->dec_lds_bytes;
+            e = ride->ef == ARCTOPK_EF21 ? launch_write_ride<T, ARCTOPK_EF21>(p, bi, rowlist, slotmap, dr, shm, st)
+                                         : launch_write_ride<T, ARCTOPK_EF_NONE>(p, bi, rowlist, slotmap, dr, shm, st);
+            if (e) return e;
+            if (rode) *rode = true;
+            continue;
+        }
         e = ms_arc_write(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, rowlist, slotmap, st);
         if (e) return e;
     }

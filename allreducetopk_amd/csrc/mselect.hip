@@ -10,40 +10,15 @@
 #include <cstdlib>
 
 #include "mselect.h"
+#include "mselect_dev.h"
 
 namespace arctopk {
 namespace {
 
 constexpr int kW1 = 12;  // first-pass digit width (kMBins = 1 << kW1)
 constexpr int kW2 = 10;  // refinement digit width (12 + 10 + 10 >= 32 key bits)
-constexpr int kPerLane = kMTile / 256;  // keys per lane of a tile (16)
 constexpr int kCandPerBlock = 2048;     // candidates per block of a refinement pass
 
-// key sources: 0 = uint32 keys (ARC energies), 1 = |x| of fp32 x, 2 = |x| of bf16 x (the bf16
-// bits widened to the fp32 bit pattern of the same value: exact, so the order is bf16's)
-template <int SRC>
-__device__ __forceinline__ uint32_t load_bits(const uint32_t* __restrict__ keys,
-                                              const void* __restrict__ x, int64_t i) {
-    if constexpr (SRC == 1) return __float_as_uint(static_cast<const float*>(x)[i]);
-    else if constexpr (SRC == 2) return (uint32_t)static_cast<const uint16_t*>(x)[i] << 16;
-    else return keys[i];
-}
-
-// |x| for TopK keys: NaN sorts above inf
-template <int SRC>
-__device__ __forceinline__ uint32_t key_of(uint32_t bits) {
-    if constexpr (SRC != 0) return bits & 0x7FFFFFFFu;
-    else return bits;
-}
-
-// the selected value of x (TopK outputs), in x's own type
-template <int SRC>
-__device__ __forceinline__ void store_val(void* __restrict__ out, int64_t j, uint32_t bits) {
-    if constexpr (SRC == 1) static_cast<float*>(out)[j] = __uint_as_float(bits);
-    else if constexpr (SRC == 2) static_cast<uint16_t*>(out)[j] = (uint16_t)(bits >> 16);
-}
-
-__device__ __forceinline__ uint32_t popc64(uint64_t v) { return (uint32_t)__popcll(v); }
 
 // Flat grids of the per-range kernels: block x is range r of item t, items back to back
 // (no idle blocks padding small items up to the largest item's range count).
@@ -449,11 +424,6 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
 // One block per range, 4096-key tiles (each wave a contiguous 1024 keys, 16 per lane):
 // ballot compaction in index order.  ARC: rows[out_off + slot] = i and the slot map for
 // every key; TopK: idx[out_off + slot] = i, vals[out_off + slot] = x[key_off + i].
-template <int SRC, bool ARC>
-__device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, const uint32_t* __restrict__ keys,
-                                              const void* __restrict__ x, MWorkspace* ws,
-                                              int32_t* __restrict__ out_idx, void* __restrict__ out_val,
-                                              int32_t* __restrict__ out_slot, void* zero_x);
 
 template <int SRC, bool ARC>
 __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __restrict__ keys,
@@ -473,85 +443,6 @@ __global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp
     int t, r;
     if (!ms_locate(g, &t, &r)) return;
     ms_write_body<0, true>(*bp, t, r, keys, nullptr, ws, out_idx, nullptr, out_slot, nullptr);
-}
-
-// TopK (!ARC) with zero_x (= x): the tile is rewritten with its selected elements zeroed,
-// whole tiles, so no line is left partially dirty -- EF14's `tensor.view(-1)[indices] = 0`
-// (sparse_hook.py:104) fused into the pass that already reads every element
-template <int SRC, bool ARC>
-__device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, const uint32_t* __restrict__ keys,
-                                              const void* __restrict__ x, MWorkspace* ws,
-                                              int32_t* __restrict__ out_idx, void* __restrict__ out_val,
-                                              int32_t* __restrict__ out_slot, void* zero_x) {
-    __shared__ uint32_t s_eq[4], s_gt[4];
-    const MItem it = b.it[t];
-    const uint32_t T = ws->st[t].prefix;
-    uint32_t take_left = ws->take_eq[t][r];
-    int64_t run = ws->sel_before[t][r];
-    const int64_t r0 = (int64_t)r * it.range;
-    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (int64_t tile = r0; tile < r1; tile += kMTile) {
-        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
-        uint32_t bits[kPerLane];
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j)
-            bits[j] = load_bits<SRC>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1));
-        uint32_t weq = 0, wgt = 0;
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-            const bool valid = wb + j * 64 + lane < r1;
-            const uint32_t key = key_of<SRC>(bits[j]);
-            weq += popc64(__ballot(valid && key == T));
-            wgt += popc64(__ballot(valid && key > T));
-        }
-        if (lane == 0) {
-            s_eq[wave] = weq;
-            s_gt[wave] = wgt;
-        }
-        __syncthreads();
-        uint32_t eqb = 0, gtb = 0, teq = 0, tgt = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            eqb += w < wave ? s_eq[w] : 0u;
-            gtb += w < wave ? s_gt[w] : 0u;
-            teq += s_eq[w];
-            tgt += s_gt[w];
-        }
-        __syncthreads();
-        uint32_t run_eq = eqb;
-        int64_t run_sel = run + gtb + min(eqb, take_left);
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-            const int64_t i = wb + j * 64 + lane;
-            const bool valid = i < r1;
-            const uint32_t key = key_of<SRC>(bits[j]);
-            const bool eq = valid && key == T;
-            const bool gt = valid && key > T;
-            const uint64_t beq = __ballot(eq);
-            const bool sel = gt || (eq && run_eq + popc64(beq & lt) < take_left);
-            const uint64_t bsel = __ballot(sel);
-            const int64_t my = run_sel + popc64(bsel & lt);
-            if (sel && my < it.k) {  // bound: never store past the item's k outputs
-                out_idx[it.out_off + my] = (int32_t)i;
-                if constexpr (!ARC) store_val<SRC>(out_val, it.out_off + my, bits[j]);
-            }
-            if constexpr (ARC) {
-                if (valid) out_slot[it.slot_off + i] = sel ? (int32_t)my : -1;
-            } else {
-                if (zero_x && valid) {
-                    if constexpr (SRC == 1) static_cast<float*>(zero_x)[it.key_off + i] = sel ? 0.f : __uint_as_float(bits[j]);
-                    else if constexpr (SRC == 2) static_cast<uint16_t*>(zero_x)[it.key_off + i] = sel ? (uint16_t)0 : (uint16_t)(bits[j] >> 16);
-                }
-            }
-            run_eq += popc64(beq);
-            run_sel += popc64(bsel);
-        }
-        const uint32_t te = min(teq, take_left);
-        run += tgt + te;
-        take_left -= te;
-    }
 }
 
 }  // namespace
