@@ -124,6 +124,7 @@ _SIGS = {
     "arctopk_event_create_timed": (c_int32, [POINTER(c_void_p)]),
     "arctopk_event_elapsed_ms": (c_int32, [POINTER(ctypes.c_float), c_void_p, c_void_p]),
     "arctopk_round_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "arctopk_diag_host_times": (c_int32, [c_void_p, c_int32, c_void_p]),
     "arctopk_draw_projections": (c_int32, [c_void_p, c_uint64, c_void_p, c_void_p]),
     "arctopk_plan_philox_advance": (c_int32, [c_void_p, POINTER(c_uint64)]),
     "arctopk_version": (c_char_p, []),

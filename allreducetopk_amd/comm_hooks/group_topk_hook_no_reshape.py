@@ -37,6 +37,7 @@ import collections
 import logging
 import os
 import time
+import weakref
 from typing import Dict, List, Tuple
 
 import torch
@@ -78,10 +79,17 @@ def group_runs(segs, numel: int, esz: int, target_bytes: int):
     if ng < 2:
         return None
 
+    # arctopk_plan_group (plan.hip) checks the V offset of the run's first SKETCH segment, which
+    # need not be the run's first segment (DDP's reverse order puts biases and norms first): the
+    # V offset a run starting at i is bound to is that of the first SKETCH segment at or after i
+    next_v = [0] * (len(segs) + 1)
+    for i in range(len(segs) - 1, -1, -1):
+        next_v[i] = int(segs[i].v_off) if segs[i].kind == N.SEG_SKETCH else next_v[i + 1]
+
     def ok(i):
         s = segs[i]
         return (s.offset % 8 == 0 and s.sketch_off % 8 == 0 and s.packed_off % 8 == 0
-                and s.row_off % 4 == 0 and (s.kind != N.SEG_SKETCH or s.v_off % 8 == 0))
+                and s.row_off % 4 == 0 and next_v[i] % 8 == 0)
 
     cuts = [0]
     for j in range(1, ng):
@@ -345,7 +353,10 @@ class GroupPlan:
         N.check(L.arctopk_plan_group(parent.handle, seg_begin, seg_end, N.ctypes.byref(handle)),
                 f"arctopk_plan_group({seg_begin}, {seg_end})")
         self.handle = handle
-        self.parent = parent
+        # a weak reference: the parent caches its groups, and a strong one back would make a
+        # replaced bucket plan (DDP's bucket rebuild) wait for the cyclic GC to free its device
+        # buffers and native plans; the views below keep the buffers' storage alive
+        self.parent = weakref.ref(parent)
         self.seg_begin, self.seg_end = seg_begin, seg_end
         info = N.PlanInfo()
         N.check(L.arctopk_plan_query(handle, N.ctypes.byref(info)), "arctopk_plan_query")

@@ -1560,7 +1560,7 @@ __global__ void __launch_bounds__(kRefineThreads) k_arc_refine(const MBatch* __r
 // threshold itself instead: it stages the item's candidates in LDS, runs the same two 10-bit
 // rounds, counts the candidates of the ranges before its own, and writes its range.  The
 // selection is the same exact top-k (same T, same lowest-range-first T-equal allowances).
-constexpr int kFuseCap = 8192;              // staged candidates per block (32 KiB of LDS)
+constexpr int kFuseCap = ARCTOPK_FUSE_CAP;  // staged candidates per block (32 KiB of LDS at 8,192)
 constexpr int64_t kFuseMaxRows = ARCTOPK_FUSE_MAX_ROWS;  // host rule: largest item of a fused batch
 constexpr int kFuseNT = 256;
 constexpr int kFuseMaxBlocks = 512;         // host rule: two blocks per CU (LDS allows three)

@@ -28,6 +28,9 @@
 #ifndef ARCTOPK_FUSE_MAX_ROWS
 #define ARCTOPK_FUSE_MAX_ROWS 262144   // largest item whose refine runs in the write blocks
 #endif
+#ifndef ARCTOPK_FUSE_CAP
+#define ARCTOPK_FUSE_CAP 8192         // candidates a fused write block stages in LDS (more: swept from L2)
+#endif
 #ifndef ARCTOPK_QUAD_DEC_CHUNK
 #define ARCTOPK_QUAD_DEC_CHUNK 8192    // short-row (4 <= m < 256) fp32 decode, lane per output quad: elements per chunk
 #endif

@@ -780,7 +780,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     return e;
 }
 
-// Diagnostics (not in the public header): host ns spent in the exchange step's parts since the
+// Diagnostics (include/arctopk.h, diagnostics section): host ns spent in the exchange step's parts since the
 // last read (ARCTOPK_HOST_TIMING=1), summed over `*calls` steps; resets the sums.
 extern "C" int arctopk_diag_host_times(int64_t* ns, int32_t n, int64_t* calls) {
     if (!ns || n < 0 || !calls) return ARCTOPK_EINVAL;

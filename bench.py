@@ -370,9 +370,7 @@ def main():
         _G.HOST_TIMES.clear()
         import ctypes
         from allreducetopk_amd import _native as N
-        native_ht = N.lib().arctopk_diag_host_times  # (diagnostic export, not in the header)
-        native_ht.restype = ctypes.c_int32
-        native_ht.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        native_ht = N.lib().arctopk_diag_host_times  # (diagnostics section of include/arctopk.h)
         _ns, _calls = (ctypes.c_int64 * 8)(), ctypes.c_int64()
         native_ht(_ns, 8, ctypes.byref(_calls))  # reset
     # the timed region: K steps, no markers

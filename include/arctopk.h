@@ -269,7 +269,12 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   decode; for EF21, defer = 1 defers the pack as well, to the first blocks of the
  *   next step's encode launch (that step's `ride`; same EF mode and dtype, other bucket and
  *   residual buffers) or arctopk_exchange_finish.  Until the decode the plan's packed buffer and
- *   the residual's selected rows are not final.
+ *   the residual's selected rows are not final.  CONTRACT at world size 1 with defer = 1: the
+ *   deferred decode (and EF21's deferred pack) READS `bucket` and `err` -- the selected rows
+ *   are taken from them when it runs, not when this step is enqueued -- so a caller must leave
+ *   the bucket and residual (and gerr) untouched on every stream until that decode has been
+ *   enqueued (by arctopk_exchange_finish or a later step's `ride` / `finish`); the DDP hook does
+ *   (the Reducer reads a bucket only after its Future completes, which flushes the decode).
  * ride: an earlier step's deferred decode, run inside this step's select launch (extra blocks of
  *   the single-block select launch, or of the multi-block select's last, fused write launch: the
  *   select's latency then hides behind the decode's HBM stream), else right after the select;
@@ -504,6 +509,13 @@ int arctopk_event_elapsed_ms(float* ms, void* start, void* end);
 /* Test entry point: the kernels' fp32 -> bf16 rounding (RNE, NaN -> 0x7FC0) of n device
  * values, to check it against c10::BFloat16 on the host. */
 int arctopk_round_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
+
+/* Diagnostics (not part of the codec): with ARCTOPK_HOST_TIMING=1 in the environment at the
+ * first exchange step, the host nanoseconds each part of arctopk_exchange_step took, summed over
+ * the steps since the last read -- ns[0 .. min(n, 8)) = entry, encode, sketch all-reduce, select,
+ * pack, packed all-reduce, finish, decode; *calls = steps summed -- and the sums are reset.
+ * All zero when the variable is unset.  (bench.py --host-timing breakdowns) */
+int arctopk_diag_host_times(int64_t* ns, int32_t n, int64_t* calls);
 
 /* library build identification (for smoke tests) */
 const char* arctopk_version(void);

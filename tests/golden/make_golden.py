@@ -66,6 +66,18 @@ CASES += [
     dict(name="arc_ties_noef_ws1", hook="arc", shapes=TIES, ratio=0.25, r=4, ef="noef",
          ws=1, iters=1, start=0, seed=11, ties=True),
 ]
+# a mix in DDP's reverse order (a bias / norm vector before each weight) whose offsets allow the
+# exchange's cuts below a bucket (group_runs: 6 groups of <= 8 KiB): the two-rank grouped
+# exchange replays these (tests/test_gpu_multirank.py)
+GMIX = [[16], [16, 64], [64], [64], [64, 32, 3, 3], [32], [32, 32, 1, 1], [96, 40], [40], [40, 16, 3, 3], [8]]
+CASES += [
+    dict(name="arc_gmix_ef14_ws2", hook="arc", shapes=GMIX, ratio=0.2, r=4, ef="ef14", ws=2, iters=3,
+         start=0, seed=4321),
+    dict(name="arc_gmix_ef21_ws2", hook="arc", shapes=GMIX, ratio=0.2, r=4, ef="ef21", ws=2, iters=3,
+         start=0, seed=4321),
+    dict(name="arc_gmix_noef_bf16_ws2", hook="arc", shapes=GMIX, ratio=0.2, r=4, ef="noef", ws=2, iters=2,
+         start=0, seed=4321, dtype="bf16"),
+]
 # bf16 buckets (the Llama driver's default dtype, c4/run_llama_pretraining.py:55): V, the
 # sketch, norms and values all in bf16 as the reference keeps them in the bucket dtype
 for ef, ws, iters in (("ef14", 1, 3), ("ef21", 1, 3), ("noef", 2, 2)):

@@ -152,13 +152,35 @@ def test_residual_checks_before_any_kernel():
     assert got.is_contiguous() and table[0] is got and torch.equal(got, t)
 
 
-@pytest.mark.parametrize("shapes", SHAPE_SETS)
+# DDP's reverse parameter order: a bias / BN vector before each conv, so cuts land on RAW
+# segments; with r = 2 a 3x3 conv's V (m * r = 36) leaves the next V offset 4 mod 8
+GROUP_SHAPE_SETS = SHAPE_SETS + [
+    [[64], [64, 64, 3, 3], [64], [64], [64, 64, 3, 3], [64], [128, 64, 3, 3], [128], [128, 128, 3, 3]] * 3,
+    [[10], [10, 511], [512], [512], [512, 512, 3, 3], [512], [512, 256, 1, 1], [256], [256, 256, 3, 3]] * 2,
+    [[80, 80, 3, 3], [80]] * 6 + [[80, 80, 3, 3]],
+]
+
+
+def plan_group_accepts(segs, a, b):
+    """arctopk_plan_group's (plan.hip) alignment rule for the run [a, b), restated: the run's
+    first segment's bucket / sketch / packed offsets multiples of 8, its slot-map offset of 4,
+    and the V offset of the run's first SKETCH segment a multiple of 8."""
+    s = segs[a]
+    if s.offset % 8 or s.sketch_off % 8 or s.packed_off % 8 or s.row_off % 4:
+        return False
+    v = next((t.v_off for t in segs[a:b] if t.kind == N.SEG_SKETCH), -1)
+    return v <= 0 or v % 8 == 0
+
+
+@pytest.mark.parametrize("shapes", GROUP_SHAPE_SETS)
 @pytest.mark.parametrize("target", [1 << 12, 1 << 20, 64 << 20])
-def test_group_runs_cut_only_at_aligned_boundaries(lib, shapes, target):
+@pytest.mark.parametrize("r", [2, 4, 3])
+def test_group_runs_cut_only_at_aligned_boundaries(lib, shapes, target, r):
     """The exchange groups (arctopk_plan_group): consecutive runs covering every segment once,
-    each starting where the kernels' alignment holds, about `target` bytes each."""
+    each one a run the native group planner accepts (its rule restated), about `target` bytes
+    each."""
     from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import group_runs
-    st, segs, info = _describe(lib, shapes)
+    st, segs, info = _describe(lib, shapes, r=r)
     assert st == 0
     runs = group_runs(segs, info.numel, 4, target)
     if runs is None:
@@ -166,11 +188,28 @@ def test_group_runs_cut_only_at_aligned_boundaries(lib, shapes, target):
     assert runs[0][0] == 0 and runs[-1][1] == len(segs) and len(runs) >= 2
     for (a, b), (c, _) in zip(runs, runs[1:]):
         assert a < b == c
-    for a, _ in runs:
-        s = segs[a]
-        assert s.offset % 8 == 0 and s.sketch_off % 8 == 0 and s.packed_off % 8 == 0 and s.row_off % 4 == 0
-        assert s.kind != N.SEG_SKETCH or s.v_off % 8 == 0
+    for a, b in runs:
+        assert plan_group_accepts(segs, a, b), (a, b)
     assert len(runs) <= -(-info.numel * 4 // target)
+
+
+def test_group_runs_skip_misaligned_v_after_a_bias(lib):
+    """The ADVICE r05 case: r = 2, a bias then a 3x3 conv whose V offset is 4 mod 8 -- the
+    bias's own offsets are aligned, but a run starting there would bind a misaligned V."""
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import group_runs
+    shapes = [[80, 80, 3, 3], [80]] * 6 + [[80, 80, 3, 3]]
+    st, segs, info = _describe(lib, shapes, r=2)
+    assert st == 0
+    bad = [i for i in range(1, len(segs)) if segs[i].kind == N.SEG_RAW
+           and not plan_group_accepts(segs, i, len(segs))
+           and segs[i].offset % 8 == 0 and segs[i].sketch_off % 8 == 0 and segs[i].packed_off % 8 == 0]
+    assert bad, "the shape set no longer exercises the misaligned-V cut"
+    cut = 0
+    for target in (1 << 12, 1 << 16, 1 << 18, 1 << 19):
+        runs = group_runs(segs, info.numel, 4, target) or []
+        assert not any(a in bad for a, _ in runs)
+        cut += len(runs)
+    assert cut, "no run at all: the test checks nothing"
 
 
 def test_group_runs_headline_bucket():

@@ -56,7 +56,8 @@ def _golden_worker(rank, ws, port, td, name):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["arc_mix_ef14_ws2", "arc_mix_ef21_ws2", "arc_warmup_ef21_ws2"])
+@pytest.mark.parametrize("name", ["arc_mix_ef14_ws2", "arc_mix_ef21_ws2", "arc_warmup_ef21_ws2",
+                                  "arc_gmix_ef14_ws2", "arc_gmix_ef21_ws2"])
 def test_oracle_hook_replays_ws2_golden_over_gloo(name):
     _spawn(_golden_worker, name)
 

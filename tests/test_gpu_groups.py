@@ -104,3 +104,22 @@ def test_grouped_exchange_over_callback_communicators():
     g = dist.new_group([0], backend="gloo")
     _same(ref, _run("auto", "ef14", pg=g), "groups over a gloo callback communicator")
     _same(ref, _run("off", "ef14", pg=g), "whole buckets over a gloo callback communicator")
+
+
+def test_every_run_group_runs_returns_is_a_valid_native_group():
+    """group_runs must only return runs arctopk_plan_group accepts -- including a
+    run that starts with a 1-D segment (DDP's reverse order) whose first SKETCH tensor's V
+    offset is what the native planner checks (r = 2 and 3 make 3x3-conv V offsets 4 mod 8)."""
+    from test_capi import GROUP_SHAPE_SETS
+    from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import BucketPlan
+    built = 0
+    for shapes in GROUP_SHAPE_SETS:
+        if sum(torch.Size(s).numel() for s in shapes) > (1 << 24):
+            continue  # (the 256 MiB sets: cut at 1 KiB they are thousands of native plans)
+        for r in (2, 3, 4):
+            for dtype in (torch.float32, torch.bfloat16):
+                plan = BucketPlan([tuple(s) for s in shapes], r, 0.2, dtype, DEV)
+                for target in (1 << 12, 1 << 16):
+                    groups = plan.groups(target)  # arctopk_plan_group for every run: raises on EINVAL
+                    built += len(groups or [])
+    assert built > 0

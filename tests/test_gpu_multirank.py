@@ -390,10 +390,12 @@ def test_forced_exchange_buckets_in_flight(ef, sketch_comm):
                 gE[b] = res["gE_new"]
 
 
-def _golden_ws2_worker(rank, ws, port, name):
+def _golden_ws2_worker(rank, ws, port, name, group_bytes=0):
     """The reference's own two-rank outputs (tests/golden, made by running the reference
     hook over a real two-rank gloo group) replayed through the HIP hook -- ARC-TopK through
-    the exchange step, TopK through sparse_hook_sync -- bit for bit."""
+    the exchange step, TopK through sparse_hook_sync -- bit for bit.  group_bytes > 0: the
+    ARC-TopK bucket runs as exchange groups of about that size (exchange_groups="all"), each
+    with its own two-rank sketch and packed all-reduce, and both ranks' rows are compared."""
     sys.path.insert(0, REPO)
     sys.path.insert(0, HERE)
     torch.set_num_threads(2)
@@ -411,6 +413,8 @@ def _golden_ws2_worker(rank, ws, port, name):
         st = G.GroupTopKState(None, r=m["r"], compress_ratio=m["ratio"], start_compress_iter=m["start"],
                               use_error_feedback=m["ef"], seed=m["seed"])
         st.projections = "host"  # the golden vectors come from the reference run on CPU
+        if group_bytes:
+            st.exchange_groups, st.group_bytes = "all", group_bytes
         hook = G.group_topk_hook
     else:
         mod = sparse_hook_c4 if m["hook"] == "sparse_c4" else sparse_hook
@@ -432,6 +436,12 @@ def _golden_ws2_worker(rank, ws, port, name):
         if m["hook"] == "arc" and g.has(rank, it, "topk0_in"):
             plan = st._plans[0][1]
             rl = plan.rowlist.cpu()
+            if group_bytes:  # the bucket really ran as >= 3 groups, and both ranks chose the same rows
+                units = plan.groups(group_bytes)
+                assert units is not None and len(units) >= 3, f"{name}: {units} groups"
+                both = [torch.empty_like(rl) for _ in range(ws)]
+                dist.all_gather(both, rl)
+                assert all(torch.equal(both[0], x) for x in both[1:]), f"{name} it{it}: ranks' rows differ"
             rows = []
             for j, s_ in enumerate(plan.segments):
                 r_ = rl[s_.sel_off:s_.sel_off + s_.k_rows].long()
@@ -473,3 +483,15 @@ def test_reference_ws2_golden_through_hip_hook(name):
     torch.randperm draws, sparse_hook_c4.py:20)."""
     from parity import rendezvous
     mp.spawn(_golden_ws2_worker, args=(2, rendezvous(), name), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize("name", ["arc_gmix_ef14_ws2", "arc_gmix_ef21_ws2", "arc_gmix_noef_bf16_ws2"])
+@pytest.mark.parametrize("group_bytes", [0, 8192])
+def test_reference_ws2_golden_through_grouped_exchange(name, group_bytes):
+    """The exchange pipeline below a bucket at two ranks: the reference's
+    two-rank fixtures of a DDP-ordered mix (a bias or norm before each weight, so cuts land on
+    1-D segments) replayed with every bucket cut into 6 groups of <= 8 KiB, each group's sketch
+    and packed values all-reduced over the two ranks on its own -- outputs, E, gE and bits bit
+    for bit, the same rows on both ranks -- and whole (group_bytes 0) for comparison."""
+    from parity import rendezvous
+    mp.spawn(_golden_ws2_worker, args=(2, rendezvous(), name, group_bytes), nprocs=2, join=True)
