@@ -81,7 +81,7 @@ _SIGS = {
     "arctopk_exchange_step": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                         c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
-                                        c_void_p]),
+                                        c_void_p, c_void_p]),
     "arctopk_exchange_finish": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "arctopk_row_energy": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,

@@ -470,6 +470,25 @@ class GroupTopKState(HookState):
         if self.exchange_groups not in ("auto", "all", "off"):
             raise ValueError("ARCTOPK_EXCHANGE_GROUPS must be 'auto', 'all' or 'off'")
         self.group_bytes = int(float(os.environ.get("ARCTOPK_GROUP_MIB", "128")) * (1 << 20))
+        # Select streams: the encode (and sketch all-reduce) stay on the
+        # caller's stream, and the latency-bound select chain, the pack and the decodes of a
+        # deferred bucket run on one of two high-priority side streams (alternating), so they
+        # overlap the next buckets' encodes and each other.  Each hand-over costs a cross-queue
+        # dependency (~12 us measured) and the backward's last two decodes no longer pair, so
+        # "auto" uses them only where the overlap pays: buckets of at most `select_stream_bytes`
+        # (a large bucket's encode and decode stream at HBM speed) in a backward whose previous
+        # pass had at least `select_stream_min_buckets` such buckets (ResNet-50's DDP buckets:
+        # +11 %; ResNet-18's two: -15 %).  "on": every bucket; "off": the
+        # caller's stream only.  Results are the same bits either way.
+        self.select_streams = os.environ.get("ARCTOPK_SELECT_STREAMS", "auto")
+        if self.select_streams not in ("auto", "on", "off"):
+            raise ValueError("ARCTOPK_SELECT_STREAMS must be 'auto', 'on' or 'off'")
+        self.select_stream_bytes = int(float(os.environ.get("ARCTOPK_SELECT_STREAM_MIB", "64")) * (1 << 20))
+        self.select_stream_min_buckets = int(os.environ.get("ARCTOPK_SELECT_STREAM_MIN_BUCKETS", "4"))
+        self._sel_streams: Dict[int, List[torch.cuda.Stream]] = {}
+        self._sel_turn = 0
+        self._sel_small = 0        # select-stream-sized buckets hooked so far in this backward
+        self._sel_small_last = 0   # ... in the previous backward
         # The plan of a bucket is found by its buffer's identity (no gradients() walk per
         # call).  DDP rebuilds its buckets once, after the first iteration, and the caching
         # allocator may hand a rebuilt bucket the same block: for the first
@@ -612,6 +631,17 @@ class GroupTopKState(HookState):
             s = torch.cuda.Stream(device=device, priority=priority)
             table[idx] = s
         return s
+
+    def _select_stream(self, device) -> "torch.cuda.Stream":
+        """The next of the device's two select streams (high priority: their latency-bound
+        launches are dispatched ahead of the caller's queued encode blocks)."""
+        idx = torch.device(device).index or 0
+        pair = self._sel_streams.get(idx)
+        if pair is None:
+            pair = [torch.cuda.Stream(device=device, priority=XSTREAM_PRIORITY) for _ in range(2)]
+            self._sel_streams[idx] = pair
+        self._sel_turn ^= 1
+        return pair[self._sel_turn]
 
     def _after_load(self) -> None:
         # prefetched projections were keyed on seeds of the old rng position
@@ -894,6 +924,11 @@ def cal_k(state, tensor) -> int:
     return max(1, int(n * state.compress_ratio)) * m
 
 
+def _bucket_plan_of(p):
+    """The bucket plan a pending exchange entry belongs to (a GroupPlan's parent)."""
+    return p.parent() if isinstance(p, GroupPlan) else p
+
+
 def _check_bucket_layout(buf: torch.Tensor, grads) -> None:
     if not buf.is_cuda:
         raise RuntimeError("ARC-TopK HIP codec needs the bucket on a GPU (got CPU tensor); "
@@ -1068,17 +1103,30 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             units = (plan,)
         # finish first: a caller that skipped buckets, or one whose stream changed since a
         # pending step (its decode is enqueued on that step's own stream)
-        if any(getattr(e_[0], "parent", e_[0]) is plan or e_[4] != sid for e_ in pend):
+        if any(_bucket_plan_of(e_[0]) is plan or e_[4] != sid for e_ in pend):
             state.flush_exchange()
-        # the decode riding in this call's select launch: the previous bucket's without
-        # collectives, the one before it with them (its all-reduce has had a whole call to
-        # finish, so the select is not held back waiting for it)
-        depth = 2 if comms else 1
         ars = None
         if comms:
             ars = state._side_stream(state._ar_streams, dev, XSTREAM_PRIORITY)
             if pk.kind == "callback" and ars.cuda_stream not in pk._streams:
                 pk.known_stream(ars)
+        # a select stream for this bucket (whole buckets of deferring callers, no markers)
+        small = total * input_tensor.element_size() <= state.select_stream_bytes
+        state._sel_small += int(small)
+        if bucket.is_last():
+            state._sel_small_last, state._sel_small = state._sel_small, 0
+        side = None
+        if (state.select_streams != "off" and not grouped and marks is None and dd
+                and (not comms or ars is not None)
+                and (state.select_streams == "on"
+                     or (small and state._sel_small_last >= state.select_stream_min_buckets))):
+            side = state._select_stream(dev)
+            nplan, nseed = None, 0  # the select does not draw the next call's V (that encode would wait)
+        # the decode riding in this call's select launch: the previous bucket's without
+        # collectives, the one before it with them (its all-reduce has had a whole call to
+        # finish, so the select is not held back waiting for it) or with select streams (the
+        # same stream's previous bucket: the streams alternate)
+        depth = 2 if (comms or side is not None) else 1
         if defer:
             fut = ExchangeFuture()
             fut._arctopk_state = state
@@ -1126,7 +1174,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                                           ars.cuda_stream if ars is not None else None,
                                           int(u_defer), ride[0].handle if ride is not None else None,
                                           ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
-                                          u_vptr, marks)
+                                          u_vptr, marks, side.cuda_stream if side is not None else None)
             if st_:
                 if comms:
                     for c in (sk, pk):

@@ -330,16 +330,19 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
                         if (ok) __builtin_nontemporal_store(x, reinterpret_cast<u4_t*>(ep) + c);
                     }
                     if (!ok) x = u4_t{0u, 0u, 0u, 0u};
-                    const bf2_t x0 = __builtin_bit_cast(bf2_t, x.x), x1 = __builtin_bit_cast(bf2_t, x.y);
-                    const bf2_t x2 = __builtin_bit_cast(bf2_t, x.z), x3 = __builtin_bit_cast(bf2_t, x.w);
+                    // The words go through scalars: ROCm 7.2's clang lowers __builtin_bit_cast of an
+                    // ext_vector ELEMENT (x.y, x.z, ...) to element 0 (and loads only that dword;
+                    // scripts/probe/dot2vec.hip), which paired every column with the wrong V entry
+                    const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                     for (int j = 0; j < R; ++j) {
                         const u4_t v = vp[j * mu + c];
+                        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
                         float a = acc[j];
-                        a = __builtin_amdgcn_fdot2_f32_bf16(x0, __builtin_bit_cast(bf2_t, v.x), a, false);
-                        a = __builtin_amdgcn_fdot2_f32_bf16(x1, __builtin_bit_cast(bf2_t, v.y), a, false);
-                        a = __builtin_amdgcn_fdot2_f32_bf16(x2, __builtin_bit_cast(bf2_t, v.z), a, false);
-                        a = __builtin_amdgcn_fdot2_f32_bf16(x3, __builtin_bit_cast(bf2_t, v.w), a, false);
+#pragma unroll
+                        for (int h = 0; h < 4; ++h)
+                            a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, xw[h]),
+                                                                __builtin_bit_cast(bf2_t, vw[h]), a, false);
                         acc[j] = a;
                     }
                 }
@@ -3052,11 +3055,20 @@ __global__ void __launch_bounds__(256) k_sketch_combine(const SegDev* __restrict
     }
 }
 
+// a launch that completes `done` itself when given one (hipExtLaunchKernelGGL's stop event)
+template <typename... KArgs, typename... Args>
+inline void launch_done(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipStream_t st, hipEvent_t done,
+                        Args... args) {
+    if (done) hipExtLaunchKernelGGL(k, grid, block, lds, st, nullptr, done, 0, args...);
+    else hipLaunchKernelGGL(k, grid, block, lds, st, args...);
+}
+
 // one launch (every tile's V slice fits in LDS), then the partial-sketch sums of
-// column-split tensors
+// column-split tensors; done: completed by the last of them
 template <typename T, int R>
 int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
-                    uint32_t* keys, hipStream_t st, PackRide<T> pr) {
+                    uint32_t* keys, hipStream_t st, PackRide<T> pr, hipEvent_t done = nullptr) {
+    hipEvent_t enc_done = p->n_split == 0 ? done : nullptr;
     if (p->n_enc > 0 || pr.n > 0) {
         const bool use_e = p->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
         const int nt = use_e ? p->n_enc_e : p->n_enc;
@@ -3067,47 +3079,52 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
         float* pb = p->d_part;
         if (p->enc_short) {  // no wave-per-row tile: the lean kernel
             if (ef == ARCTOPK_EF_NONE)
-                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+                launch_done(&k_encode_short<T, R, ARCTOPK_EF_NONE, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
             else if (ef == ARCTOPK_EF14 && err_in)
-                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+                launch_done(&k_encode_short<T, R, ARCTOPK_EF14, true>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
             else if (ef == ARCTOPK_EF14)
-                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+                launch_done(&k_encode_short<T, R, ARCTOPK_EF14, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
             else
-                hipLaunchKernelGGL((k_encode_short<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+                launch_done(&k_encode_short<T, R, ARCTOPK_EF21, true>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         } else if (ef == ARCTOPK_EF_NONE)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF_NONE, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+            launch_done(&k_encode<T, R, ARCTOPK_EF_NONE, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         else if (ef == ARCTOPK_EF14 && err_in)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+            launch_done(&k_encode<T, R, ARCTOPK_EF14, true>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         else if (ef == ARCTOPK_EF14)
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF14, false>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+            launch_done(&k_encode<T, R, ARCTOPK_EF14, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         else
-            hipLaunchKernelGGL((k_encode<T, R, ARCTOPK_EF21, true>), grid, block, lds, st, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
+            launch_done(&k_encode<T, R, ARCTOPK_EF21, true>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
         const int e = (int)hipGetLastError();
         if (e) return e;
     }
-    if (p->n_split == 0) return 0;
+    if (p->n_split == 0) {
+        // (no encode launch at all: nothing for `done` to follow but the stream itself)
+        if (done && !(p->n_enc > 0 || pr.n > 0)) return (int)hipEventRecord(done, st);
+        return 0;
+    }
     const int gx = (int)std::min<int64_t>(256, (p->split_rows_max * R + 255) / 256);
-    hipLaunchKernelGGL(k_sketch_combine<T>, dim3(gx, p->n_split), dim3(256), 0, st, p->d_segs, p->d_split, R,
-                       p->d_part, sk);
+    launch_done(&k_sketch_combine<T>, dim3(gx, p->n_split), dim3(256), 0, st, done, (const SegDev*)p->d_segs,
+                (const int32_t*)p->d_split, R, (const float*)p->d_part, sk);
     return (int)hipGetLastError();
 }
 
 template <typename T>
 int launch_encode(const arctopk_plan* p, const void* grad, void* err, int ef, int err_in, const void* V,
-                  void* sketch, uint32_t* keys, hipStream_t st, PackRide<T> pr = PackRide<T>{}) {
+                  void* sketch, uint32_t* keys, hipStream_t st, PackRide<T> pr = PackRide<T>{},
+                  hipEvent_t done = nullptr) {
     const T* G = static_cast<const T*>(grad);
     T* E = static_cast<T*>(err);
     const T* Vt = static_cast<const T*>(V);
     T* sk = static_cast<T*>(sketch);
     switch (p->r) {
-        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
-        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
-        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
-        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
-        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
-        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
-        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
-        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, keys, st, pr);
+        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
     }
     return ARCTOPK_EINVAL;
 }
@@ -3459,7 +3476,8 @@ namespace arctopk {
 // (the sketch all-reduce is the identity, so the keys are the select's; its key pass then only
 // builds the histograms).  Every other segment's sketch is written as arctopk_encode writes it.
 int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef, int32_t err_in, const void* V,
-                 void* sketch, void* stream, const arctopk_plan* rp, const void* rp_grad, void* rp_err, int* rode) {
+                 void* sketch, void* stream, const arctopk_plan* rp, const void* rp_grad, void* rp_err, int* rode,
+                 void* done) {
     if (rode) *rode = 0;
     if (!p || !grad || !sketch) return ARCTOPK_EINVAL;
     if (ef != ARCTOPK_EF_NONE && !err) return ARCTOPK_EINVAL;
@@ -3477,7 +3495,7 @@ int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef,
         if (take)
             pr = PackRide<bf16_t>{rp->d_segs, rp->d_pack, static_cast<const bf16_t*>(rp_grad), static_cast<bf16_t*>(rp_err),
                                   rp->b_rowlist, rp->b_slotmap, static_cast<bf16_t*>(rp->b_packed), rp->d_dfirst, rp->n_pack};
-        const int e = launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, keys, st, pr);
+        const int e = launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, keys, st, pr, (hipEvent_t)done);
         if (!e && take) *rode = 1;
         return e;
     }
@@ -3485,7 +3503,7 @@ int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef,
     if (take)
         pr = PackRide<float>{rp->d_segs, rp->d_pack, static_cast<const float*>(rp_grad), static_cast<float*>(rp_err),
                              rp->b_rowlist, rp->b_slotmap, static_cast<float*>(rp->b_packed), rp->d_dfirst, rp->n_pack};
-    const int e = launch_encode<float>(p, grad, err, ef, err_in, V, sketch, keys, st, pr);
+    const int e = launch_encode<float>(p, grad, err, ef, err_in, V, sketch, keys, st, pr, (hipEvent_t)done);
     if (!e && take) *rode = 1;
     return e;
 }

@@ -416,6 +416,12 @@ struct arctopk_plan {
     void* x_err;                        //   next call's encode launch, or by exchange_finish; the
                                         //   residual it gathers from
     void* x_ev_dec;                     // completed by an inline decode after a collective
+    void* x_stream;                     // the select stream the deferred step's select, pack and
+                                        //   decode run on (NULL: the caller's stream)
+    void* x_ev_enc;                     // recorded on the caller's stream after the encode (and
+                                        //   the sketch all-reduce) when a select stream takes over
+    void* x_ev_join;                    // recorded on the select stream after the decode, for the
+                                        //   stream that finishes the step to wait on
 };
 namespace arctopk {
 // keyed: the call's encode ran in keys mode (encode_keyed; world size 1 only)
@@ -426,10 +432,12 @@ int select_ride(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* 
 int select_draw_keyed(const arctopk_plan* p, const void* sketch, int32_t ws, int32_t* rowlist, int32_t* slotmap,
                       const arctopk_plan* next, uint64_t next_seed, void* next_V, bool keyed, void* stream);
 // keyed encode; rp (may be null): a plan whose deferred pack (its bound buffers, bucket rp_grad
-// and residual rp_err, the same EF mode and dtype) rides in the launch: *rode = 1 when it did
+// and residual rp_err, the same EF mode and dtype) rides in the launch: *rode = 1 when it did;
+// done (may be null): an event the encode's last kernel completes itself (its stop event: no
+// marker packet on the stream)
 int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef, int32_t err_in, const void* V,
                  void* sketch, void* stream, const arctopk_plan* rp = nullptr, const void* rp_grad = nullptr,
-                 void* rp_err = nullptr, int* rode = nullptr);
+                 void* rp_err = nullptr, int* rode = nullptr, void* done = nullptr);
 int decode_pair(const arctopk_plan* pa, int32_t ws_a, int32_t ef_a, void* gerr_a, void* out_a,
                 const arctopk_plan* pb, int32_t ws_b, int32_t ef_b, void* gerr_b, void* out_b, void* stream,
                 void* done);

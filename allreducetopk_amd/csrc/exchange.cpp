@@ -584,16 +584,38 @@ int pack_now(arctopk_plan* p, void* stream) {
 }
 }  // namespace
 
+namespace {
+// `to` waits for everything enqueued on `from` so far (plan p's join event)
+int join_stream(arctopk_plan* p, hipStream_t from, hipStream_t to) {
+    if (from == to) return 0;
+    if (int e = ensure_event(&p->x_ev_join, hipEventDisableTiming | hipEventReleaseToDevice)) return e;
+    hipError_t he = hipEventRecord((hipEvent_t)p->x_ev_join, from);
+    if (he == hipSuccess) he = hipStreamWaitEvent(to, (hipEvent_t)p->x_ev_join, 0);
+    return (int)he;
+}
+// the stream a deferred step's remaining work goes on: its select stream, else the caller's
+inline hipStream_t x_stream_of(const arctopk_plan* p, hipStream_t caller) {
+    return p->x_stream ? (hipStream_t)p->x_stream : caller;
+}
+}  // namespace
+
 extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* const* marks) {
     if (!p) return ARCTOPK_EINVAL;
     if (!p->x_deferred) return 0;
-    hipStream_t st = (hipStream_t)stream;
-    int e = pack_now(p, stream);
+    hipStream_t cs = (hipStream_t)stream;
+    // where the step's select and pack ran (its select stream, or the caller's); `stream` then
+    // waits for the decode
+    hipStream_t st = x_stream_of(p, cs);
+    int e = pack_now(p, st);
     if (!e) e = wait_ar(p, st);
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
-    if (!e) e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, stream, nullptr);
+    if (!e) e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, p->x_ws, p->x_ef, p->x_gerr, p->x_bucket, st, nullptr);
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
-    if (!e) p->x_deferred = p->x_fin = 0;
+    if (!e) e = join_stream(p, st, cs);
+    if (!e) {
+        p->x_deferred = p->x_fin = 0;
+        p->x_stream = nullptr;
+    }
     return e;
 }
 
@@ -603,8 +625,15 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
                                      void* stream, void* ar_stream, int32_t defer, arctopk_plan* ride,
                                      void* const* ride_marks, arctopk_plan* const* finish,
                                      void* const* const* finish_marks, int32_t nfinish, const void* V,
-                                     void* const* marks) {
+                                     void* const* marks, void* sel_stream) {
     if (!p || !bucket || !p->b_sketch || !sketch_comm != !packed_comm || nfinish < 0 || (nfinish && !finish))
+        return ARCTOPK_EINVAL;
+    // a select stream takes the select, pack and decodes off the caller's stream (not with markers:
+    // the marker pass times the phases in one stream's order); its packed all-reduce must then go
+    // on the all-reduce stream (a communicator's collectives stay on one stream each), and it draws
+    // no projections for the next call (that call's encode on the caller's stream would wait for it)
+    const bool side = sel_stream && sel_stream != stream && !marks;
+    if (side && ((packed_comm && (!ar_stream || ar_stream == stream || ar_stream == sel_stream)) || next))
         return ARCTOPK_EINVAL;
     if (sketch_comm && sketch_comm->nranks != packed_comm->nranks) return ARCTOPK_EINVAL;
     if (next && (!next->b_sketch || next->dtype != p->dtype || next->device != p->device)) return ARCTOPK_EINVAL;
@@ -616,6 +645,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (int f = comm_failed(packed_comm)) return f;
     const int ws = packed_comm ? packed_comm->nranks : 1;
     hipStream_t st = (hipStream_t)stream, as = (hipStream_t)ar_stream;
+    hipStream_t ss = side ? (hipStream_t)sel_stream : st;  // the select, pack and decodes
     HostTimer ht;
     if (ht.on) g_ht_calls.fetch_add(1, std::memory_order_relaxed);
     // this bucket's own deferred decode, if a caller never finished it (the hook always does)
@@ -630,6 +660,14 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // world size 1 (no communicators): the sketch is not all-reduced, so the multi-block select
     // items' encode writes their energy keys directly (keys mode)
     const bool keyed = !sketch_comm;
+    // with a select stream at world size 1 the encode's last kernel completes x_ev_enc itself (its
+    // stop event), so the caller's stream carries no marker packet; with collectives the event
+    // follows the sketch all-reduce (a marker after it, below)
+    void* enc_done = nullptr;
+    if (!e && side && keyed) {
+        if ((e = ensure_event(&p->x_ev_enc, 0))) return e;
+        enc_done = p->x_ev_enc;
+    }
     // the ride's deferred pack (world size 1) runs as the first blocks of this encode launch when
     // it can: same EF mode and dtype, other buffers (a bucket hooked twice in a row reads the
     // residual the pack rewrites: then the pack goes first, in its own launch)
@@ -639,16 +677,18 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         int prode = 0;
         if (fits) {
             e = arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream, ride, ride->x_bucket,
-                                      ride->x_err, &prode);
+                                      ride->x_err, &prode, enc_done);
             if (!e && prode) ride->x_pack = 0;
             if (!e) e = pack_now(ride, stream);  // (not taken: nothing of this call's touches it)
         } else {
             e = pack_now(ride, stream);
-            if (!e) e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream)
+            if (!e) e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream, nullptr,
+                                                      nullptr, nullptr, nullptr, enc_done)
                               : arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
         }
     } else if (!e) {
-        e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream)
+        e = keyed ? arctopk::encode_keyed(p, bucket, err, ef, err_in, V, p->b_sketch, stream, nullptr, nullptr,
+                                          nullptr, nullptr, enc_done)
                   : arctopk_encode(p, bucket, err, ef, err_in, V, p->b_sketch, stream);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_ENCODE, st);
@@ -657,28 +697,50 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (!e && sketch_comm) e = arctopk_comm_allreduce(sketch_comm, p->b_sketch, p->info.sketch_len, p->dtype, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_SKETCH_AR, st);
     if (e) return e;
+    // The select stream takes over after the encode and the sketch all-reduce: the latency-bound
+    // select chain (and the decode riding in it) overlaps the caller's next encode instead of
+    // delaying it (select streams)
+    if (side) {
+        hipError_t he = hipSuccess;
+        if (!enc_done) {  // (with collectives: after the sketch all-reduce)
+            if ((e = ensure_event(&p->x_ev_enc, 0))) return e;
+            he = hipEventRecord((hipEvent_t)p->x_ev_enc, st);
+        }
+        if (he == hipSuccess) he = hipStreamWaitEvent(ss, (hipEvent_t)p->x_ev_enc, 0);
+        if (he != hipSuccess) return (int)he;
+    }
     ht.lap(2);
+    // a ride whose step ran on another select stream is not ordered before this one: finished on
+    // its own stream instead (the caller's stream then waits for it)
+    if (ride && ride->x_stream && ride->x_stream != (void*)ss) {
+        if ((e = arctopk_exchange_finish(ride, stream, ride_marks))) return e;
+        ride = nullptr;
+    }
     // the select, with an earlier bucket's deferred decode riding in the same launch when
     // both fit (the select's latency hides behind the decode's stream)
     int rode = 0;
     if (ride) {
-        if ((e = wait_ar(ride, st)) || (e = mark(ride_marks, ARCTOPK_MARK_PACKED_AR, st))) return e;
+        if ((e = wait_ar(ride, ss)) || (e = mark(ride_marks, ARCTOPK_MARK_PACKED_AR, ss))) return e;
         e = arctopk::select_ride(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
                                  next ? next->b_V : nullptr, ride, ride->x_ws, ride->x_ef, ride->x_gerr,
-                                 ride->x_bucket, &rode, stream, keyed);
+                                 ride->x_bucket, &rode, ss, keyed);
         if (!e && rode) {
             ride->x_deferred = ride->x_fin = 0;
-            e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
+            ride->x_stream = nullptr;
+            e = mark(ride_marks, ARCTOPK_MARK_DECODE, ss);
         }
         if (!e && !rode) {  // a separate decode launch after the select
             e = arctopk::decode_signal(ride, ride->b_packed, ride->b_slotmap, ride->x_ws, ride->x_ef, ride->x_gerr,
-                                       ride->x_bucket, stream, nullptr);
-            if (!e) ride->x_deferred = ride->x_fin = 0;
-            if (!e) e = mark(ride_marks, ARCTOPK_MARK_DECODE, st);
+                                       ride->x_bucket, ss, nullptr);
+            if (!e) {
+                ride->x_deferred = ride->x_fin = 0;
+                ride->x_stream = nullptr;
+            }
+            if (!e) e = mark(ride_marks, ARCTOPK_MARK_DECODE, ss);
         }
     } else {
         e = arctopk::select_draw_keyed(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
-                                       next ? next->b_V : nullptr, keyed, stream);
+                                       next ? next->b_V : nullptr, keyed, ss);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_SELECT, st);
     if (e) return e;
@@ -695,7 +757,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         if ((e = ensure_event(&p->x_ev_packed, 0)) ||
             (e = ensure_event(&p->x_ev_ar, hipEventDisableTiming | hipEventReleaseToDevice)))
             return e;
-        e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream,
+        e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, ss,
                                  p->x_ev_packed);
         if (!e) Watchdog::get().watch(sketch_comm, p->x_ev_packed);
     } else if (!marks && ef != ARCTOPK_EF21) {
@@ -704,13 +766,14 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         // selected rows from E / the bucket itself and zeroes the rest (finalize_chunk)
         p->x_fin = 1;
         p->x_err = err;
-    } else if (defer && !marks) {
+    } else if (defer && !marks && !side) {
         // world size 1, deferred (EF21): nothing reads the packed values before the next call's
         // select (the decode rides there), so the pack rides in the next call's encode launch
+        // (not with a select stream: that encode, on the caller's stream, would wait for this select)
         p->x_pack = 1;
         p->x_err = err;
     } else {
-        e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, stream);
+        e = arctopk_pack(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, ss);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_PACK, st);
     if (e) return e;
@@ -728,7 +791,8 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     // launch with its own decode, after its own packed all-reduce (unless markers were asked for)
     arctopk_plan* pair = nullptr;
     if (!defer && !async_ar && nfinish > 0 && finish[nfinish - 1] && finish[nfinish - 1] != p &&
-        finish[nfinish - 1]->x_deferred && !(finish_marks && finish_marks[nfinish - 1]) && !marks)
+        finish[nfinish - 1]->x_deferred && !(finish_marks && finish_marks[nfinish - 1]) && !marks &&
+        x_stream_of(finish[nfinish - 1], st) == ss)
         pair = finish[nfinish - 1];
     // earlier buckets' deferred decodes the caller wants done now (in its order)
     for (int32_t i = 0; i < nfinish && !e; ++i)
@@ -742,40 +806,44 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         p->x_gerr = gerr;
         p->x_ef = ef;
         p->x_ws = ws;
+        p->x_stream = side ? (void*)ss : nullptr;
         return 0;
     }
     if (async_ar) {  // this step's own packed all-reduce, on the all-reduce stream
-        if ((e = (int)hipStreamWaitEvent(st, (hipEvent_t)p->x_ev_ar, 0))) return e;
+        if ((e = (int)hipStreamWaitEvent(ss, (hipEvent_t)p->x_ev_ar, 0))) return e;
     } else if (packed_comm) {
-        e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, stream);
+        e = arctopk_comm_allreduce(packed_comm, p->b_packed, p->info.packed_len, p->dtype, ss);
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_PACKED_AR, st);
     if (e) return e;
     if (pair) {
         if (packed_comm && (e = ensure_event(&p->x_ev_dec, hipEventDisableTiming | hipEventReleaseToDevice))) return e;
-        if ((e = pack_now(pair, stream)) || (e = wait_ar(pair, st))) return e;
+        if ((e = pack_now(pair, ss)) || (e = wait_ar(pair, ss))) return e;
         e = arctopk::decode_pair(pair, pair->x_ws, pair->x_ef, pair->x_gerr, pair->x_bucket, p, ws, ef, gerr, bucket,
-                                 stream, packed_comm ? p->x_ev_dec : nullptr);
+                                 ss, packed_comm ? p->x_ev_dec : nullptr);
         if (!e) {
             pair->x_deferred = pair->x_fin = 0;
+            pair->x_stream = nullptr;
             p->x_fin = 0;
             if (packed_comm) Watchdog::get().watch(packed_comm, p->x_ev_dec);
+            e = join_stream(p, ss, st);  // the caller's stream sees the bucket decoded
             ht.lap(7);
-            return 0;
+            return e;
         }
         if (e != ARCTOPK_EINVAL) return e;
         // the pair does not qualify (dtype, EF class, LDS): one by one
-        if ((e = arctopk_exchange_finish(pair, stream, nullptr))) return e;
+        if ((e = arctopk_exchange_finish(pair, ss, nullptr))) return e;
     }
     if (packed_comm) {  // the decode kernel completes x_ev_dec: the inline all-reduce is watched too
         if ((e = ensure_event(&p->x_ev_dec, hipEventDisableTiming | hipEventReleaseToDevice))) return e;
-        e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream, p->x_ev_dec);
+        e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, ss, p->x_ev_dec);
         if (!e) Watchdog::get().watch(packed_comm, p->x_ev_dec);
     } else {
-        e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, stream, nullptr);
+        e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, ss, nullptr);
         p->x_fin = 0;
     }
     if (!e) e = mark(marks, ARCTOPK_MARK_DECODE, st);
+    if (!e) e = join_stream(p, ss, st);  // the caller's stream sees the bucket decoded
     ht.lap(7);
     return e;
 }

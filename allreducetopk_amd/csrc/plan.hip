@@ -507,6 +507,8 @@ extern "C" int arctopk_plan_destroy(arctopk_plan* p) {
     if (p->x_ev_packed) (void)hipEventDestroy((hipEvent_t)p->x_ev_packed);
     if (p->x_ev_ar) (void)hipEventDestroy((hipEvent_t)p->x_ev_ar);
     if (p->x_ev_dec) (void)hipEventDestroy((hipEvent_t)p->x_ev_dec);
+    if (p->x_ev_enc) (void)hipEventDestroy((hipEvent_t)p->x_ev_enc);
+    if (p->x_ev_join) (void)hipEventDestroy((hipEvent_t)p->x_ev_join);
     delete[] p->h_large_batches;
     if (p->d_large_batches) (void)hipFree(p->d_large_batches);
     if (p->d_mws) (void)hipFree(p->d_mws);

@@ -121,6 +121,24 @@ def sparse_algorithmic_bytes(hook: str, ef: str, n_el: int, k_el: int, ws: int, 
     return int(16 * n_el + 28 * k_el)
 
 
+def pmc_call_traffic(workload: str, ef: str, tag: str = "fx"):
+    """HBM bytes per hook call of the N > 1 code path (every libarctopk kernel of a call: encode,
+    key / select passes, pack, decode) from the newest profiles/<round>/pmc_<workload>_<ef>_<tag>.json
+    (scripts/profile.sh with BENCH_ARGS=--force-exchange; summarize_prof.py's `per_call`)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_{workload}_{ef}_{tag}.json")))
+    if not paths:
+        return None, None, None
+    with open(paths[-1]) as fh:
+        doc = json.load(fh)
+    pc = doc.get("per_call")
+    if not pc:
+        return None, None, None
+    from allreducetopk_amd.build import embedded_hash
+    lib = doc.get("lib_hash")
+    return pc["bytes"], os.path.relpath(paths[-1], REPO), (None if lib is None else lib == embedded_hash())
+
+
 def pmc_traffic(workload: str, ef: str, kernel: str, n_gpus: int = 1):
     """HBM bytes per launch of `kernel` from the newest committed PMC profile of this
     workload (profiles/<round>/pmc_<workload>_<ef>.json, written by
@@ -412,6 +430,23 @@ def main():
         forced = {"value": round(args.steps * bytes_per_step / fe / 1e9, 2),
                   "ms_per_bucket": round(fe / args.steps / nb * 1e3, 4), "steps": args.steps,
                   "hook_path": "exchange (one-rank RCCL communicators)"}
+        # the N > 1 code path's own roofline: its algorithmic bytes -- the
+        # sketch all-reduced between encode and select, so no keys mode; packed values formed,
+        # all-reduced and decoded: (16 + 16 rho) N + sketch + select for EF14 --
+        # over the wall time per bucket (the path is device-bound at these sizes: host enqueue
+        # below device time, scripts/host_probe.py), PMC bytes per call beside it
+        fx_alg = [algorithmic_bytes(args.ef, sh, args.ratio, args.r, eb, keyed=False) for sh in layouts]
+        fx_bytes = sum(d["total"] for d in fx_alg) / nb
+        fx_s = fe / args.steps / nb
+        tr, tr_src, tr_match = pmc_call_traffic(args.workload + ("_bf16" if args.dtype == "bf16" else ""), args.ef)
+        forced["roofline"] = {
+            "bound": "hbm", "algorithmic_bytes_per_call": int(fx_bytes),
+            "bytes_formula": {"ef14": "(16 + 16 rho) N + sketch + select", "noef": "(8 + 12 rho) N + sketch + select",
+                              "ef21": "(16 + 28 rho) N + sketch + select"}[args.ef],
+            "wall_us_per_call": round(fx_s * 1e6, 1), "achieved": round(fx_bytes / fx_s / 1e9, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fx_bytes / fx_s / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": tr, "traffic_source": tr_src, "traffic_lib_match": tr_match,
+            "traffic_ratio": round(tr / fx_bytes, 3) if tr else None}
         st.force_exchange = False
 
     # The same exchange path beside an emulated N-rank wire (exchange.Comm.wire): each all-reduce

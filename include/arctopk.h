@@ -282,6 +282,15 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  * finish[0 .. nfinish): earlier deferred steps decoded after this pack, in order.
  * `V`: the projections to encode with (NULL: the plan's bound projection buffer, drawn there
  * for `seed` when draw != 0).  `marks`: see ARCTOPK_MARK_*.
+ * sel_stream (NULL: `stream`): a SELECT STREAM.  The draw, the encode and the sketch all-reduce
+ *   stay on `stream`; the select (+ ride), the pack, the `finish` decodes and this step's own
+ *   decode go on sel_stream after an event on the encode, so the latency-bound select chain runs
+ *   beside the caller's next encode.  A deferred step remembers its select stream: its decode
+ *   (arctopk_exchange_finish, or a later step's `ride`) goes there, and the finishing stream then
+ *   waits for it; a ride from another select stream is finished on its own instead of riding.
+ *   A non-deferred step leaves `stream` waiting for its decode.  With a select stream: `next`
+ *   must be NULL (the next call draws its own projections), markers disable it, and with
+ *   communicators `ar_stream` must be a third stream (ARCTOPK_EINVAL otherwise).
  * Replaces: the whole of group_topk_hook's compressed path (:254-290) given the seed.
  */
 int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
@@ -290,9 +299,10 @@ int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* ger
                           void* stream, void* ar_stream, int32_t defer, arctopk_plan* ride,
                           void* const* ride_marks, arctopk_plan* const* finish,
                           void* const* const* finish_marks, int32_t nfinish, const void* V,
-                          void* const* marks);
-/* The deferred decode of `plan`'s last deferred exchange step, on `stream` (no-op if none):
- * after that step's packed all-reduce (and, at world size 1, its deferred pack). */
+                          void* const* marks, void* sel_stream);
+/* The deferred decode of `plan`'s last deferred exchange step (no-op if none): after that step's
+ * packed all-reduce (and, at world size 1, its deferred pack), on the step's select stream if it
+ * had one (then `stream` waits for it), else on `stream`. */
 int arctopk_exchange_finish(arctopk_plan* plan, void* stream, void* const* marks);
 
 /*

@@ -6,7 +6,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${OUT:-tests}
 mkdir -p "$OUT"
-timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 240 --timeout-method thread \
+[ $# -eq 0 ] && set -- tests
+timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest "$@" -m gpu -x -v --timeout 240 --timeout-method thread \
     > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 tail -3 "$OUT/pytest_gpu.log"

@@ -22,5 +22,6 @@ for r in rows[start:start + 40]:
     if "k_encode" in r["Kernel_Name"] and int(r["Start_Timestamp"]) > t0 and r is not rows[start]:
         if rows.index(r) > start + 1 and "k_encode" in rows[rows.index(r) - 1]["Kernel_Name"]:
             pass
+    q = r.get("Stream_Id") or r.get("Queue_Id") or "?"
     print(f"    +{(int(r['Start_Timestamp']) - t0) / 1e3:8.1f} us  {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:8.2f} us  "
-          f"{r['Kernel_Name'].split('(')[0].replace('void ', '')[:50]:50s} grid={r['Grid_Size_X']}x{r['Grid_Size_Y']} lds={r['LDS_Block_Size']}")
+          f"q{q:>3s} {r['Kernel_Name'].split('(')[0].replace('void ', '')[:50]:50s} grid={r['Grid_Size_X']}x{r['Grid_Size_Y']} lds={r['LDS_Block_Size']}")

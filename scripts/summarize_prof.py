@@ -62,8 +62,17 @@ for ent in out.values():
     ent["bytes_per_launch"] = ent["read_bytes"] + ent["write_bytes"]
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from allreducetopk_amd.build import embedded_hash  # noqa: E402
+# per hook call: every libarctopk kernel's bytes (k_*; torch's own fills / copies / randn excluded)
+# over the calls, counted as encode launches (one per call; profile runs skip the marker pass)
+calls = sum(v["launches"] for k, v in out.items() if k in ("k_encode", "k_encode_short"))
+per_call = None
+if calls:
+    tot = sum(v["bytes_per_launch"] * v["launches"] for k, v in out.items() if k.startswith("k_"))
+    per_call = {"calls": calls, "bytes": round(tot / calls),
+                "kernels": sorted(k for k in out if k.startswith("k_"))}
+    print(f"== per hook call: {calls} calls, {tot / calls / 1e6:.2f} MB of libarctopk kernel traffic each ==")
 with open(os.path.join(root, "pmc_per_launch.json"), "w") as fh:
     json.dump({"note": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads) + WRITE_SIZE, "
                        "KiB -> bytes, averaged per launch; separate --pmc passes",
                "lib_hash": embedded_hash(),  # the libarctopk.so source hash these counters were taken on
-               "kernels": out}, fh, indent=1)
+               "kernels": out, "per_call": per_call}, fh, indent=1)

@@ -741,3 +741,49 @@ def test_public_decode_needs_only_its_slot_map(ef):
             plan.encode(G, None, N.EF_NONE, True, torch.randn(max(1, plan.info.v_len), device=DEV), stream)
             plan.select(1, stream)
             plan.pack(G, None, N.EF_NONE, stream)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
+def test_row_path_sketch_matches_fp32_accumulation(dtype, ef):
+    """The wave-per-row encode (m >= 64) of every dtype against the sketch the reference forms,
+    X.view(n, m) @ V with fp32 accumulation and one rounding to the bucket dtype (CPU `mm`;
+    another summation order: within one rounding of the dtype).  Structured inputs pin the
+    column <-> projection pairing exactly (a bf16 path that paired the wrong elements passed
+    every property test of round 5: the bf16 goldens have no m >= 64 tensor)."""
+    shapes = [[16, 64], [8], [64, 128], [100, 72], [256, 2048]]
+    n_el = bucket_numel(shapes)
+    g = torch.Generator().manual_seed(17)
+    G = torch.randn(n_el, generator=g).to(dtype)
+    E = torch.randn(n_el, generator=g).to(dtype)
+    p = BucketPlan([tuple(s) for s in shapes], 4, 0.2, dtype, DEV)
+    V = torch.randn(p.info.v_len, generator=g).to(dtype)
+    code = {"noef": N.EF_NONE, "ef14": N.EF14, "ef21": N.EF21}[ef]
+    Ed = E.to(DEV)
+    p.encode(G.to(DEV), Ed if ef != "noef" else None, code, True, V.to(DEV), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    X = G if ef == "noef" else (G + E if ef == "ef14" else G - E)  # rounded to the dtype, as the reference
+    sk = p.sketch.cpu()
+    tol = 2.0 ** -7 if dtype == torch.bfloat16 else 2e-5
+    for s in p.segments:
+        if s.kind == N.SEG_RAW:
+            continue
+        x = X[s.offset:s.offset + s.n * s.m].view(s.n, s.m).float()
+        v = V[s.v_off:s.v_off + s.m * 4].view(s.m, 4).float()
+        ref = (x @ v).to(dtype).float()
+        d = sk[s.sketch_off:s.sketch_off + s.n * 4].view(s.n, 4).float()
+        scale = (x.abs() @ v.abs()).clamp_min(1e-30)  # the sum's magnitude bounds its rounding
+        bad = ((d - ref).abs() > tol * scale).sum().item()
+        assert bad == 0, f"{dtype} {ef} [{s.n}, {s.m}]: {bad} sketch entries off by more than one rounding"
+    if ef == "ef14":
+        assert torch.equal(Ed.cpu(), X), "E := G + E (rounded to the dtype)"
+    # the pairing, exactly: G[r][c] = c + 1 and V[c][j] = [c == j]  ->  sketch[r][j] = j + 1
+    q = BucketPlan([(4, 64)], 4, 0.25, dtype, DEV)
+    Gc = (torch.arange(64, dtype=torch.float32) + 1).repeat(4).to(dtype)
+    Vi = torch.zeros(64, 4)
+    for j in range(4):
+        Vi[j, j] = 1.0
+    q.encode(Gc.to(DEV), None, N.EF_NONE, True, Vi.flatten().to(dtype).to(DEV), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = torch.tensor([1.0, 2.0, 3.0, 4.0]).repeat(4, 1)
+    assert torch.equal(q.sketch[:16].view(4, 4).float().cpu(), want)

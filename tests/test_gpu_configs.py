@@ -59,11 +59,13 @@ class ArcRun:
     """Drives one GroupTopKState over a sequence of calls per bucket and replays every
     compressed call through the oracle (single rank)."""
 
-    def __init__(self, ef, seed=1234, force_exchange=False):
+    def __init__(self, ef, seed=1234, force_exchange=False, select_streams=None):
         self.ef = ef
         self.st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0,
                                  use_error_feedback=ef, seed=seed)
         self.st.force_exchange = force_exchange
+        if select_streams is not None:  # default: the state's ("auto": select streams for <= 64 MiB)
+            self.st.select_streams = select_streams
         self.st.defer_decode = True  # every bucket's Future is waited after the last one, as DDP does
         self.ost = A.OracleState(r=4, compress_ratio=0.2, start_compress_iter=0,
                                  use_error_feedback=ef, seed=seed)
@@ -169,31 +171,41 @@ def test_roberta_embedding_ef14():
     assert run.checked == 3
 
 
-@pytest.mark.parametrize("force_exchange", [False, True])
-def test_resnet18_ddp_buckets_ef14(force_exchange):
+@pytest.mark.parametrize("force_exchange,select_streams", [(False, "auto"), (True, "auto"), (False, "off"),
+                                                           (True, "off")])
+def test_resnet18_ddp_buckets_ef14(force_exchange, select_streams):
     """configs[1]: the CIFAR ResNet-18's three DDP buckets (reverse parameter order,
     1 MiB first bucket, 25 MiB cap), hooked in bucket order over three backwards on one
     state: per-bucket plans, residuals and projections stay separate.  With the exchange
-    step (one-rank RCCL) two buckets per backward are overlapped and deferred."""
+    step (one-rank RCCL) two buckets per backward are overlapped and deferred.  "auto": each
+    bucket's select, pack and decodes on one of the two select streams."""
     layouts = ddp_buckets(resnet18_cifar_shapes())
     assert len(layouts) == 3 and sum(bucket_numel(sh) for sh in layouts) == 11_173_962
-    run = ArcRun("ef14", seed=11, force_exchange=force_exchange)
+    run = ArcRun("ef14", seed=11, force_exchange=force_exchange, select_streams=select_streams)
     for it in range(3):
         run.step({b: (sh, _randn(bucket_numel(sh), 900 + 10 * it + b)) for b, sh in enumerate(layouts)})
     assert run.checked == 9
 
 
-@pytest.mark.parametrize("force_exchange", [False, True])
-def test_resnet50_ddp_buckets_ef14(force_exchange):
+@pytest.mark.parametrize("force_exchange,select_streams,ef", [(False, "auto", "ef14"), (True, "auto", "ef14"),
+                                                              (False, "off", "ef14"), (False, "auto", "ef21"),
+                                                              (True, "auto", "noef")])
+def test_resnet50_ddp_buckets_ef14(force_exchange, select_streams, ef):
     """configs[3]'s model as DDP hooks it: the CIFAR-100 ResNet-50's five DDP buckets (161
     tensors: 1x1 convs of m = 2, 3x3 convs of m = 18, BatchNorm vectors, the [100, 2048]
-    classifier), hooked in bucket order over two backwards on one state."""
+    classifier), hooked in bucket order over two backwards on one state (EF21 / noef also
+    through the select streams: EF21's pack then runs on the select stream, not in the next
+    encode)."""
     layouts = ddp_buckets(resnet50_cifar_shapes())
     assert len(layouts) == 5 and sum(bucket_numel(sh) for sh in layouts) == 23_705_252
-    run = ArcRun("ef14", seed=13, force_exchange=force_exchange)
+    run = ArcRun(ef, seed=13, force_exchange=force_exchange, select_streams=select_streams)
+    if ef == "ef21":  # the dense init backward, then two compressed ones
+        run.step({b: (sh, _randn(bucket_numel(sh), 1600 + b)) for b, sh in enumerate(layouts)})
     for it in range(2):
         run.step({b: (sh, _randn(bucket_numel(sh), 1700 + 10 * it + b)) for b, sh in enumerate(layouts)})
     assert run.checked == 10
+    if select_streams == "auto":
+        assert run.st._sel_streams, "the select streams were not used"
 
 
 def test_resnet50_ddp_buckets_topk_ef14():
