@@ -332,7 +332,7 @@ __device__ __forceinline__ void encode_tile(const SegDev* __restrict__ segs, con
                     if (!ok) x = u4_t{0u, 0u, 0u, 0u};
                     // The words go through scalars: ROCm 7.2's clang lowers __builtin_bit_cast of an
                     // ext_vector ELEMENT (x.y, x.z, ...) to element 0 (and loads only that dword;
-                    // scripts/probe/dot2vec.hip), which paired every column with the wrong V entry
+                    // scripts/probe_dot2vec.hip), which paired every column with the wrong V entry
                     const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                     for (int j = 0; j < R; ++j) {
