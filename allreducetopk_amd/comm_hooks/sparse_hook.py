@@ -10,10 +10,13 @@ Per bucket call (all on the caller's stream, no host synchronisation):
     RandK: indices      torch.randperm(numel, device)[:k] after the shared reseed
                         (index_source="torch": the reference's own draw on a GPU), the
                         same draw on the CPU generator (index_source="host": the reference
-                        run on CPU, as the golden vectors were made), or a keyed device
-                        permutation (index_source="hash", perf mode); then gather
+                        run on CPU, as the golden vectors were made), then gather; or
+                        (index_source="hash", perf mode) the k largest keyed-hash keys per
+                        tensor -- a uniform k-subset -- through the TopK radix select:
+                        ascending indices, gather (and EF14's E[idx] = 0) in its last pass
     residual        EF14: E[idx] = 0 | EF21: E[idx] += values
     RandK: all_reduce(values)              -> decode: zero + scatter(values / ws)
+                                              (hash: one pass over whole chunks)
     TopK : all_gather(values), all_gather(indices)
                                            -> decode: zero + rank-ordered scatter-add, / ws
     EF21: gE += out; out = gE (fused into decode)
@@ -225,11 +228,15 @@ def _compress_exchange(state: SparseState, bucket, group, world_size: int, ef: i
             for t, k, ko in zip(tensors, ks, k_off):
                 host[ko:ko + k].copy_(torch.randperm(t.numel())[:k])
             indices.copy_(host)
-        else:
-            N.check(L.arctopk_randk_indices(nt, a_n, a_k, a_ko, int(seed), indices.data_ptr(),
-                                            stream), "arctopk_randk_indices")
-        N.check(L.arctopk_sparse_gather(xsrc, nt, a_off, a_k, a_ko, indices.data_ptr(),
-                                        values.data_ptr(), dt, stream), "arctopk_sparse_gather")
+        else:  # "hash": the k largest keyed-hash keys per tensor, ascending, gathered in the select;
+            # EF14's `E[indices] = 0` (:104) happens in its last pass, as for TopK
+            ws_buf = _workspace(state, device, numels)
+            N.check(L.arctopk_randk_select(xsrc, nt, a_off, a_n, a_k, a_ko, int(seed), indices.data_ptr(),
+                                           values.data_ptr(), ws_buf.data_ptr(), dt, int(fold14), stream),
+                    "arctopk_randk_select")
+        if state.index_source != "hash":
+            N.check(L.arctopk_sparse_gather(xsrc, nt, a_off, a_k, a_ko, indices.data_ptr(),
+                                            values.data_ptr(), dt, stream), "arctopk_sparse_gather")
         bits_sum = sum_k * dtype_bits(dtype)
     else:
         ws_buf = _workspace(state, device, numels)
@@ -244,7 +251,8 @@ def _compress_exchange(state: SparseState, bucket, group, world_size: int, ef: i
     state.last_indices, state.last_k = indices, ks
     if on_values is not None:
         on_values(values)
-    if ef != N.EF_NONE and not (fold14 and not state.random):  # residual persistence (:257-267)
+    fused_residual = fold14 and (not state.random or state.index_source == "hash")
+    if ef != N.EF_NONE and not fused_residual:  # residual persistence (:257-267)
         N.check(L.arctopk_sparse_residual(state.error_dict[b].data_ptr(), nt, a_off, a_k, a_ko,
                                           indices.data_ptr(), values.data_ptr(), ef, e_decay, dt, stream),
                 "arctopk_sparse_residual")
@@ -255,8 +263,10 @@ def _compress_exchange(state: SparseState, bucket, group, world_size: int, ef: i
             state.comm_bits_this_round += 2 * (world_size - 1) * bits_sum
         if world_size > 1:
             dist.all_reduce(values, group=group, async_op=False)
+        ascending = 2 if state.index_source == "hash" else 0  # one pass of whole chunks
         N.check(L.arctopk_sparse_decode(x, total, nt, a_off, a_k, a_ko, sum_k, indices.data_ptr(),
-                                        values.data_ptr(), 1, world_size, 0, gerr, g_decay, dt, stream),
+                                        values.data_ptr(), 1, world_size, ascending, gerr, g_decay, dt,
+                                        stream),
                 "arctopk_sparse_decode")
     else:
         if count_bits:

@@ -36,7 +36,7 @@ struct MItem {
     int64_t cand_cap;  // candidate-list capacity
     int32_t range;     // keys per range (multiple of kMTile)
     int32_t nranges;   // ceil(n / range) <= kMMaxRanges
-    int32_t pad_;
+    uint32_t hseed;    // RandK (hash keys): the tensor's key seed (rk_key)
 };
 
 struct MBatch {
@@ -246,9 +246,12 @@ int64_t ms_workspace_bytes(int64_t cap_total);
 // (the items' cand_off + cand_cap must fit).  The workspace's `done` counters must be
 // zero before the first use (hipMemset once; every kernel leaves them zero).
 // zero_x (TopK only, = x or null): write x back with the selected elements zeroed
+// hashed (RandK): the keys are rk_key(it.hseed, index) instead of |x| -- the k largest of these
+// distinct keys are a uniformly random k-subset, emitted in ascending index order; x (may be null:
+// indices only) is then only the source of the gathered values and of zero_x
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
-              int32_t* out_slot, void* zero_x, hipStream_t st);
+              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed = false);
 
 // ARC selection after the fused key kernel (keys + first-pass histogram + digit, every
 // item in candidate mode), in three launches per batch: ms_arc_compact (per range: the

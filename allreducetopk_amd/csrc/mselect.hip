@@ -67,10 +67,11 @@ __device__ __forceinline__ uint32_t block_exscan_u32(uint32_t v, uint32_t* lds, 
     return before + x - v;
 }
 
-// TopK start state: |x| keys, only the sign bit is known
+// TopK start state: |x| keys, only the sign bit is known (RandK hash keys: nothing is)
+template <int SRC>
 __global__ void __launch_bounds__(256) k_ms_init(MBatch b, MWorkspace* ws) {
     const int t = blockIdx.x;
-    ms_init_item(ws, t, b.it[t].k, 0x7FFFFFFFu, 0u);
+    ms_init_item(ws, t, b.it[t].k, SRC >= 3 ? 0xFFFFFFFFu : 0x7FFFFFFFu, 0u);
     if (threadIdx.x == 0) ws->done[t].v = 0;
 }
 
@@ -110,15 +111,13 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
         uint32_t k4[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            k4[u] = from_cand ? src[i + u * stride]
-                              : key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + i + u * stride));
+            k4[u] = from_cand ? src[i + u * stride] : item_key<SRC>(it, keys, x, i + u * stride);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if ((k4[u] & s.mask) == s.prefix) atomicAdd(&h[(k4[u] >> shift) & dmask], 1u);
     }
     for (; i < n; i += stride) {
-        const uint32_t key = from_cand ? src[i]
-                                       : key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + i));
+        const uint32_t key = from_cand ? src[i] : item_key<SRC>(it, keys, x, i);
         if ((key & s.mask) == s.prefix) atomicAdd(&h[(key >> shift) & dmask], 1u);
     }
     __syncthreads();
@@ -189,7 +188,7 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
         uint32_t kv[kPerLane];
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j)
-            kv[j] = key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)));
+            kv[j] = item_key<SRC>(it, keys, x, min<int64_t>(wb + j * 64 + lane, r1 - 1));
         uint32_t nin = 0;
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
@@ -364,7 +363,7 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
             const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
             uint32_t gt = 0, eq = 0;
             for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
-                const uint32_t key = key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + i));
+                const uint32_t key = item_key<SRC>(it, keys, x, i);
                 const bool in = (key & s.m1) == s.p1;
                 gt += (in && key > T) ? 1u : 0u;
                 eq += key == T ? 1u : 0u;
@@ -455,7 +454,7 @@ void ms_item_geometry(MItem& it) {
     // candidates: the k-th key's 12-bit bin; a few % of n on gradient-like data, all of
     // n on degenerate data (e.g. a zero tensor) -> full mode past the cap
     it.cand_cap = it.n <= 65536 ? it.n : std::max<int64_t>(65536, it.n / 8);
-    it.pad_ = 0;
+    it.hseed = 0;
 }
 
 RangeGrid ms_range_grid(const MBatch& b) {
@@ -472,7 +471,7 @@ int64_t ms_workspace_bytes(int64_t cap_total) {
 
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
-              int32_t* out_slot, void* zero_x, hipStream_t st) {
+              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed) {
     const int cnt = b.cnt;
     if (cnt < 1) return 0;
     int gr = 1;
@@ -493,7 +492,7 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
     const dim3 gh(hb, cnt), gt(gr, cnt), gflat(total_ranges(b));
 #define MS_LAUNCH(FF, AR)                                                                              \
     do {                                                                                               \
-        if (!AR) hipLaunchKernelGGL(k_ms_init, dim3(cnt), dim3(256), 0, st, b, ws);                    \
+        if (!AR) hipLaunchKernelGGL(k_ms_init<FF>, dim3(cnt), dim3(256), 0, st, b, ws);                \
         hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
         hipLaunchKernelGGL(k_ms_compact<FF>, gflat, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);     \
         hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
@@ -504,6 +503,10 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
     } while (0)
     if (arc)
         MS_LAUNCH(0, true);
+    else if (hashed && x_bf16)
+        MS_LAUNCH(4, false);
+    else if (hashed)
+        MS_LAUNCH(3, false);
     else if (x_bf16)
         MS_LAUNCH(2, false);
     else

@@ -10,12 +10,13 @@ namespace arctopk {
 constexpr int kPerLane = kMTile / 256;  // keys per lane of a tile (16)
 
 // key sources: 0 = uint32 keys (ARC energies), 1 = |x| of fp32 x, 2 = |x| of bf16 x (the bf16
-// bits widened to the fp32 bit pattern of the same value: exact, so the order is bf16's)
+// bits widened to the fp32 bit pattern of the same value: exact, so the order is bf16's);
+// 3 / 4 = RandK hash keys (rk_key of the index) with fp32 / bf16 x as the value source
 template <int SRC>
 __device__ __forceinline__ uint32_t load_bits(const uint32_t* __restrict__ keys,
                                               const void* __restrict__ x, int64_t i) {
-    if constexpr (SRC == 1) return __float_as_uint(static_cast<const float*>(x)[i]);
-    else if constexpr (SRC == 2) return (uint32_t)static_cast<const uint16_t*>(x)[i] << 16;
+    if constexpr (SRC == 1 || SRC == 3) return __float_as_uint(static_cast<const float*>(x)[i]);
+    else if constexpr (SRC == 2 || SRC == 4) return (uint32_t)static_cast<const uint16_t*>(x)[i] << 16;
     else return keys[i];
 }
 
@@ -26,11 +27,34 @@ __device__ __forceinline__ uint32_t key_of(uint32_t bits) {
     else return bits;
 }
 
-// the selected value of x (TopK outputs), in x's own type
+// RandK keys: a keyed bijection of the element's index in its tensor (xorshift-multiply rounds,
+// each invertible on 32 bits), so the keys of a tensor are distinct and the k largest form a
+// uniformly random k-subset -- selected by the same exact radix select as TopK, ascending
+__device__ __forceinline__ uint32_t rk_mix(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ uint32_t rk_key(uint32_t seed, int64_t i) {
+    return rk_mix(rk_mix((uint32_t)i ^ seed) + 0x9E3779B9u * (seed | 1u));
+}
+
+// the select key of element i (index within its item)
+template <int SRC>
+__device__ __forceinline__ uint32_t item_key(const MItem& it, const uint32_t* __restrict__ keys,
+                                             const void* __restrict__ x, int64_t i) {
+    if constexpr (SRC >= 3) return rk_key(it.hseed, i);
+    else return key_of<SRC>(load_bits<SRC>(keys, x, it.key_off + i));
+}
+
+// the selected value of x (TopK / RandK outputs), in x's own type
 template <int SRC>
 __device__ __forceinline__ void store_val(void* __restrict__ out, int64_t j, uint32_t bits) {
-    if constexpr (SRC == 1) static_cast<float*>(out)[j] = __uint_as_float(bits);
-    else if constexpr (SRC == 2) static_cast<uint16_t*>(out)[j] = (uint16_t)(bits >> 16);
+    if constexpr (SRC == 1 || SRC == 3) static_cast<float*>(out)[j] = __uint_as_float(bits);
+    else if constexpr (SRC == 2 || SRC == 4) static_cast<uint16_t*>(out)[j] = (uint16_t)(bits >> 16);
 }
 
 __device__ __forceinline__ uint32_t popc64(uint64_t v) { return (uint32_t)__popcll(v); }
@@ -54,15 +78,23 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, con
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (int64_t tile = r0; tile < r1; tile += kMTile) {
         const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
-        uint32_t bits[kPerLane];
+        uint32_t bits[kPerLane], kv[kPerLane];  // x's bits (TopK: also the key's source), the keys
 #pragma unroll
-        for (int j = 0; j < kPerLane; ++j)
-            bits[j] = load_bits<SRC>(keys, x, it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1));
+        for (int j = 0; j < kPerLane; ++j) {
+            const int64_t i = min<int64_t>(wb + j * 64 + lane, r1 - 1);
+            if constexpr (SRC >= 3) {  // RandK: keys from the index; x only for values / zero_x
+                kv[j] = rk_key(it.hseed, i);
+                bits[j] = x ? load_bits<SRC>(keys, x, it.key_off + i) : 0u;
+            } else {
+                bits[j] = load_bits<SRC>(keys, x, it.key_off + i);
+                kv[j] = key_of<SRC>(bits[j]);
+            }
+        }
         uint32_t weq = 0, wgt = 0;
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
             const bool valid = wb + j * 64 + lane < r1;
-            const uint32_t key = key_of<SRC>(bits[j]);
+            const uint32_t key = kv[j];
             weq += popc64(__ballot(valid && key == T));
             wgt += popc64(__ballot(valid && key > T));
         }
@@ -86,7 +118,7 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, con
         for (int j = 0; j < kPerLane; ++j) {
             const int64_t i = wb + j * 64 + lane;
             const bool valid = i < r1;
-            const uint32_t key = key_of<SRC>(bits[j]);
+            const uint32_t key = kv[j];
             const bool eq = valid && key == T;
             const bool gt = valid && key > T;
             const uint64_t beq = __ballot(eq);
@@ -95,14 +127,16 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, con
             const int64_t my = run_sel + popc64(bsel & lt);
             if (sel && my < it.k) {  // bound: never store past the item's k outputs
                 out_idx[it.out_off + my] = (int32_t)i;
-                if constexpr (!ARC) store_val<SRC>(out_val, it.out_off + my, bits[j]);
+                if constexpr (!ARC) {
+                    if (out_val) store_val<SRC>(out_val, it.out_off + my, bits[j]);
+                }
             }
             if constexpr (ARC) {
                 if (valid) out_slot[it.slot_off + i] = sel ? (int32_t)my : -1;
             } else {
                 if (zero_x && valid) {
-                    if constexpr (SRC == 1) static_cast<float*>(zero_x)[it.key_off + i] = sel ? 0.f : __uint_as_float(bits[j]);
-                    else if constexpr (SRC == 2) static_cast<uint16_t*>(zero_x)[it.key_off + i] = sel ? (uint16_t)0 : (uint16_t)(bits[j] >> 16);
+                    if constexpr (SRC == 1 || SRC == 3) static_cast<float*>(zero_x)[it.key_off + i] = sel ? 0.f : __uint_as_float(bits[j]);
+                    else if constexpr (SRC == 2 || SRC == 4) static_cast<uint16_t*>(zero_x)[it.key_off + i] = sel ? (uint16_t)0 : (uint16_t)(bits[j] >> 16);
                 }
             }
             run_eq += popc64(beq);

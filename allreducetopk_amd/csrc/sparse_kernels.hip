@@ -31,46 +31,6 @@ struct SparseBatch {
 
 
 
-// ---- RandK index source: keyed Feistel permutation of [0, 2^bits), cycle-walked to [0, n)
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352du;
-    x ^= x >> 15; x *= 0x846ca68bu;
-    x ^= x >> 16;
-    return x;
-}
-
-__device__ __forceinline__ uint32_t feistel(uint32_t v, int half, uint32_t hmask, uint64_t key) {
-    uint32_t L = v >> half, R = v & hmask;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t f = mix32(R ^ (uint32_t)(key >> (r * 8)) ^ (uint32_t)(key >> 32) * (r + 1)) & hmask;
-        const uint32_t nl = R;
-        R = L ^ f;
-        L = nl;
-    }
-    return (L << half) | R;
-}
-
-__global__ void __launch_bounds__(256) k_randk(SparseBatch b, uint64_t seed, int32_t* __restrict__ idx) {
-    const int t = blockIdx.y;
-    const int64_t n = b.n[t], k = b.k[t];
-    int bits = 2;
-    while ((1ll << bits) < n) ++bits;
-    if (bits & 1) ++bits;  // balanced halves
-    const int half = bits / 2;
-    const uint32_t hmask = (1u << half) - 1u;
-    const uint64_t key = seed * 0x9E3779B97F4A7C15ull + (uint64_t)(t + 1) * 0xD1B54A32D192ED03ull;
-    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
-        uint32_t v = (uint32_t)j;
-        // cycle walking: the orbit of j returns below n; bounded for safety
-        for (int it = 0; it < 4096; ++it) {
-            v = feistel(v, half, hmask, key);
-            if (v < (uint32_t)n) break;
-        }
-        idx[b.koff[t] + j] = (int32_t)v;
-    }
-}
-
 template <typename T>
 __global__ void __launch_bounds__(256) k_gather(SparseBatch b, const T* __restrict__ x,
                                                 const int32_t* __restrict__ idx,
@@ -120,11 +80,12 @@ __global__ void __launch_bounds__(256) k_scatter(SparseBatch b, T* __restrict__ 
     }
 }
 
-// TopK's first payload (rank 0) into the bucket, zero fill included: each block composes a
-// 4096-element chunk of one tensor in LDS (zeros, then 0 + v at the payload's indices that
-// fall in the chunk) and writes it whole.  The payload's indices are ascending per tensor
-// (arctopk_topk_select), so the chunk's slice of them is found by two 64-way searches.
-// Replaces the bucket memset + a scattered read-modify-write pass.
+// TopK's first payload (rank 0) -- or RandK's all-reduced payload (DIV: v / ws) -- into the
+// bucket, zero fill included: each block composes a 4096-element chunk of one tensor in LDS
+// (zeros, then the values at the payload's indices that fall in the chunk) and writes it whole.
+// The payload's indices are ascending per tensor (arctopk_topk_select, arctopk_randk_select), so
+// the chunk's slice of them is found by two 64-way searches.  Replaces the bucket memset + a
+// scattered pass.
 constexpr int kDecChunk = 4096;
 
 // first position in a[lo, hi) with a[p] >= target (a ascending), one wave
@@ -146,10 +107,10 @@ __device__ __forceinline__ int64_t wave_lower_bound(const int32_t* __restrict__ 
     return lo + __popcll(__ballot(p < hi && a[p] < target));
 }
 
-template <typename T>
+template <typename T, bool DIV>
 __global__ void __launch_bounds__(256) k_scatter_first(SparseBatch b, T* __restrict__ out,
                                                        const int32_t* __restrict__ idx,
-                                                       const T* __restrict__ vals) {
+                                                       const T* __restrict__ vals, float wsf) {
     using arctopk::from_f;
     using arctopk::to_f;
     __shared__ T chunk[kDecChunk];
@@ -168,8 +129,8 @@ __global__ void __launch_bounds__(256) k_scatter_first(SparseBatch b, T* __restr
     }
     for (int e = threadIdx.x; e < kDecChunk; e += 256) chunk[e] = from_f<T>(0.f);
     __syncthreads();
-    for (int64_t j = s_lb[0] + threadIdx.x; j < s_lb[1]; j += 256)
-        chunk[it[j] - c0] = from_f<T>(0.f + to_f(vt[j]));
+    for (int64_t j = s_lb[0] + threadIdx.x; j < s_lb[1]; j += 256)  // TopK: 0 + v; RandK: v / ws
+        chunk[it[j] - c0] = DIV ? from_f<T>(__fdiv_rn(to_f(vt[j]), wsf)) : from_f<T>(0.f + to_f(vt[j]));
     __syncthreads();
     T* o = out + b.off[t] + c0;
     for (int64_t e = threadIdx.x; e < c1 - c0; e += 256) o[e] = chunk[e];
@@ -277,18 +238,47 @@ extern "C" int arctopk_topk_select(const void* x, int32_t nt, const int64_t* off
     return 0;
 }
 
-extern "C" int arctopk_randk_indices(int32_t nt, const int64_t* numels, const int64_t* ks,
-                                     const int64_t* k_off, uint64_t seed, int32_t* idx, void* stream) {
-    if (!numels || !ks || !k_off || !idx || nt < 1) return ARCTOPK_EINVAL;
-    for (int32_t first = 0; first < nt; first += kB) {
-        SparseBatch b;
-        int64_t maxn, maxk;
-        const int cnt = std::min<int32_t>(kB, nt - first);
-        int e = fill_batch(b, first, cnt, nullptr, numels, ks, k_off, maxn, maxk);
-        if (e) return e;
-        hipLaunchKernelGGL(k_randk, dim3(grid_for(maxk, 2048), cnt), dim3(256), 0,
-                           (hipStream_t)stream, b, seed + (uint64_t)first, idx);
-        e = (int)hipGetLastError();
+// RandK's per-tensor key seed: splitmix64 of the call's seed and the tensor's place in the bucket
+static uint32_t rk_tensor_seed(uint64_t seed, int32_t t) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(t + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)(z ^ (z >> 31));
+}
+
+extern "C" int arctopk_randk_select(const void* x, int32_t nt, const int64_t* offsets, const int64_t* numels,
+                                    const int64_t* ks, const int64_t* k_off, uint64_t seed, int32_t* idx,
+                                    void* vals, void* workspace, int32_t dtype, int32_t zero_selected,
+                                    void* stream) {
+    if (!numels || !ks || !k_off || !idx || !workspace || nt < 1) return ARCTOPK_EINVAL;
+    if (x ? (!offsets || !vals) : (vals != nullptr || zero_selected)) return ARCTOPK_EINVAL;
+    if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
+    for (int32_t j = 0; j < nt; ++j)
+        if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j])
+            return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    arctopk::MWorkspace* ws = (arctopk::MWorkspace*)workspace;
+    const int64_t cap_total = topk_cap_total(nt, numels);
+    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
+        arctopk::MBatch b;
+        b.cnt = std::min<int32_t>(arctopk::kMB, nt - first);
+        int64_t maxn = 0, cap = 0;
+        for (int i = 0; i < b.cnt; ++i) {
+            const int j = first + i;
+            arctopk::MItem& it = b.it[i];
+            it.key_off = x ? offsets[j] : 0;
+            it.n = numels[j];
+            it.k = ks[j];
+            it.out_off = k_off[j];
+            it.slot_off = 0;
+            arctopk::ms_item_geometry(it);
+            it.hseed = rk_tensor_seed(seed, j);
+            it.cand_off = cap;
+            cap += it.cand_cap;
+            maxn = std::max(maxn, numels[j]);
+        }
+        int e = arctopk::ms_select(b, maxn, nullptr, x, dtype == ARCTOPK_BF16, false, ws, cap_total, idx, vals,
+                                   nullptr, zero_selected ? const_cast<void*>(x) : nullptr, st, true);
         if (e) return e;
     }
     return 0;
@@ -366,8 +356,8 @@ int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, c
                     const int64_t* k_off, int64_t packed_len, const int32_t* idx, const T* vals,
                     int32_t nranks, int32_t world_size, int32_t accumulate, T* gerr, float decay,
                     hipStream_t st) {
-    // TopK (accumulate, ascending indices per tensor): rank 0's payload writes the whole
-    // bucket, zeros included (k_scatter_first); the tensors tile the bucket in order
+    // TopK (accumulate 1) and RandK with ascending indices (accumulate 2): the first payload
+    // writes the whole bucket, zeros included (k_scatter_first); the tensors tile the bucket in order
     bool tiled = accumulate != 0;
     for (int32_t i = 0; tiled && i < nt; ++i) {
         const int64_t end = i + 1 < nt ? offsets[i + 1] : numel;
@@ -387,11 +377,15 @@ int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, c
             int e = fill_batch(b, first, cnt, offsets, numels.data(), ks, k_off, maxn, maxk);
             if (e) return e;
             const dim3 grid((unsigned)((maxn + kDecChunk - 1) / kDecChunk), cnt);
-            hipLaunchKernelGGL(k_scatter_first<T>, grid, dim3(256), 0, st, b, out, idx, vals);
+            if (accumulate == 2)
+                hipLaunchKernelGGL((k_scatter_first<T, true>), grid, dim3(256), 0, st, b, out, idx, vals,
+                                   (float)world_size);
+            else
+                hipLaunchKernelGGL((k_scatter_first<T, false>), grid, dim3(256), 0, st, b, out, idx, vals, 1.0f);
         }
     }
     const float wsf = (float)world_size;
-    const int nr = accumulate ? nranks : 1;
+    const int nr = accumulate == 1 ? nranks : 1;
     for (int q = tiled ? 1 : 0; q < nr; ++q) {
         for (int32_t first = 0; first < nt; first += kB) {
             SparseBatch b;
@@ -402,16 +396,16 @@ int sparse_decode_t(T* out, int64_t numel, int32_t nt, const int64_t* offsets, c
             dim3 grid(grid_for(maxk, 2048), cnt);
             const int32_t* iq = idx + (int64_t)q * packed_len;
             const T* vq = vals + (int64_t)q * packed_len;
-            if (accumulate && q > 0)
+            if (accumulate == 1 && q > 0)
                 hipLaunchKernelGGL((k_scatter<T, 1>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
-            else if (accumulate)
+            else if (accumulate == 1)
                 hipLaunchKernelGGL((k_scatter<T, 2>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
             else
                 hipLaunchKernelGGL((k_scatter<T, 0>), grid, dim3(256), 0, st, b, out, iq, vq, wsf);
         }
     }
     // TopK's out /= ws (sparse_hook.py:293) is the identity at ws = 1 (x / 1 == x for every x)
-    const bool div = accumulate && world_size > 1;
+    const bool div = accumulate == 1 && world_size > 1;
     if (div || gerr) {
         hipLaunchKernelGGL(k_div_gE<T>, dim3(grid_for(numel, 8192)), dim3(256), 0, st, out, gerr,
                            numel, wsf, div ? 1 : 0, decay);
@@ -426,7 +420,7 @@ extern "C" int arctopk_sparse_decode(void* out, int64_t numel, int32_t nt, const
                                      int32_t world_size, int32_t accumulate, void* gerr,
                                      float decay, int32_t dtype, void* stream) {
     if (!out || !offsets || !ks || !k_off || !idx || !vals || nt < 1 || nranks < 1 ||
-        world_size < 1 || numel < 0)
+        world_size < 1 || numel < 0 || accumulate < 0 || accumulate > 2)
         return ARCTOPK_EINVAL;
     if (dtype != ARCTOPK_F32 && dtype != ARCTOPK_BF16) return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;

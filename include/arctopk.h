@@ -389,13 +389,22 @@ int arctopk_topk_select(const void* x, int32_t ntensors, const int64_t* offsets,
                         int32_t zero_selected, void* stream);
 
 /*
- * RandK index source, device-side: idx[k_off[i] + j] = pi_i(j) for j < k, where pi_i is
- * a keyed pseudo-random permutation of [0, numel_i) (4-round Feistel network with cycle
- * walking, keyed by (seed, i)).  The k indices are distinct.  This is the performance
- * mode; the parity mode draws torch.randperm on the host (sparse_hook.py:20).
+ * RandK, device-side index source (the performance mode; the parity mode draws torch.randperm
+ * on the host, sparse_hook.py:20): tensor i's k indices are those of its k largest keys
+ * key(j) = rk(s_i, j), a keyed bijection of the index j (two xorshift-multiply rounds; s_i =
+ * splitmix64(seed + 0x9E3779B97F4A7C15 * (i + 1)) truncated to 32 bits), so the keys are
+ * distinct and the subset is a uniformly random k-subset of [0, numel_i).  They are selected by
+ * the same exact multi-block radix select as arctopk_topk_select and written ASCENDING
+ * (idx[k_off[i] ..]), so every later pass streams the tensor in order.  x != NULL: also
+ * vals = x[offsets[i] + idx] and (zero_selected) x written back with those entries zeroed in
+ * the same pass (EF14's residual, sparse_hook.py:104, x = E after arctopk_ef14_fold); x = NULL:
+ * indices only (offsets / vals NULL, zero_selected 0).  workspace: arctopk_sparse_workspace_bytes.
+ * Replaces: torch.randperm(numel, device=...)[:k] + tensor[indices] (sparse_hook.py:20-22).
  */
-int arctopk_randk_indices(int32_t ntensors, const int64_t* numels, const int64_t* ks,
-                          const int64_t* k_off, uint64_t seed, int32_t* idx, void* stream);
+int arctopk_randk_select(const void* x, int32_t ntensors, const int64_t* offsets,
+                         const int64_t* numels, const int64_t* ks, const int64_t* k_off,
+                         uint64_t seed, int32_t* idx, void* vals, void* workspace, int32_t dtype,
+                         int32_t zero_selected, void* stream);
 
 /* Gather vals[k_off[i] + j] = x[offsets[i] + idx[k_off[i] + j]]  (sparse_hook.py:22). */
 int arctopk_sparse_gather(const void* x, int32_t ntensors, const int64_t* offsets,
@@ -415,6 +424,8 @@ int arctopk_sparse_residual(void* E, int32_t ntensors, const int64_t* offsets,
 /*
  * Decode into `out` (every element written):
  *   accumulate = 0 (RandK): out = 0; out[off + idx[j]] = vals[j] / world_size     (:273-278)
+ *   accumulate = 2 (RandK, each tensor's idx ascending: arctopk_randk_select): the same, as one
+ *                           pass of whole chunks (zeros and values composed in LDS)
  *   accumulate = 1 (TopK) : out = 0; for rank q = 0..nranks-1 in order:
  *                           out[off + idx_q[j]] += vals_q[j]; then out /= world_size (:285-292)
  * `vals`/`idx` hold nranks consecutive payloads of packed_len entries each.

@@ -53,6 +53,42 @@ def randk_indices(numel: int, k: int, g: torch.Generator) -> torch.Tensor:
     return torch.randperm(numel, generator=g)[:k].to(torch.int32)
 
 
+_M32 = 0xFFFFFFFF
+
+
+def _rk_mix(h):  # numpy uint64 arrays holding 32-bit values
+    import numpy as np
+    h = h ^ (h >> np.uint64(16))
+    h = (h * np.uint64(0x7FEB352D)) & np.uint64(_M32)
+    h = h ^ (h >> np.uint64(15))
+    h = (h * np.uint64(0x846CA68B)) & np.uint64(_M32)
+    return h ^ (h >> np.uint64(16))
+
+
+def randk_hash_seed(seed: int, t: int) -> int:
+    """The tensor key seed of the device RandK draw (sparse_kernels.hip rk_tensor_seed):
+    splitmix64(seed + golden * (t + 1)), low 32 bits."""
+    m = (1 << 64) - 1
+    z = (seed + 0x9E3779B97F4A7C15 * (t + 1)) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return (z ^ (z >> 31)) & _M32
+
+
+def randk_hash_indices(numel: int, k: int, seed: int, t: int) -> torch.Tensor:
+    """The device RandK index rule (index_source="hash", the performance mode -- not the
+    reference's torch.randperm draw, sparse_hook.py:20): the indices of the k largest keys
+    rk(s, j) = mix(mix(j ^ s) + 0x9E3779B9 * (s | 1)) over j < numel, ascending.  mix is a
+    bijection on 32 bits, so the keys are distinct and the subset is a uniform k-subset."""
+    import numpy as np
+    s = np.uint64(randk_hash_seed(seed, t))
+    j = np.arange(numel, dtype=np.uint64)
+    inner = _rk_mix(j ^ s)
+    key = _rk_mix((inner + np.uint64((0x9E3779B9 * (int(s) | 1)) & _M32)) & np.uint64(_M32))
+    top = np.argpartition(-key.astype(np.int64), k - 1)[:k] if k < numel else np.arange(numel)
+    return torch.from_numpy(np.sort(top).astype(np.int32))
+
+
 def encode(G, E, ef):
     X = G.clone()
     if E is not None:

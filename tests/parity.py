@@ -84,3 +84,21 @@ def assert_close_rel(a: torch.Tensor, b: torch.Tensor, rtol: float, what: str):
     floor = rtol * b.abs().max().clamp_min(1e-30)
     err = (a - b).abs() - (rtol * b.abs() + floor)
     assert (err <= 0).all(), f"{what}: worst excess {err.max().item():.3e} (rtol {rtol})"
+
+
+def device_randk_hash(numels, ks, seed: int, device):
+    """The device RandK draw (arctopk_randk_select, indices only) as per-tensor int32 CPU
+    tensors, ascending."""
+    from allreducetopk_amd import _native as N
+    kof = [sum(ks[:i]) for i in range(len(ks))]
+    nb = int(N.lib().arctopk_sparse_workspace_bytes(len(numels), N.i64_array(numels)))
+    assert nb > 0
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    buf = torch.empty(sum(ks), dtype=torch.int32, device=device)
+    N.check(N.lib().arctopk_randk_select(None, len(ks), None, N.i64_array(numels), N.i64_array(ks),
+                                         N.i64_array(kof), int(seed), buf.data_ptr(), None,
+                                         ws.data_ptr(), N.DTYPE_CODE[torch.float32], 0,
+                                         torch.cuda.current_stream(device).cuda_stream),
+            "arctopk_randk_select")
+    flat = buf.cpu()
+    return [flat[o:o + k] for o, k in zip(kof, ks)]

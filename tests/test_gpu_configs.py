@@ -37,7 +37,7 @@ from allreducetopk_amd.comm_hooks.group_topk_hook_no_reshape import GroupTopKSta
 from workloads import WORKLOADS, ddp_buckets, resnet18_cifar_shapes, resnet50_cifar_shapes
 from oracle import arctopk as A
 from oracle import sparse as S
-from parity import assert_bitwise, check_rows_tie_aware, ensure_group
+from parity import assert_bitwise, check_rows_tie_aware, device_randk_hash, ensure_group
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -327,19 +327,13 @@ def test_resnet50_mix_randk():
     rng = torch.Generator().manual_seed(9)
     numels = [bucket_numel([s]) for s in RESNET50]
     ks = [max(1, int(x * 0.2)) for x in numels]
-    kof = [sum(ks[:i]) for i in range(len(ks))]
     E = None
     for it in range(3):
         G = _randn(n, 1300 + it)
         out = sparse_hook.sparse_hook_sync(st, SyntheticBucket(G.to(DEV), RESNET50)).wait()
         torch.cuda.synchronize()
         seed = int(torch.randint(0, 1_000_000_000, (1,), generator=rng).item())
-        buf = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
-        N.check(N.lib().arctopk_randk_indices(len(ks), N.i64_array(numels), N.i64_array(ks),
-                                              N.i64_array(kof), seed, buf.data_ptr(),
-                                              torch.cuda.current_stream().cuda_stream), "randk")
-        flat = buf.cpu()
-        idx = [flat[o:o + k] for o, k in zip(kof, ks)]
+        idx = device_randk_hash(numels, ks, seed, DEV)
         res = S.simulate_step([G], [E], None, RESNET50, 0.2, "ef14", True, None,
                               indices_override=[idx])
         assert_bitwise(out, res["out"], f"it{it} out")

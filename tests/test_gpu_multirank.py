@@ -81,16 +81,10 @@ def _worker(rank, ws, port, td, ef, kind):
             seed = None
             if kind == "randk":
                 seed = int(torch.randint(0, 1_000_000_000, (1,), generator=rng).item())
-                from allreducetopk_amd import _native as N
+                from parity import device_randk_hash
                 numels = [int(torch.Size(s).numel()) for s in MIX]
                 ks = [max(1, int(x * 0.2)) for x in numels]
-                kof = [sum(ks[:i]) for i in range(len(ks))]
-                buf = torch.empty(sum(ks), dtype=torch.int32, device=dev)
-                N.check(N.lib().arctopk_randk_indices(len(ks), N.i64_array(numels), N.i64_array(ks),
-                                                      N.i64_array(kof), seed, buf.data_ptr(),
-                                                      torch.cuda.current_stream().cuda_stream), "r")
-                flat = buf.cpu()
-                idx = [[flat[o:o + k] for o, k in zip(kof, ks)]] * ws
+                idx = [device_randk_hash(numels, ks, seed, dev)] * ws
             res = S.simulate_step(allg, [None] * ws if (first or Es is None) else Es, gE, MIX, 0.2,
                                   ef, kind == "randk", seed, indices_override=idx)
         assert torch.equal(out.cpu(), res["out"]), f"it{it} rank{rank} output"

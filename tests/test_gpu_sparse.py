@@ -7,7 +7,7 @@ from allreducetopk_amd.bucket import SyntheticBucket, bucket_numel
 from allreducetopk_amd.comm_hooks import sparse_hook, sparse_hook_c4
 from golden_io import Golden, case_names
 from oracle import sparse as S
-from parity import assert_bitwise, check_rows_tie_aware, ensure_group
+from parity import assert_bitwise, check_rows_tie_aware, device_randk_hash, ensure_group
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -127,6 +127,42 @@ def test_topk_select_degenerate_large(case):
         assert torch.equal(i[:k], torch.arange(k))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("zero", [0, 1])
+def test_randk_select_kernel_vs_restatement(dtype, zero):
+    """arctopk_randk_select against the restated index rule (oracle randk_hash_indices):
+    bit-exact ascending indices per tensor, gathered values, and (zero_selected) x with
+    exactly those entries zeroed -- over tensors from n = 1 and k = n to a multi-range 3M
+    tensor, more tensors than one launch batch."""
+    L = N.lib()
+    g = torch.Generator().manual_seed(21)
+    numels = [1, 7, 64, 1000, 4096, 65_537, 3_000_000] + [300 + 37 * i for i in range(40)]
+    ks = [1, 7, 13, 1, 4096, 13_107, 600_000] + [max(1, (300 + 37 * i) // 5) for i in range(40)]
+    offs = [sum(numels[:i]) for i in range(len(numels))]
+    kof = [sum(ks[:i]) for i in range(len(ks))]
+    x = torch.randn(sum(numels), generator=g).to(dtype)
+    xd = x.to(DEV)
+    idx = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
+    vals = torch.empty(sum(ks), dtype=dtype, device=DEV)
+    ws = torch.empty(int(L.arctopk_sparse_workspace_bytes(len(numels), N.i64_array(numels))),
+                     dtype=torch.uint8, device=DEV)
+    seed = 123_456_789
+    N.check(L.arctopk_randk_select(xd.data_ptr(), len(numels), N.i64_array(offs), N.i64_array(numels),
+                                   N.i64_array(ks), N.i64_array(kof), seed, idx.data_ptr(),
+                                   vals.data_ptr(), ws.data_ptr(), N.DTYPE_CODE[dtype], zero,
+                                   torch.cuda.current_stream().cuda_stream), "randk_select")
+    torch.cuda.synchronize()
+    i, v, xo = idx.cpu().long(), vals.cpu(), xd.cpu()
+    expect_x = x.clone()
+    for t, (n, k, o, ko) in enumerate(zip(numels, ks, offs, kof)):
+        ref = S.randk_hash_indices(n, k, seed, t).long()
+        assert torch.equal(i[ko:ko + k], ref), f"tensor {t} (n={n}, k={k}) indices"
+        assert torch.equal(v[ko:ko + k], x[o + ref]), f"tensor {t} values"
+        if zero:
+            expect_x[o + ref] = 0
+    assert_bitwise(xo, expect_x, "x after the select")
+
+
 @pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
 @pytest.mark.parametrize("source", ["torch", "host", "hash"])
 def test_randk_hook_vs_oracle(ef, source):
@@ -152,15 +188,9 @@ def test_randk_hook_vs_oracle(ef, source):
             torch.manual_seed(seed)
             idx = [torch.randperm(n)[:k] for n, k in zip(numels, ks)]
         else:
-            kof = [sum(ks[:i]) for i in range(len(ks))]
-            buf = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
-            N.check(N.lib().arctopk_randk_indices(len(ks), N.i64_array(numels), N.i64_array(ks),
-                                                  N.i64_array(kof), seed, buf.data_ptr(),
-                                                  torch.cuda.current_stream().cuda_stream), "randk")
-            flat = buf.cpu()
-            idx = [flat[o:o + k] for o, k in zip(kof, ks)]
-            for t, n in zip(idx, numels):
-                assert t.min() >= 0 and t.max() < n and torch.unique(t).numel() == t.numel()
+            idx = device_randk_hash(numels, ks, seed, DEV)
+            for t, (n, k) in enumerate(zip(numels, ks)):  # the device draw is the restated rule
+                assert torch.equal(idx[t], S.randk_hash_indices(n, k, seed, t)), f"tensor {t} draw"
         res = S.simulate_step([G], [E if not (ef == "ef14" and E is None) else None], gE, SHAPES,
                               0.2, ef, True, None, indices_override=[idx])
         assert_bitwise(out, res["out"], f"it{it} out")

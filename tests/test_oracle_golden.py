@@ -221,3 +221,24 @@ def test_large_batch_errors_match_reference():
     assert (type(ei.value).__name__, str(ei.value), st.iter) == (
         cases["sparse_iter0"]["raises"], cases["sparse_iter0"]["message"], cases["sparse_iter0"]["iter_after"])
     assert cases["sparse_c4_compressed"]["raises"] == "AttributeError"
+
+
+def test_randk_hash_rule_is_a_uniform_subset():
+    """The device RandK index rule (performance mode) as restated in the oracle: k distinct
+    ascending indices per draw, and over many seeds every index is drawn k/n of the time
+    (chi-square over 2000 draws of 10 of 50) -- the property torch.randperm(n)[:k] has."""
+    import numpy as np
+    from oracle import sparse as S
+    n, k, draws = 50, 10, 2000
+    counts = np.zeros(n)
+    for s in range(draws):
+        idx = S.randk_hash_indices(n, k, 1000 + s, s % 3).numpy()
+        assert len(idx) == k and np.all(np.diff(idx) > 0) and idx.min() >= 0 and idx.max() < n
+        counts[idx] += 1
+    exp = draws * k / n
+    chi2 = float(((counts - exp) ** 2 / exp).sum())
+    assert chi2 < 90, chi2  # 49 dof: p < 1e-3 above ~85
+    assert np.array_equal(S.randk_hash_indices(7, 7, 5, 0).numpy(), np.arange(7))
+    # seeds differ per tensor of the bucket
+    assert not np.array_equal(S.randk_hash_indices(1000, 100, 5, 0).numpy(),
+                              S.randk_hash_indices(1000, 100, 5, 1).numpy())
