@@ -19,6 +19,7 @@ LIB_PATH = LIB_OVERRIDE or os.path.join(PKG, "lib", "libarctopk.so")
 
 EF_NONE, EF14, EF21 = 0, 1, 2
 EF_CODE = {"noef": EF_NONE, "ef14": EF14, "ef21": EF21}
+EINVAL = 1001  # ARCTOPK_EINVAL
 SEG_RAW, SEG_SKETCH = 0, 1
 F32 = 0
 BF16 = 1
@@ -81,7 +82,9 @@ _SIGS = {
     "arctopk_exchange_step": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                         c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
-                                        c_void_p, c_void_p]),
+                                        c_void_p, c_void_p, c_void_p]),
+    "arctopk_exchange_trail": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                         c_uint64, c_void_p, c_void_p]),
     "arctopk_exchange_finish": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "arctopk_row_energy": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "arctopk_pack": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,

@@ -485,6 +485,14 @@ class GroupTopKState(HookState):
             raise ValueError("ARCTOPK_SELECT_STREAMS must be 'auto', 'on' or 'off'")
         self.select_stream_bytes = int(float(os.environ.get("ARCTOPK_SELECT_STREAM_MIB", "64")) * (1 << 20))
         self.select_stream_min_buckets = int(os.environ.get("ARCTOPK_SELECT_STREAM_MIN_BUCKETS", "4"))
+        # Trailing steps: at world size 1, a bucket of at most
+        # `trail_bytes` whose tensors all take single-block selects (ResNet-18's and ResNet-50's
+        # first DDP buckets: the fc layer and a few BatchNorm vectors) enqueues nothing; the next
+        # bucket's encode and compact launches carry its encode tiles and selects, so it costs no
+        # launch of its own.  0 disables.  Results are the same bits either way.
+        self.trail_bytes = int(float(os.environ.get("ARCTOPK_TRAIL_MIB", "2")) * (1 << 20))
+        self._trail = None  # the pending entry (in _x_pend) of a recorded trailing step
+        self.trail_calls = 0
         self._sel_streams: Dict[int, List[torch.cuda.Stream]] = {}
         self._sel_turn = 0
         self._sel_small = 0        # select-stream-sized buckets hooked so far in this backward
@@ -596,7 +604,10 @@ class GroupTopKState(HookState):
         complete their Futures: all of them, or up to and including `upto`'s.  The hook does
         this itself in later calls; a Python wait()/value() on such a Future does it too."""
         while self._x_pend:
-            plan, fut, marks, t, sid, _keep = self._x_pend.pop(0)
+            e_ = self._x_pend.pop(0)
+            plan, fut, marks, t, sid, _keep = e_
+            if e_ is self._trail:  # (a trailing step: enqueued, then decoded, by the finish)
+                self._trail = None
             N.check(N.lib().arctopk_exchange_finish(plan.handle, sid, marks), "arctopk_exchange_finish")
             if fut is None:  # a group of a bucket: its last group's entry holds the Future
                 continue
@@ -1094,6 +1105,32 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         # one collective latency, so "auto" groups only the buckets whose all-reduce would
         # otherwise leave the wire idle: the first after the pipeline drained (nothing in flight)
         # and the backward's last (its decode is the drain).
+        # a small bucket of single-block selects, with a bucket after it in this backward: a
+        # trailing step, carried by the next step's launches (arctopk_exchange_trail)
+        if (not comms and defer and marks is None and device_v and state.trail_bytes > 0
+                and ef != N.EF21 and state._trail is None
+                and total * input_tensor.element_size() <= state.trail_bytes):
+            rc = L.arctopk_exchange_trail(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
+                                          int(err_in), int(draw), seed, None, sid)
+            if rc == 0:
+                fut = ExchangeFuture()
+                fut._arctopk_state = state
+                state._trail = (plan, fut, None, input_tensor, sid, (err, gerr))
+                pend.append(state._trail)
+                state.trail_calls += 1
+                state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
+                state.maybe_increase_iter(bucket)
+                _ht("trail")
+                return fut
+            if rc != N.EINVAL:
+                N.check(rc, "arctopk_exchange_trail")
+        trail = state._trail
+        if trail is not None and (trail[4] != sid or trail[0] is plan):
+            state.flush_exchange()  # another stream, or the same bucket again: enqueued on its own
+            trail = None
+        if trail is not None:  # not a ride candidate of this call: carried (or enqueued) by it
+            pend.remove(trail)
+            state._trail = None
         units = None
         if (comms and state.async_exchange and marks is None and state.exchange_groups != "off"
                 and (state.exchange_groups == "all" or not pend or bucket.is_last())):
@@ -1157,6 +1194,10 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
             else:
                 u_x, u_e, u_g, u_draw, u_next, u_nseed, u_vptr = x_p, e_p, g_p, draw, nplan, nseed, vptr
             ride = pend.pop(0) if len(pend) >= depth else None
+            u_trail = None
+            if trail is not None and ui == 0:  # deferred once this step returns
+                pend.append(trail)
+                u_trail = trail[0].handle
             fin = pend[:] if not u_defer else []
             if not u_defer:
                 pend.clear()
@@ -1174,7 +1215,8 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                                           ars.cuda_stream if ars is not None else None,
                                           int(u_defer), ride[0].handle if ride is not None else None,
                                           ride[2] if ride is not None else None, fin_plans, fin_marks, nf,
-                                          u_vptr, marks, side.cuda_stream if side is not None else None)
+                                          u_vptr, marks, side.cuda_stream if side is not None else None,
+                                          u_trail)
             if st_:
                 if comms:
                     for c in (sk, pk):

@@ -596,6 +596,44 @@ __global__ void __launch_bounds__(256) k_encode_short(const SegDev* __restrict__
     encode_tile<T, R, EF, ERR_IN, false>(segs, tiles[blockIdx.x - pr.n], G, E, V, sketch, part_buf, keys, lds);
 }
 
+// A trailing step's encode (arctopk_exchange_trail: a small bucket whose codec rides in the next
+// bucket's launches) -- its tile table and buffers; same dtype, r and EF mode as the carrier
+template <typename T>
+struct EncRide {
+    const SegDev* segs;
+    const EncTile* tiles;
+    const T* G;
+    T* E;
+    const T* V;
+    T* sketch;
+    float* part;
+    uint32_t* keys;
+    int32_t n;  // tiles (blocks); 0: none
+};
+// k_encode_short (ROWS false) / k_encode with a trailing step's tiles after the riding pack's
+// chunks (kernels of their own, so the product encode kernels keep their code)
+template <typename T, int R, int EF, bool ERR_IN, bool ROWS>
+__global__ void __launch_bounds__(256) k_encode_carry(const SegDev* __restrict__ segs,
+                                                            const EncTile* __restrict__ tiles, int ntiles,
+                                                            const T* __restrict__ G, T* __restrict__ E,
+                                                            const T* __restrict__ V, T* __restrict__ sketch,
+                                                            float* __restrict__ part_buf,
+                                                            uint32_t* __restrict__ keys, PackRide<T> pr,
+                                                            EncRide<T> er) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if ((int)blockIdx.x < pr.n) {
+        pack_chunk<T, EF>(pr.segs, pr.chunks[blockIdx.x], pr.G, pr.E, pr.rowlist, pr.slotmap, pr.packed,
+                          pr.dfirst, reinterpret_cast<int32_t*>(lds));
+        return;
+    }
+    const int b = (int)blockIdx.x - pr.n;
+    if (b < er.n) {
+        encode_tile<T, R, EF, ERR_IN, ROWS>(er.segs, er.tiles[b], er.G, er.E, er.V, er.sketch, er.part, er.keys, lds);
+        return;
+    }
+    encode_tile<T, R, EF, ERR_IN, ROWS>(segs, tiles[b - er.n], G, E, V, sketch, part_buf, keys, lds);
+}
+
 // ---------------------------------------------------------------------------
 // K2 select
 // ---------------------------------------------------------------------------
@@ -1937,10 +1975,50 @@ __device__ __forceinline__ void decode_chunk(const SegDev* __restrict__ segs, co
                                              const int32_t* __restrict__ slotmap, Scale sc,
                                              T* __restrict__ gE, T* __restrict__ out,
                                              float* __restrict__ dlds);
+// The decode of a bucket that is already zero (fin 3: exchange.cpp zeroed it while its packed
+// values were on the wire, EF14 / noef): only the selected rows are written, with the values
+// decode_chunk writes there (the mean of the all-reduced row, rounded to T); every other element
+// keeps the +0 that decode_chunk would have written.
+template <typename T>
+__device__ __forceinline__ void scatter_chunk(const SegDev* __restrict__ segs, const Chunk ch,
+                                              const T* __restrict__ packed, const int32_t* __restrict__ slotmap,
+                                              T* __restrict__ out, Scale sc) {
+    auto mean4 = [&](float4 v) { return rnd4<T>(sc(v)); };
+    auto mean1 = [&](float v) { return rnd<T>(sc(v)); };
+    const SegDev s = segs[ch.seg];
+    const int m = (int)s.m;
+    const int64_t base = s.offset + ch.row0 * m;
+    const int32_t* sm = slotmap + s.row_off + ch.row0;
+    const T* pk = packed + s.packed_off;
+    if (s.vec && m >= 256) {  // decode_chunk's row path: wave per selected row, float4 streams
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m4 = m >> 2;
+        for (int64_t j = wave; j < ch.nrows; j += 4) {
+            const int32_t slot = sm[j];
+            if (slot < 0) continue;
+            const T* pp = pk + (int64_t)slot * m;
+            T* op = out + base + j * m;
+#pragma unroll 4
+            for (int c = lane; c < m4; c += 64) stq<T, kNtDecode>(op, c, mean4(ldq<T, false>(pp, c)));
+        }
+        return;
+    }
+    // shorter rows: thread per element of the chunk, the selected ones stored
+    const int64_t cnt = ch.nrows * m;
+    for (int64_t e = threadIdx.x; e < cnt; e += 256) {
+        const int row = m == 1 ? (int)e : (int)div32((uint32_t)e, s.magic32);
+        const int32_t slot = sm[row];
+        if (slot >= 0) st1<T>(out + base + e, mean1(to_f(pk[(int64_t)slot * m + (e - (int64_t)row * m)])));
+    }
+}
+
 // chunk c of a ride: its decode, or (world size 1, fin) the fused pack + decode
 template <typename T, int EF>
 __device__ __forceinline__ void ride_chunk(const DecodeRide<T>& d, int c, float* __restrict__ dlds) {
     if constexpr (EF != ARCTOPK_EF21) {
+        if (d.fin == 3) {
+            scatter_chunk<T>(d.segs, d.chunks[c], d.packed, d.slotmap, d.out, d.sc);
+            return;
+        }
         if (d.fin) {
             finalize_chunk<T>(d.segs, d.chunks[c], d.slotmap, d.E, d.out, d.fin, d.sc);
             return;
@@ -1995,6 +2073,34 @@ __global__ void __launch_bounds__(256) k_arc_write_ride(const MBatch* __restrict
     int t, r;
     if (!ms_locate(g, &t, &r)) return;
     ms_write_body<0, true>(*bp, t, r, keys, nullptr, ws, out_idx, nullptr, out_slot, nullptr);
+}
+
+// The compact launch of a batch (arc_compact_range per range) with a trailing step's single-block
+// selects after its range blocks: the latency-bound selects of a small bucket run beside the
+// compact instead of in launches of their own (arctopk_exchange_trail)
+template <typename T>
+struct SelCarry {
+    const SegDev* segs;
+    const int32_t* ids;
+    const T* sketch;
+    int32_t* rowlist;
+    int32_t* slotmap;
+    int32_t n;  // segments (blocks)
+};
+template <typename T>
+__global__ void __launch_bounds__(256) k_arc_compact_carry(const MBatch* __restrict__ bp, const RangeGrid g,
+                                                           const uint32_t* __restrict__ keys, MWorkspace* ws,
+                                                           uint32_t* __restrict__ ckey, SelCarry<T> sc, int R,
+                                                           Scale scale) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    const int nflat = g.first[g.cnt];
+    if ((int)blockIdx.x >= nflat) {
+        select_small_seg<T, kST>(sc.segs, sc.ids[blockIdx.x - nflat], sc.sketch, R, scale, sc.rowlist, sc.slotmap, dyn);
+        return;
+    }
+    int t, r;
+    if (!ms_locate(g, &t, &r)) return;
+    arc_compact_range(bp->it[t], t, r, keys, ws, ckey);
 }
 
 struct KeysGrid {
@@ -3067,17 +3173,39 @@ inline void launch_done(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, 
 // column-split tensors; done: completed by the last of them
 template <typename T, int R>
 int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in, const T* V, T* sk,
-                    uint32_t* keys, hipStream_t st, PackRide<T> pr, hipEvent_t done = nullptr) {
+                    uint32_t* keys, hipStream_t st, PackRide<T> pr, hipEvent_t done = nullptr,
+                    EncRide<T> er = EncRide<T>{}, int er_lds = 0, bool er_short = true) {
     hipEvent_t enc_done = p->n_split == 0 ? done : nullptr;
-    if (p->n_enc > 0 || pr.n > 0) {
+    if (p->n_enc > 0 || pr.n > 0 || er.n > 0) {
         const bool use_e = p->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
         const int nt = use_e ? p->n_enc_e : p->n_enc;
-        dim3 grid(nt + pr.n), block(256);
+        dim3 grid(nt + pr.n + er.n), block(256);
         // (a riding pack chunk stages up to kSmallTileRows rows of its row list in the same LDS)
-        const size_t lds = std::max<size_t>((size_t)p->enc_lds_bytes, pr.n ? (size_t)kSmallTileRows * 4 : 0);
+        const size_t lds = std::max<size_t>(std::max<size_t>((size_t)p->enc_lds_bytes, (size_t)er_lds),
+                                            pr.n ? (size_t)kSmallTileRows * 4 : 0);
         const EncTile* tiles = use_e ? p->d_enc_e : p->d_enc;
         float* pb = p->d_part;
-        if (p->enc_short) {  // no wave-per-row tile: the lean kernel
+        if (er.n > 0) {  // a trailing step's tiles too: the lean kernel only if both tables are short
+            if (p->enc_short && er_short) {
+                if (ef == ARCTOPK_EF_NONE)
+                    launch_done(&k_encode_carry<T, R, ARCTOPK_EF_NONE, false, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr, er);
+                else if (ef == ARCTOPK_EF14 && err_in)
+                    launch_done(&k_encode_carry<T, R, ARCTOPK_EF14, true, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr, er);
+                else if (ef == ARCTOPK_EF14)
+                    launch_done(&k_encode_carry<T, R, ARCTOPK_EF14, false, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr, er);
+                else
+                    return ARCTOPK_EINVAL;
+            } else {
+                if (ef == ARCTOPK_EF_NONE)
+                    launch_done(&k_encode_carry<T, R, ARCTOPK_EF_NONE, false, true>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr, er);
+                else if (ef == ARCTOPK_EF14 && err_in)
+                    launch_done(&k_encode_carry<T, R, ARCTOPK_EF14, true, true>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr, er);
+                else if (ef == ARCTOPK_EF14)
+                    launch_done(&k_encode_carry<T, R, ARCTOPK_EF14, false, true>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr, er);
+                else
+                    return ARCTOPK_EINVAL;
+            }
+        } else if (p->enc_short) {  // no wave-per-row tile: the lean kernel
             if (ef == ARCTOPK_EF_NONE)
                 launch_done(&k_encode_short<T, R, ARCTOPK_EF_NONE, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr);
             else if (ef == ARCTOPK_EF14 && err_in)
@@ -3111,22 +3239,43 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
 template <typename T>
 int launch_encode(const arctopk_plan* p, const void* grad, void* err, int ef, int err_in, const void* V,
                   void* sketch, uint32_t* keys, hipStream_t st, PackRide<T> pr = PackRide<T>{},
-                  hipEvent_t done = nullptr) {
+                  hipEvent_t done = nullptr, EncRide<T> er = EncRide<T>{}, int er_lds = 0, bool er_short = true) {
     const T* G = static_cast<const T*>(grad);
     T* E = static_cast<T*>(err);
     const T* Vt = static_cast<const T*>(V);
     T* sk = static_cast<T*>(sketch);
     switch (p->r) {
-        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
-        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
-        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
-        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
-        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
-        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
-        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
-        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done);
+        case 1: return launch_encode_r<T, 1>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
+        case 2: return launch_encode_r<T, 2>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
+        case 3: return launch_encode_r<T, 3>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
+        case 4: return launch_encode_r<T, 4>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
+        case 5: return launch_encode_r<T, 5>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
+        case 6: return launch_encode_r<T, 6>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
+        case 7: return launch_encode_r<T, 7>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
+        case 8: return launch_encode_r<T, 8>(p, G, E, ef, err_in, Vt, sk, keys, st, pr, done, er, er_lds, er_short);
     }
     return ARCTOPK_EINVAL;
+}
+
+// the trailing step carried by plan p's exchange step (p->x_carry), as its encode ride
+template <typename T>
+EncRide<T> make_enc_ride(const arctopk_plan* p, int ef, int err_in, int* lds) {
+    EncRide<T> er{};
+    *lds = 0;
+    const arctopk_plan* c = p->x_carry;
+    if (!c) return er;
+    const bool use_e = c->n_enc_e > 0 && (ef == ARCTOPK_EF21 || (ef == ARCTOPK_EF14 && err_in));
+    er.segs = c->d_segs;
+    er.tiles = use_e ? c->d_enc_e : c->d_enc;
+    er.n = use_e ? c->n_enc_e : c->n_enc;
+    er.G = static_cast<const T*>(c->x_t_bucket);
+    er.E = static_cast<T*>(c->x_t_err);
+    er.V = static_cast<const T*>(c->x_t_V ? c->x_t_V : c->b_V);
+    er.sketch = static_cast<T*>(c->b_sketch);
+    er.part = c->d_part;
+    er.keys = c->any_keyed ? c->d_keys : nullptr;
+    *lds = c->enc_lds_bytes;
+    return er;
 }
 
 Scale make_scale(int32_t ws) {
@@ -3158,6 +3307,7 @@ struct RideArgs {
 };
 // the fused pack + decode of plan rp's deferred step (exchange.cpp sets x_fin at world size 1)
 inline int ride_fin(const arctopk_plan* rp, int32_t ef) {
+    if (rp->x_fin == 3) return ef == ARCTOPK_EF21 ? 0 : 3;
     return rp->x_fin ? (ef == ARCTOPK_EF14 ? 1 : 2) : 0;
 }
 
@@ -3274,7 +3424,19 @@ int launch_select(const arctopk_plan* p, const void* sketch_, int32_t ws, int32_
             hipLaunchKernelGGL((k_arc_keys<T, 1024>), dim3(kg.first[b.cnt]), dim3(1024), 0, st, p->d_segs,
                                p->d_large, bi * kMB, sketch, p->r, make_scale(ws), p->d_keys, p->d_mws, kg,
                                keyed ? 1 : 0);
-        int e = ms_arc_compact(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, st);
+        int e = 0;
+        if (bi == 0 && p->x_carry) {  // the trailing step's selects ride in the compact launch
+            const arctopk_plan* c = p->x_carry;
+            const SelCarry<T> sc{c->d_segs, c->d_small, static_cast<const T*>(c->b_sketch), c->b_rowlist,
+                                 c->b_slotmap, c->n_small};
+            const RangeGrid g = ms_range_grid(b);
+            hipLaunchKernelGGL(k_arc_compact_carry<T>, dim3(g.first[g.cnt] + sc.n), dim3(256), (size_t)c->small_lds,
+                               st, (const MBatch*)(p->d_large_batches + bi), g, (const uint32_t*)p->d_keys, p->d_mws,
+                               reinterpret_cast<uint32_t*>(p->d_mws + 1), sc, (int)p->r, make_scale(1));
+            e = (int)hipGetLastError();
+        } else {
+            e = ms_arc_compact(b, p->d_large_batches + bi, p->d_keys, p->d_mws, p->mws_cap, st);
+        }
         if (e) return e;
         const int nsm = bi == 0 ? p->n_small : 0;
         VDrawJob bj = job;
@@ -3495,7 +3657,10 @@ int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef,
         if (take)
             pr = PackRide<bf16_t>{rp->d_segs, rp->d_pack, static_cast<const bf16_t*>(rp_grad), static_cast<bf16_t*>(rp_err),
                                   rp->b_rowlist, rp->b_slotmap, static_cast<bf16_t*>(rp->b_packed), rp->d_dfirst, rp->n_pack};
-        const int e = launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, keys, st, pr, (hipEvent_t)done);
+        int er_lds = 0;
+        const EncRide<bf16_t> er = make_enc_ride<bf16_t>(p, ef, err_in, &er_lds);
+        const int e = launch_encode<bf16_t>(p, grad, err, ef, err_in, V, sketch, keys, st, pr, (hipEvent_t)done, er,
+                                            er_lds, p->x_carry ? p->x_carry->enc_short != 0 : true);
         if (!e && take) *rode = 1;
         return e;
     }
@@ -3503,7 +3668,10 @@ int encode_keyed(const arctopk_plan* p, const void* grad, void* err, int32_t ef,
     if (take)
         pr = PackRide<float>{rp->d_segs, rp->d_pack, static_cast<const float*>(rp_grad), static_cast<float*>(rp_err),
                              rp->b_rowlist, rp->b_slotmap, static_cast<float*>(rp->b_packed), rp->d_dfirst, rp->n_pack};
-    const int e = launch_encode<float>(p, grad, err, ef, err_in, V, sketch, keys, st, pr, (hipEvent_t)done);
+    int er_lds = 0;
+    const EncRide<float> er = make_enc_ride<float>(p, ef, err_in, &er_lds);
+    const int e = launch_encode<float>(p, grad, err, ef, err_in, V, sketch, keys, st, pr, (hipEvent_t)done, er, er_lds,
+                                       p->x_carry ? p->x_carry->enc_short != 0 : true);
     if (!e && take) *rode = 1;
     return e;
 }

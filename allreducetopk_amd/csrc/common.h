@@ -28,6 +28,10 @@
 #ifndef ARCTOPK_FUSE_MAX_ROWS
 #define ARCTOPK_FUSE_MAX_ROWS 262144   // largest item whose refine runs in the write blocks
 #endif
+#ifndef ARCTOPK_ZERO_AHEAD
+#define ARCTOPK_ZERO_AHEAD 1           // the backward's last exchange step (EF14 / noef) zeroes its bucket
+#endif                                 //   while its packed values are on the wire; its decode then
+                                       //   writes the selected rows only (exchange.cpp)
 #ifndef ARCTOPK_FUSE_CAP
 #define ARCTOPK_FUSE_CAP 8192         // candidates a fused write block stages in LDS (more: swept from L2)
 #endif
@@ -410,8 +414,10 @@ struct arctopk_plan {
     void* x_bucket;                     //   the bucket,
     void* x_gerr;                       //   the global residual (EF21),
     int x_ef, x_ws;                     //   the EF mode and world size of that call
-    int x_fin;                          // world size 1, EF14 / noef: no pack; the decode is the
-                                        //   fused pack + decode from the residual x_err (finalize)
+    int x_fin;                          // 1: world size 1, EF14 / noef: no pack; the decode is the
+                                        //   fused pack + decode from the residual x_err (finalize);
+                                        // 3: the bucket is already zero, the decode writes only the
+                                        //   selected rows (scatter_chunk)
     int x_pack;                         // its pack is deferred too (world size 1): enqueued in the
     void* x_err;                        //   next call's encode launch, or by exchange_finish; the
                                         //   residual it gathers from
@@ -422,6 +428,16 @@ struct arctopk_plan {
                                         //   the sketch all-reduce) when a select stream takes over
     void* x_ev_join;                    // recorded on the select stream after the decode, for the
                                         //   stream that finishes the step to wait on
+    // a trailing step (arctopk_exchange_trail): recorded, not enqueued; the next exchange step
+    // carries its encode tiles and single-block selects in its own launches
+    int x_trail;
+    void* x_t_bucket;
+    void* x_t_err;
+    void* x_t_gerr;
+    const void* x_t_V;
+    int x_t_ef, x_t_err_in;
+    const arctopk_plan* x_carry;        // during an exchange step: the trailing plan its encode and
+                                        //   compact launches carry (encode_keyed, launch_select)
 };
 namespace arctopk {
 // keyed: the call's encode ran in keys mode (encode_keyed; world size 1 only)

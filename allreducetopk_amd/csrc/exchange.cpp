@@ -599,8 +599,54 @@ inline hipStream_t x_stream_of(const arctopk_plan* p, hipStream_t caller) {
 }
 }  // namespace
 
+namespace {
+// a trailing step enqueued on its own (no step carried it): encode + select on `st`, then a
+// deferred world-size-1 step like any other (its decode: the fused finalize, x_fin 1)
+int trail_run(arctopk_plan* c, hipStream_t st) {
+    const void* V = c->x_t_V ? c->x_t_V : c->b_V;
+    int e = arctopk::encode_keyed(c, c->x_t_bucket, c->x_t_err, c->x_t_ef, c->x_t_err_in, V, c->b_sketch, st);
+    if (!e) e = arctopk::select_draw_keyed(c, c->b_sketch, 1, c->b_rowlist, c->b_slotmap, nullptr, 0, nullptr, true, st);
+    if (e) return e;
+    c->x_trail = 0;
+    c->x_deferred = 2;
+    c->x_fin = 1;
+    c->x_bucket = c->x_t_bucket;
+    c->x_err = c->x_t_err;
+    c->x_gerr = c->x_t_gerr;
+    c->x_ef = c->x_t_ef;
+    c->x_ws = 1;
+    c->x_stream = nullptr;
+    return 0;
+}
+}  // namespace
+
+extern "C" int arctopk_exchange_trail(arctopk_plan* p, void* bucket, void* err, void* gerr, int32_t ef,
+                                      int32_t err_in, int32_t draw, uint64_t seed, const void* V, void* stream) {
+    if (!p || !bucket || !p->b_sketch || (ef != ARCTOPK_EF_NONE && ef != ARCTOPK_EF14)) return ARCTOPK_EINVAL;
+    // only a plan another step's launches can carry: single-block selects, short-row / 1-D tiles
+    if (p->n_large_batches > 0 || p->n_small == 0 || p->n_split || p->any_keyed)
+        return ARCTOPK_EINVAL;
+    if (ef == ARCTOPK_EF14 && !err) return ARCTOPK_EINVAL;
+    if (p->x_trail || p->x_deferred) return ARCTOPK_EINVAL;  // the caller finishes a plan's step first
+    if (!V) V = p->b_V;
+    if (draw && p->info.v_len > 0) {
+        if (int e = arctopk_draw_projections(p, seed, const_cast<void*>(V), stream)) return e;
+    }
+    p->x_trail = 1;
+    p->x_t_bucket = bucket;
+    p->x_t_err = err;
+    p->x_t_gerr = gerr;
+    p->x_t_V = V;
+    p->x_t_ef = ef;
+    p->x_t_err_in = err_in;
+    return 0;
+}
+
 extern "C" int arctopk_exchange_finish(arctopk_plan* p, void* stream, void* const* marks) {
     if (!p) return ARCTOPK_EINVAL;
+    if (p->x_trail) {
+        if (int e = trail_run(p, (hipStream_t)stream)) return e;
+    }
     if (!p->x_deferred) return 0;
     hipStream_t cs = (hipStream_t)stream;
     // where the step's select and pack ran (its select stream, or the caller's); `stream` then
@@ -625,9 +671,10 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
                                      void* stream, void* ar_stream, int32_t defer, arctopk_plan* ride,
                                      void* const* ride_marks, arctopk_plan* const* finish,
                                      void* const* const* finish_marks, int32_t nfinish, const void* V,
-                                     void* const* marks, void* sel_stream) {
+                                     void* const* marks, void* sel_stream, arctopk_plan* trail) {
     if (!p || !bucket || !p->b_sketch || !sketch_comm != !packed_comm || nfinish < 0 || (nfinish && !finish))
         return ARCTOPK_EINVAL;
+    if (trail && (trail == p || !trail->x_trail)) return ARCTOPK_EINVAL;
     // a select stream takes the select, pack and decodes off the caller's stream (not with markers:
     // the marker pass times the phases in one stream's order); its packed all-reduce must then go
     // on the all-reduce stream (a communicator's collectives stay on one stream each), and it draws
@@ -650,6 +697,26 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (ht.on) g_ht_calls.fetch_add(1, std::memory_order_relaxed);
     // this bucket's own deferred decode, if a caller never finished it (the hook always does)
     int e = arctopk_exchange_finish(p, stream, nullptr);
+    // the trailing step: carried by this step's encode and compact launches when both plans
+    // qualify, else enqueued on its own now
+    arctopk_plan* carry = nullptr;
+    if (!e && trail) {
+        constexpr int64_t big_rows = ARCTOPK_SEL_BIG_ROWS;
+        const bool fits = !sketch_comm && !marks && trail->device == p->device && trail->dtype == p->dtype &&
+                          trail->r == p->r && trail->x_t_ef == ef && trail->x_t_err_in == err_in &&
+                          ef != ARCTOPK_EF21 && p->n_large_batches > 0 && p->n_split == 0 &&
+                          trail->n_large_batches == 0 && trail->n_small > 0 &&
+                          trail->n_split == 0 && !trail->any_keyed && trail->small_lds <= big_rows * 4 + 16 &&
+                          trail->small_lds <= 48 * 1024 && trail->x_t_bucket != bucket &&
+                          (!err || trail->x_t_err != err);
+        if (fits) carry = trail;
+        else e = trail_run(trail, st);
+    }
+    p->x_carry = carry;
+    struct CarryReset {  // no early return leaves the carry set on the plan
+        arctopk_plan* p;
+        ~CarryReset() { p->x_carry = nullptr; }
+    } carry_reset{p};
     // a step with markers times its own encode: the ride's deferred pack goes first, unmarked
     if (!e && marks && ride) e = pack_now(ride, stream);
     if (!e) e = mark(marks, ARCTOPK_MARK_START, st);
@@ -742,6 +809,18 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk::select_draw_keyed(p, p->b_sketch, ws, p->b_rowlist, p->b_slotmap, next, next_seed,
                                        next ? next->b_V : nullptr, keyed, ss);
     }
+    p->x_carry = nullptr;
+    if (!e && carry) {  // the trailing step was encoded and selected in this step's launches
+        carry->x_trail = 0;
+        carry->x_deferred = 2;
+        carry->x_fin = 1;
+        carry->x_bucket = carry->x_t_bucket;
+        carry->x_err = carry->x_t_err;
+        carry->x_gerr = carry->x_t_gerr;
+        carry->x_ef = carry->x_t_ef;
+        carry->x_ws = 1;
+        carry->x_stream = side ? (void*)ss : nullptr;
+    }
     if (!e) e = mark(marks, ARCTOPK_MARK_SELECT, st);
     if (e) return e;
     ht.lap(3);
@@ -760,6 +839,18 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         e = arctopk::pack_signal(p, bucket, err, ef, p->b_rowlist, p->b_slotmap, p->b_packed, ss,
                                  p->x_ev_packed);
         if (!e) Watchdog::get().watch(sketch_comm, p->x_ev_packed);
+        // The backward's last step: its decode comes after its own packed all-reduce, the end of
+        // the wire's work.  EF14 / noef: the bucket is dead once packed (EF14 packs the residual,
+        // noef the bucket itself, both read by the pack before this), so it is zeroed now, while
+        // the packed values are on the wire, and the decode after the wire writes only the
+        // selected rows (x_fin 3): the same bytes, most of them moved off the drain.  EF21's
+        // decode writes gE to the unselected elements and keeps the whole-bucket decode.
+        if (!e && ARCTOPK_ZERO_AHEAD && !defer && async_ar && ef != ARCTOPK_EF21 && p->n_dec > 0) {
+            const size_t esz = p->dtype == ARCTOPK_BF16 ? 2 : 4;
+            const hipError_t he = hipMemsetAsync(bucket, 0, (size_t)p->info.numel * esz, ss);
+            if (he != hipSuccess) return (int)he;
+            p->x_fin = 3;
+        }
     } else if (!marks && ef != ARCTOPK_EF21) {
         // world size 1 (EF14 / noef): the all-reduce is the identity, so no packed buffer is
         // needed -- the decode (riding in a later select launch, or inline below) takes the
@@ -838,6 +929,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         if ((e = ensure_event(&p->x_ev_dec, hipEventDisableTiming | hipEventReleaseToDevice))) return e;
         e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, ss, p->x_ev_dec);
         if (!e) Watchdog::get().watch(packed_comm, p->x_ev_dec);
+        p->x_fin = 0;
     } else {
         e = arctopk::decode_signal(p, p->b_packed, p->b_slotmap, ws, ef, gerr, bucket, ss, nullptr);
         p->x_fin = 0;

@@ -235,7 +235,7 @@ __device__ inline void ms_arc_digit_local(const uint32_t* __restrict__ hist_t, i
 
 
 // host-side geometry of one item: fills range / nranges / cand_cap (cand_off by caller)
-void ms_item_geometry(MItem& it);
+void ms_item_geometry(MItem& it, int max_ranges = kMMaxRanges);
 // workspace bytes for batches whose candidate capacities sum to <= cap_total
 int64_t ms_workspace_bytes(int64_t cap_total);
 

@@ -18,6 +18,8 @@ namespace {
 constexpr int kW1 = 12;  // first-pass digit width (kMBins = 1 << kW1)
 constexpr int kW2 = 10;  // refinement digit width (12 + 10 + 10 >= 32 key bits)
 constexpr int kCandPerBlock = 2048;     // candidates per block of a refinement pass
+constexpr int kCompactRanges = 4;       // ranges per block of the TopK / RandK compact pass
+constexpr int kCompactStage = 4096;     // candidates a compact block stages in LDS (32 KiB)
 
 
 // Flat grids of the per-range kernels: block x is range r of item t, items back to back
@@ -84,8 +86,11 @@ template <int SRC, int PASS>
 __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __restrict__ keys,
                                                  const void* __restrict__ x, MWorkspace* ws,
                                                  const uint32_t* __restrict__ ckey) {
-    constexpr int W = PASS == 0 ? kW1 : kW2;
-    constexpr int PER = (1 << W) / 256;
+    // RandK hash keys are uniform over 32 bits, so every block finds every first-pass bin
+    // occupied: their first digit is 8 bits (256 bins to merge per block, not 4,096; the k-th
+    // key's bin then holds ~n/256 candidates) and the two refinements 12 bits each (8+12+12)
+    constexpr int W = SRC >= 3 ? (PASS == 0 ? 8 : 12) : (PASS == 0 ? kW1 : kW2);
+    constexpr int PER = (1 << W) >= 256 ? (1 << W) / 256 : 1;
     __shared__ uint32_t h[1 << W];
     __shared__ uint32_t lds[4];
     const int t = blockIdx.y;
@@ -164,158 +169,100 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
     }
 }
 
-// One block per range: count of keys above the first-pass bin, and (candidate mode)
-// append the bin's keys + local indices to the item's candidate list, one counter
-// atomic per block tile (a tile's candidates stay contiguous).
+// kCompactRanges consecutive ranges of one item per block: per range, the count of keys above
+// the first-pass bin; in candidate mode the bin's keys + local indices are staged in LDS and
+// appended to the item's candidate list with ONE counter atomic per block (per full stage): the
+// counter is one memory-side word per item, and appends to it serialise -- one per 4,096-key
+// tile measured ~70 us on a 16 x 4 M-key batch.  Candidate order does not matter (the later
+// passes histogram them and count them by their index's range).
 template <int SRC>
 __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __restrict__ keys,
                                                     const void* __restrict__ x, MWorkspace* ws,
                                                     uint32_t* __restrict__ ckey,
                                                     uint32_t* __restrict__ cidx) {
     __shared__ uint32_t lds[4], s_cnt[4], s_base;
-    int t, r;
-    if (!ms_locate(b, &t, &r)) return;
+    __shared__ uint32_t s_ck[kCompactStage], s_ci[kCompactStage];
+    const int t = blockIdx.y;
     const MItem it = b.it[t];
+    const int ra = (int)blockIdx.x * kCompactRanges;
+    if (ra >= it.nranges) return;  // uniform per block
+    const int rb = min(it.nranges, ra + kCompactRanges);
     const MState s = ws->st[t];
     const uint32_t hi = s.p1 | ~s.m1;  // largest key of the bin
-    const int64_t r0 = (int64_t)r * it.range;
-    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint32_t gt = 0;
-    for (int64_t tile = r0; tile < r1; tile += kMTile) {
-        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
-        uint32_t kv[kPerLane];
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j)
-            kv[j] = item_key<SRC>(it, keys, x, min<int64_t>(wb + j * 64 + lane, r1 - 1));
-        uint32_t nin = 0;
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-            const bool valid = wb + j * 64 + lane < r1;
-            gt += (valid && kv[j] > hi) ? 1u : 0u;
-            if (s.cand) nin += popc64(__ballot(valid && (kv[j] & s.m1) == s.p1));
+    uint32_t staged = 0;  // candidates in the LDS stage (uniform)
+    auto flush = [&]() {  // uniform; the stage -> the item's list, one counter atomic
+        if (threadIdx.x == 0) s_base = atomicAdd(&ws->ncand[t].v, staged);
+        __syncthreads();
+        const uint32_t base = s_base;
+        for (uint32_t q = threadIdx.x; q < staged; q += 256) {
+            ckey[it.cand_off + base + q] = s_ck[q];
+            cidx[it.cand_off + base + q] = s_ci[q];
         }
-        if (s.cand) {  // uniform
-            if (lane == 0) s_cnt[wave] = nin;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-                s_base = tot ? atomicAdd(&ws->ncand[t].v, tot) : 0u;
-            }
-            __syncthreads();
-            uint32_t base = s_base;
+        __syncthreads();  // the stage is rewritten next
+        staged = 0;
+    };
+    for (int r = ra; r < rb; ++r) {
+        const int64_t r0 = (int64_t)r * it.range;
+        const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+        uint32_t gt = 0;
+        for (int64_t tile = r0; tile < r1; tile += kMTile) {
+            const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
+            uint32_t kv[kPerLane];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) base += w < wave ? s_cnt[w] : 0u;
+            for (int j = 0; j < kPerLane; ++j)
+                kv[j] = item_key<SRC>(it, keys, x, min<int64_t>(wb + j * 64 + lane, r1 - 1));
+            uint32_t nin = 0;
 #pragma unroll
             for (int j = 0; j < kPerLane; ++j) {
-                const int64_t i = wb + j * 64 + lane;
-                const bool in = i < r1 && (kv[j] & s.m1) == s.p1;
-                const uint64_t bm = __ballot(in);
-                if (in) {
-                    const uint32_t pos = base + popc64(bm & lt);
-                    ckey[it.cand_off + pos] = kv[j];
-                    cidx[it.cand_off + pos] = (uint32_t)i;
-                }
-                base += popc64(bm);
+                const bool valid = wb + j * 64 + lane < r1;
+                gt += (valid && kv[j] > hi) ? 1u : 0u;
+                if (s.cand) nin += popc64(__ballot(valid && (kv[j] & s.m1) == s.p1));
             }
-            __syncthreads();  // s_cnt / s_base are rewritten by the next tile
+            if (s.cand) {  // uniform
+                if (lane == 0) s_cnt[wave] = nin;
+                __syncthreads();
+                const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+                uint32_t before = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) before += w < wave ? s_cnt[w] : 0u;
+                __syncthreads();  // s_cnt is rewritten by the next tile
+                if (staged + tot > (uint32_t)kCompactStage) flush();
+                uint32_t pos = staged + before;
+#pragma unroll
+                for (int j = 0; j < kPerLane; ++j) {
+                    const int64_t i = wb + j * 64 + lane;
+                    const bool in = i < r1 && (kv[j] & s.m1) == s.p1;
+                    const uint64_t bm = __ballot(in);
+                    if (in) {
+                        const uint32_t q = pos + popc64(bm & lt);
+                        s_ck[q] = kv[j];
+                        s_ci[q] = (uint32_t)i;
+                    }
+                    pos += popc64(bm);
+                }
+                staged += tot;
+                __syncthreads();  // the stage is complete before a flush reads it
+            }
+        }
+        uint32_t total;
+        (void)block_exscan_u32<4>(gt, lds, &total);
+        if (threadIdx.x == 0) {
+            ws->cnt_gt[t][r] = total;
+            ws->cnt_eq[t][r] = 0u;
         }
     }
-    uint32_t total;
-    (void)block_exscan_u32<4>(gt, lds, &total);
-    if (threadIdx.x == 0) {
-        ws->cnt_gt[t][r] = total;
-        ws->cnt_eq[t][r] = 0u;
-    }
+    if (s.cand && staged) flush();
 }
 
-// ARC: one block per range, no atomics: the keys above the first-pass bin are counted and
-// the bin's keys are copied (in index order) into the range's own candidate region;
-// cnt_gt / cnt_cand per range for the refine.
+// ARC: one block per range (arc_compact_range, mselect_dev.h)
 __global__ void __launch_bounds__(256) k_arc_compact(const MBatch* __restrict__ bp, const RangeGrid g,
                                                      const uint32_t* __restrict__ keys, MWorkspace* ws,
                                                      uint32_t* __restrict__ ckey) {
-    __shared__ uint32_t lds[4], s_cnt[4], s_and[4];
     int t, r;
     if (!ms_locate(g, &t, &r)) return;
-    const MItem it = bp->it[t];
-    uint32_t d;  // the first-pass bin (keys above it are selected; its keys are the candidates)
-    {
-        __shared__ uint32_t lds_d[256 + 128];
-        uint32_t acc;
-        ms_arc_digit_local<256>(ws->hist[t], it.k, lds_d, &d, &acc);
-        if (r == 0 && threadIdx.x == 0) {  // the item's state for the refine (next launch)
-            MState g;
-            arc_bin_state(d, &g.prefix, &g.mask, &g.bit);
-            g.cand = 1;
-            g.kk = it.k - (int64_t)acc;
-            g.p1 = g.prefix;
-            g.m1 = g.mask;
-            g.ncand = 0;
-            ws->st[t] = g;
-        }
-    }
-    const int64_t r0 = (int64_t)r * it.range;
-    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint32_t* dst = ckey + it.cand_off + r0;
-    uint32_t gt = 0, run = 0, kor = 0u, kand = ~0u;
-    for (int64_t tile = r0; tile < r1; tile += kMTile) {
-        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
-        uint32_t kv[kPerLane];
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) kv[j] = keys[it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)];
-        uint64_t bm[kPerLane];
-        uint32_t nin = 0;
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-            const bool valid = wb + j * 64 + lane < r1;
-            const uint32_t dj = arc_digit(kv[j]);
-            gt += (valid && dj > d) ? 1u : 0u;
-            bm[j] = __ballot(valid && dj == d);
-            nin += popc64(bm[j]);
-        }
-        if (lane == 0) s_cnt[wave] = nin;
-        __syncthreads();
-        uint32_t base = run, tot = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            base += w < wave ? s_cnt[w] : 0u;
-            tot += s_cnt[w];
-        }
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-            if ((bm[j] >> lane) & 1ull) {
-                dst[base + popc64(bm[j] & lt)] = kv[j];
-                kor |= kv[j];
-                kand &= kv[j];
-            }
-            base += popc64(bm[j]);
-        }
-        run += tot;
-        __syncthreads();  // s_cnt is rewritten by the next tile
-    }
-    // block totals: keys above the bin, OR / AND of the bin's keys (one barrier)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        gt += __shfl_xor(gt, o, 64);
-        kor |= __shfl_xor(kor, o, 64);
-        kand &= __shfl_xor(kand, o, 64);
-    }
-    if (lane == 0) {
-        lds[wave] = gt;
-        s_cnt[wave] = kor;
-        s_and[wave] = kand;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        ws->cnt_gt[t][r] = lds[0] + lds[1] + lds[2] + lds[3];
-        ws->cnt_cand[t][r] = run;
-        ws->cand_or[t][r] = s_cnt[0] | s_cnt[1] | s_cnt[2] | s_cnt[3];
-        ws->cand_and[t][r] = s_and[0] & s_and[1] & s_and[2] & s_and[3];
-    }
+    arc_compact_range(bp->it[t], t, r, keys, ws, ckey);
 }
 
 // Per-range counts of the bin's keys > T and == T (T = the final prefix), added to the
@@ -446,9 +393,10 @@ __global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp
 
 }  // namespace
 
-void ms_item_geometry(MItem& it) {
+void ms_item_geometry(MItem& it, int max_ranges) {
     const int64_t tiles = (it.n + kMTile - 1) / kMTile;
-    const int64_t per = std::max<int64_t>(1, (tiles + kMMaxRanges - 1) / kMMaxRanges);
+    max_ranges = std::max(1, std::min(max_ranges, kMMaxRanges));
+    const int64_t per = std::max<int64_t>(1, (tiles + max_ranges - 1) / max_ranges);
     it.range = (int32_t)(per * kMTile);
     it.nranges = (int32_t)((it.n + it.range - 1) / it.range);
     // candidates: the k-th key's 12-bit bin; a few % of n on gradient-like data, all of
@@ -489,12 +437,15 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
     constexpr int64_t hist_total = ARCTOPK_TOPK_HIST_BLOCKS;  // headline TopK: 387 -> 404 GB/s (512: 399, 2048: 387)
     const int hb = (int)std::max<int64_t>(
         1, std::min<int64_t>(std::min<int64_t>(kMHistBlocks, (maxn + 8191) / 8192), hist_total / cnt));
-    const dim3 gh(hb, cnt), gt(gr, cnt), gflat(total_ranges(b));
+    // the count pass: each block arrives once on the item's one done counter (those arrivals
+    // serialise at the memory side), so a few blocks per item stride over its ranges / candidates
+    const dim3 gh(hb, cnt), gt(std::min(gr, 32), cnt), gflat(total_ranges(b)),
+        gc((gr + kCompactRanges - 1) / kCompactRanges, cnt);
 #define MS_LAUNCH(FF, AR)                                                                              \
     do {                                                                                               \
         if (!AR) hipLaunchKernelGGL(k_ms_init<FF>, dim3(cnt), dim3(256), 0, st, b, ws);                \
         hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
-        hipLaunchKernelGGL(k_ms_compact<FF>, gflat, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);     \
+        hipLaunchKernelGGL(k_ms_compact<FF>, gc, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);        \
         hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
         hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
         hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);          \

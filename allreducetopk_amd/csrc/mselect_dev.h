@@ -148,4 +148,88 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, con
     }
 }
 
+// ARC: one block per range, no atomics: the keys above the first-pass bin are counted and
+// the bin's keys are copied (in index order) into the range's own candidate region;
+// cnt_gt / cnt_cand per range for the refine.
+__device__ inline void arc_compact_range(const MItem it, int t, int r, const uint32_t* __restrict__ keys,
+                                         MWorkspace* ws, uint32_t* __restrict__ ckey) {
+    __shared__ uint32_t lds[4], s_cnt[4], s_and[4];
+    uint32_t d;  // the first-pass bin (keys above it are selected; its keys are the candidates)
+    {
+        __shared__ uint32_t lds_d[256 + 128];
+        uint32_t acc;
+        ms_arc_digit_local<256>(ws->hist[t], it.k, lds_d, &d, &acc);
+        if (r == 0 && threadIdx.x == 0) {  // the item's state for the refine (next launch)
+            MState g;
+            arc_bin_state(d, &g.prefix, &g.mask, &g.bit);
+            g.cand = 1;
+            g.kk = it.k - (int64_t)acc;
+            g.p1 = g.prefix;
+            g.m1 = g.mask;
+            g.ncand = 0;
+            ws->st[t] = g;
+        }
+    }
+    const int64_t r0 = (int64_t)r * it.range;
+    const int64_t r1 = min<int64_t>(it.n, r0 + it.range);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t* dst = ckey + it.cand_off + r0;
+    uint32_t gt = 0, run = 0, kor = 0u, kand = ~0u;
+    for (int64_t tile = r0; tile < r1; tile += kMTile) {
+        const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
+        uint32_t kv[kPerLane];
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) kv[j] = keys[it.key_off + min<int64_t>(wb + j * 64 + lane, r1 - 1)];
+        uint64_t bm[kPerLane];
+        uint32_t nin = 0;
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const bool valid = wb + j * 64 + lane < r1;
+            const uint32_t dj = arc_digit(kv[j]);
+            gt += (valid && dj > d) ? 1u : 0u;
+            bm[j] = __ballot(valid && dj == d);
+            nin += popc64(bm[j]);
+        }
+        if (lane == 0) s_cnt[wave] = nin;
+        __syncthreads();
+        uint32_t base = run, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            base += w < wave ? s_cnt[w] : 0u;
+            tot += s_cnt[w];
+        }
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            if ((bm[j] >> lane) & 1ull) {
+                dst[base + popc64(bm[j] & lt)] = kv[j];
+                kor |= kv[j];
+                kand &= kv[j];
+            }
+            base += popc64(bm[j]);
+        }
+        run += tot;
+        __syncthreads();  // s_cnt is rewritten by the next tile
+    }
+    // block totals: keys above the bin, OR / AND of the bin's keys (one barrier)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        gt += __shfl_xor(gt, o, 64);
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 0) {
+        lds[wave] = gt;
+        s_cnt[wave] = kor;
+        s_and[wave] = kand;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ws->cnt_gt[t][r] = lds[0] + lds[1] + lds[2] + lds[3];
+        ws->cnt_cand[t][r] = run;
+        ws->cand_or[t][r] = s_cnt[0] | s_cnt[1] | s_cnt[2] | s_cnt[3];
+        ws->cand_and[t][r] = s_and[0] & s_and[1] & s_and[2] & s_and[3];
+    }
+}
+
 }  // namespace arctopk

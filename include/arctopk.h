@@ -291,6 +291,13 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   A non-deferred step leaves `stream` waiting for its decode.  With a select stream: `next`
  *   must be NULL (the next call draws its own projections), markers disable it, and with
  *   communicators `ar_stream` must be a third stream (ARCTOPK_EINVAL otherwise).
+ * trail (NULL: none): a step recorded by arctopk_exchange_trail.  World size 1 without markers,
+ *   when both plans qualify (same dtype, r, EF mode and err_in; EF14 / noef; the trail's tensors
+ *   all single-block selects and no column-split encode, this plan's with a multi-block
+ *   select), the trail's encode tiles run as extra blocks of this step's encode launch and its
+ *   selects as extra blocks of this step's first compact launch; otherwise it is enqueued on its
+ *   own first.  Either way it leaves this call as a deferred step (its decode: a later `ride` /
+ *   `finish` / arctopk_exchange_finish, like a defer = 1 step's).
  * Replaces: the whole of group_topk_hook's compressed path (:254-290) given the seed.
  */
 int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
@@ -299,10 +306,20 @@ int arctopk_exchange_step(arctopk_plan* plan, void* bucket, void* err, void* ger
                           void* stream, void* ar_stream, int32_t defer, arctopk_plan* ride,
                           void* const* ride_marks, arctopk_plan* const* finish,
                           void* const* const* finish_marks, int32_t nfinish, const void* V,
-                          void* const* marks, void* sel_stream);
+                          void* const* marks, void* sel_stream, arctopk_plan* trail);
+/*
+ * A TRAILING step (world size 1, EF14 / noef, a deferring caller): the call is recorded on the
+ * plan and nothing is enqueued but the projection draw (draw != 0: on `stream`, now).  The next
+ * arctopk_exchange_step given it as `trail` carries its encode and select in its own launches
+ * (a small bucket then costs no launch of its own); arctopk_exchange_finish enqueues a trailing
+ * step that no step carried, then decodes it.  The CONTRACT of a deferred step holds from this
+ * call on (bucket, err, gerr untouched until the decode is enqueued).
+ */
+int arctopk_exchange_trail(arctopk_plan* plan, void* bucket, void* err, void* gerr, int32_t ef,
+                           int32_t err_in, int32_t draw, uint64_t seed, const void* V, void* stream);
 /* The deferred decode of `plan`'s last deferred exchange step (no-op if none): after that step's
  * packed all-reduce (and, at world size 1, its deferred pack), on the step's select stream if it
- * had one (then `stream` waits for it), else on `stream`. */
+ * had one (then `stream` waits for it), else on `stream`.  A trailing step is enqueued first. */
 int arctopk_exchange_finish(arctopk_plan* plan, void* stream, void* const* marks);
 
 /*

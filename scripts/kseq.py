@@ -13,7 +13,12 @@ for r in rows:
         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:14]:
     print(f"  {k:60s} n={len(v):5d} avg={sum(v) / len(v):8.2f} us")
-enc = [i for i, r in enumerate(rows) if "k_encode" in r["Kernel_Name"]]
+enc = []  # the call's first kernel: the encode (ARC-TopK), else the EF fold / pre-apply (TopK / RandK)
+for anchor in ("k_encode", "k_ef14_fold", "k_ef_apply", "k_ms_init"):
+    enc = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
+    if enc:
+        break
+enc = enc or [0]
 back = int(os.environ.get("KSEQ_BACK", "2"))  # encodes back from the end (one step: buckets + 1)
 start = enc[-back] if len(enc) >= back else enc[0]
 print("  -- one call:")

@@ -171,20 +171,26 @@ def test_roberta_embedding_ef14():
     assert run.checked == 3
 
 
-@pytest.mark.parametrize("force_exchange,select_streams", [(False, "auto"), (True, "auto"), (False, "off"),
-                                                           (True, "off")])
-def test_resnet18_ddp_buckets_ef14(force_exchange, select_streams):
+@pytest.mark.parametrize("force_exchange,select_streams,trail", [(False, "auto", True), (True, "auto", True),
+                                                                 (False, "off", True), (True, "off", True),
+                                                                 (False, "auto", False), (False, "on", True)])
+def test_resnet18_ddp_buckets_ef14(force_exchange, select_streams, trail):
     """configs[1]: the CIFAR ResNet-18's three DDP buckets (reverse parameter order,
     1 MiB first bucket, 25 MiB cap), hooked in bucket order over three backwards on one
     state: per-bucket plans, residuals and projections stay separate.  With the exchange
     step (one-rank RCCL) two buckets per backward are overlapped and deferred.  "auto": each
-    bucket's select, pack and decodes on one of the two select streams."""
+    bucket's select, pack and decodes on one of the two select streams.
+    trail: the 20 KB first bucket is a trailing step, its encode and selects carried by the
+    second bucket's launches (world size 1; the exchange path enqueues it on its own)."""
     layouts = ddp_buckets(resnet18_cifar_shapes())
     assert len(layouts) == 3 and sum(bucket_numel(sh) for sh in layouts) == 11_173_962
     run = ArcRun("ef14", seed=11, force_exchange=force_exchange, select_streams=select_streams)
+    if not trail:
+        run.st.trail_bytes = 0
     for it in range(3):
         run.step({b: (sh, _randn(bucket_numel(sh), 900 + 10 * it + b)) for b, sh in enumerate(layouts)})
     assert run.checked == 9
+    assert (run.st.trail_calls > 0) == (trail and not force_exchange), run.st.trail_calls
 
 
 @pytest.mark.parametrize("force_exchange,select_streams,ef", [(False, "auto", "ef14"), (True, "auto", "ef14"),
@@ -206,6 +212,8 @@ def test_resnet50_ddp_buckets_ef14(force_exchange, select_streams, ef):
     assert run.checked == 10
     if select_streams == "auto":
         assert run.st._sel_streams, "the select streams were not used"
+    if not force_exchange and ef != "ef21":  # the 0.8 MiB first bucket trails into the second
+        assert run.st.trail_calls > 0
 
 
 def test_resnet50_ddp_buckets_topk_ef14():
