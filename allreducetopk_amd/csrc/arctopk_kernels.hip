@@ -3186,7 +3186,8 @@ int launch_encode_r(const arctopk_plan* p, const T* G, T* E, int ef, int err_in,
         const EncTile* tiles = use_e ? p->d_enc_e : p->d_enc;
         float* pb = p->d_part;
         if (er.n > 0) {  // a trailing step's tiles too: the lean kernel only if both tables are short
-            if (p->enc_short && er_short) {
+            if constexpr (R != 4) return ARCTOPK_EINVAL;  // (instantiated for the default r only)
+            else if (p->enc_short && er_short) {
                 if (ef == ARCTOPK_EF_NONE)
                     launch_done(&k_encode_carry<T, R, ARCTOPK_EF_NONE, false, false>, grid, block, lds, st, enc_done, p->d_segs, tiles, nt, G, E, V, sk, pb, keys, pr, er);
                 else if (ef == ARCTOPK_EF14 && err_in)

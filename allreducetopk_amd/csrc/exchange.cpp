@@ -703,7 +703,7 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
     if (!e && trail) {
         constexpr int64_t big_rows = ARCTOPK_SEL_BIG_ROWS;
         const bool fits = !sketch_comm && !marks && trail->device == p->device && trail->dtype == p->dtype &&
-                          trail->r == p->r && trail->x_t_ef == ef && trail->x_t_err_in == err_in &&
+                          trail->r == p->r && p->r == 4 && trail->x_t_ef == ef && trail->x_t_err_in == err_in &&
                           ef != ARCTOPK_EF21 && p->n_large_batches > 0 && p->n_split == 0 &&
                           trail->n_large_batches == 0 && trail->n_small > 0 &&
                           trail->n_split == 0 && !trail->any_keyed && trail->small_lds <= big_rows * 4 + 16 &&

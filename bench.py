@@ -599,6 +599,13 @@ def main():
                     "algorithmic_bytes_per_call": sb, "wall_us_per_bucket": round(wall_s * 1e6, 1),
                     "formula": ("(28 + (8 + 16 ws) rho) B/elem (SURVEY 8d)" if args.hook == "topk"
                                 else "(16 + 28 rho) B/elem (fused RandK minimum)")}
+            # PMC bytes per call of the same command (scripts/profile.sh with BENCH_ARGS="--hook
+            # <hook>", CALL_KERNELS=k_scatter_first): profiles/<round>/pmc_<workload>_<ef>_<hook>.json
+            if world == 1:
+                tr, tr_src, tr_match = pmc_call_traffic(args.workload + ("_bf16" if args.dtype == "bf16" else ""),
+                                                        args.ef, tag=args.hook)
+                roof.update({"traffic": tr, "traffic_source": tr_src, "traffic_lib_match": tr_match,
+                             "traffic_ratio": round(tr / sb, 3) if tr else None})
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),

@@ -292,7 +292,7 @@ int arctopk_comm_allreduce(arctopk_comm* comm, void* buf, int64_t count, int32_t
  *   must be NULL (the next call draws its own projections), markers disable it, and with
  *   communicators `ar_stream` must be a third stream (ARCTOPK_EINVAL otherwise).
  * trail (NULL: none): a step recorded by arctopk_exchange_trail.  World size 1 without markers,
- *   when both plans qualify (same dtype, r, EF mode and err_in; EF14 / noef; the trail's tensors
+ *   when both plans qualify (same dtype, r = 4, EF mode and err_in; EF14 / noef; the trail's tensors
  *   all single-block selects and no column-split encode, this plan's with a multi-block
  *   select), the trail's encode tiles run as extra blocks of this step's encode launch and its
  *   selects as extra blocks of this step's first compact launch; otherwise it is enqueued on its

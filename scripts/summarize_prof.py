@@ -64,7 +64,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from allreducetopk_amd.build import embedded_hash  # noqa: E402
 # per hook call: every libarctopk kernel's bytes (k_*; torch's own fills / copies / randn excluded)
 # over the calls, counted as encode launches (one per call; profile runs skip the marker pass)
-calls = sum(v["launches"] for k, v in out.items() if k in ("k_encode", "k_encode_short"))
+# (CALL_KERNELS: the kernels launched once per call, e.g. k_scatter_first for the TopK / RandK hooks)
+call_kernels = os.environ.get("CALL_KERNELS", "k_encode,k_encode_short,k_encode_carry").split(",")
+calls = sum(v["launches"] for k, v in out.items() if k in call_kernels)
 per_call = None
 if calls:
     tot = sum(v["bytes_per_launch"] * v["launches"] for k, v in out.items() if k.startswith("k_"))
