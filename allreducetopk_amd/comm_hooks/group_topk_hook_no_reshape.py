@@ -1107,8 +1107,13 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
         # and the backward's last (its decode is the drain).
         # a small bucket of single-block selects, with a bucket after it in this backward: a
         # trailing step, carried by the next step's launches (arctopk_exchange_trail)
+        # (not in a backward that runs on select streams: there the small bucket's select already
+        # overlaps the next encode, and carrying its row tiles costs the carrier's lean encode
+        # kernel its occupancy -- ResNet-50 DDP measured 380 -> 335 GB/s)
+        sel_backward = state.select_streams == "on" or (
+            state.select_streams == "auto" and state._sel_small_last >= state.select_stream_min_buckets)
         if (not comms and defer and marks is None and device_v and state.trail_bytes > 0
-                and ef != N.EF21 and state._trail is None
+                and ef != N.EF21 and state._trail is None and not sel_backward
                 and total * input_tensor.element_size() <= state.trail_bytes):
             rc = L.arctopk_exchange_trail(plan.handle, input_tensor.data_ptr(), N.ptr(err), N.ptr(gerr), ef,
                                           int(err_in), int(draw), seed, None, sid)
@@ -1118,6 +1123,7 @@ def group_topk_hook(state: GroupTopKState, bucket: dist.GradBucket
                 state._trail = (plan, fut, None, input_tensor, sid, (err, gerr))
                 pend.append(state._trail)
                 state.trail_calls += 1
+                state._sel_small += int(total * input_tensor.element_size() <= state.select_stream_bytes)
                 state.comm_bits_this_round += 2 * (world_size - 1) * plan.bits_sum  # (:278)
                 state.maybe_increase_iter(bucket)
                 _ht("trail")

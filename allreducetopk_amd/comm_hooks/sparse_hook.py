@@ -77,6 +77,7 @@ class SparseState(HookState):
         self.index_source = index_source
         self._workspace = None
         self._ws_bytes: Dict[tuple, int] = {}
+        self._fold_in = None  # RandK "hash" under EF14: the select applies E (1) or the first-call copy (2)
 
     # ratio of this call; the c4 variant overrides (gradual compression)
     def _call_ratio(self) -> float:
@@ -137,9 +138,12 @@ def _sparse_hook_impl(state: SparseState, bucket, c4: bool = False) -> "torch.fu
             state.error_dict[b] = torch.zeros(total, device=device, dtype=dtype)
         err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
         # E := G + E (:205, :258); selection and gathers then read the pre-compression bucket
-        # from E, and the decode writes the bucket once
-        N.check(L.arctopk_ef14_fold(input_tensor.data_ptr(), err.data_ptr(), total, int(err_in),
-                                    dt, stream), "arctopk_ef14_fold")
+        # from E, and the decode writes the bucket once.  RandK's device draw folds E itself in
+        # its write pass (arctopk_randk_select_ef14: its keys never read the data)
+        if not (state.random and state.index_source == "hash"):
+            N.check(L.arctopk_ef14_fold(input_tensor.data_ptr(), err.data_ptr(), total, int(err_in),
+                                        dt, stream), "arctopk_ef14_fold")
+        state._fold_in = int(err_in)
     elif ef == N.EF21:
         if b in state.error_dict:
             err = _residual_on(state.error_dict, b, input_tensor, "error_dict")
@@ -157,6 +161,8 @@ def _sparse_hook_impl(state: SparseState, bucket, c4: bool = False) -> "torch.fu
             fut.set_result(input_tensor)
             return fut
 
+    if ef != N.EF14 or not (state.random and state.index_source == "hash"):
+        state._fold_in = None  # (set above only when the select folds E itself)
     seed = None
     if state.random:  # shared reseed so every rank draws the same indices (:230-235)
         seed = torch.randint(0, 1_000_000_000, (1,), generator=state.rng).item()
@@ -228,6 +234,13 @@ def _compress_exchange(state: SparseState, bucket, group, world_size: int, ef: i
             for t, k, ko in zip(tensors, ks, k_off):
                 host[ko:ko + k].copy_(torch.randperm(t.numel())[:k])
             indices.copy_(host)
+        elif fold14 and state._fold_in is not None:
+            # "hash" under EF14: the draw, with the fold E := G + E (:205), the gather and
+            # `E[indices] = 0` (:104) all in the select's last pass
+            ws_buf = _workspace(state, device, numels)
+            N.check(L.arctopk_randk_select_ef14(x, state.error_dict[b].data_ptr(), state._fold_in, nt, a_off,
+                                                a_n, a_k, a_ko, int(seed), indices.data_ptr(), values.data_ptr(),
+                                                ws_buf.data_ptr(), dt, stream), "arctopk_randk_select_ef14")
         else:  # "hash": the k largest keyed-hash keys per tensor, ascending, gathered in the select;
             # EF14's `E[indices] = 0` (:104) happens in its last pass, as for TopK
             ws_buf = _workspace(state, device, numels)

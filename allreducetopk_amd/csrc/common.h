@@ -31,7 +31,10 @@
 #ifndef ARCTOPK_ZERO_AHEAD
 #define ARCTOPK_ZERO_AHEAD 1           // the backward's last exchange step (EF14 / noef) zeroes its bucket
 #endif                                 //   while its packed values are on the wire; its decode then
-                                       //   writes the selected rows only (exchange.cpp)
+                                       //   writes the selected rows only (exchange.cpp) ...
+#ifndef ARCTOPK_ZERO_AHEAD_MIN_BYTES
+#define ARCTOPK_ZERO_AHEAD_MIN_BYTES (64ll << 20)  // ... for buckets of at least this many bytes (a
+#endif                                 //   small bucket's decode is short, the memset launch is not)
 #ifndef ARCTOPK_FUSE_CAP
 #define ARCTOPK_FUSE_CAP 8192         // candidates a fused write block stages in LDS (more: swept from L2)
 #endif

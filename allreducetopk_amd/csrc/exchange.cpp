@@ -845,8 +845,9 @@ extern "C" int arctopk_exchange_step(arctopk_plan* p, void* bucket, void* err, v
         // the packed values are on the wire, and the decode after the wire writes only the
         // selected rows (x_fin 3): the same bytes, most of them moved off the drain.  EF21's
         // decode writes gE to the unselected elements and keeps the whole-bucket decode.
-        if (!e && ARCTOPK_ZERO_AHEAD && !defer && async_ar && ef != ARCTOPK_EF21 && p->n_dec > 0) {
-            const size_t esz = p->dtype == ARCTOPK_BF16 ? 2 : 4;
+        const size_t esz = p->dtype == ARCTOPK_BF16 ? 2 : 4;
+        if (!e && ARCTOPK_ZERO_AHEAD && !defer && async_ar && ef != ARCTOPK_EF21 && p->n_dec > 0 &&
+            (int64_t)(p->info.numel * esz) >= (int64_t)ARCTOPK_ZERO_AHEAD_MIN_BYTES) {
             const hipError_t he = hipMemsetAsync(bucket, 0, (size_t)p->info.numel * esz, ss);
             if (he != hipSuccess) return (int)he;
             p->x_fin = 3;

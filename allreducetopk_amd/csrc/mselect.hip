@@ -111,7 +111,33 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
     const int64_t stride = nblk * 256;
     int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t* src = from_cand ? ckey + it.cand_off : nullptr;
-    const int64_t n = from_cand ? ncand : it.n;
+    int64_t n = from_cand ? ncand : it.n;
+    if constexpr (PASS == 0 && SRC == 1) {
+        // fp32 |x| over the whole item: 16-B loads, four in flight per lane (4-B loads left the
+        // pass at ~2.7 TB/s), then the < 4 tail elements below.  Plain (not nontemporal) loads:
+        // the compact pass reads the item again right after, partly from the Infinity Cache
+        const float* xf = static_cast<const float*>(x) + it.key_off;
+        if ((reinterpret_cast<uintptr_t>(xf) & 15) == 0) {
+            const int64_t n4 = it.n >> 2;
+            int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+            auto add4 = [&](float4 v) {
+                const uint32_t kq[4] = {__float_as_uint(v.x) & 0x7FFFFFFFu, __float_as_uint(v.y) & 0x7FFFFFFFu,
+                                        __float_as_uint(v.z) & 0x7FFFFFFFu, __float_as_uint(v.w) & 0x7FFFFFFFu};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if ((kq[c] & s.mask) == s.prefix) atomicAdd(&h[(kq[c] >> shift) & dmask], 1u);
+            };
+            for (; q + 3 * stride < n4; q += 4 * stride) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = ldq<float, false>(xf, q + u * stride);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) add4(v[u]);
+            }
+            for (; q < n4; q += stride) add4(ldq<float, false>(xf, q));
+            i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x;  // the tail, element by element
+        }
+    }
     for (; i + 3 * stride < n; i += 4 * stride) {  // four loads in flight per lane
         uint32_t k4[4];
 #pragma unroll
@@ -371,7 +397,7 @@ __global__ void __launch_bounds__(256) k_ms_count(MBatch b, const uint32_t* __re
 // ballot compaction in index order.  ARC: rows[out_off + slot] = i and the slot map for
 // every key; TopK: idx[out_off + slot] = i, vals[out_off + slot] = x[key_off + i].
 
-template <int SRC, bool ARC>
+template <int SRC, bool ARC, int FOLD = 0>
 __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __restrict__ keys,
                                                   const void* __restrict__ x, MWorkspace* ws,
                                                   int32_t* __restrict__ out_idx,
@@ -379,7 +405,7 @@ __global__ void __launch_bounds__(256) k_ms_write(MBatch b, const uint32_t* __re
                                                   int32_t* __restrict__ out_slot, void* zero_x) {
     int t, r;
     if (!ms_locate(b, &t, &r)) return;
-    ms_write_body<SRC, ARC>(b, t, r, keys, x, ws, out_idx, out_val, out_slot, zero_x);
+    ms_write_body<SRC, ARC, FOLD>(b, t, r, keys, x, ws, out_idx, out_val, out_slot, zero_x);
 }
 
 // ARC: the batch from device memory (plan-resident)
@@ -419,7 +445,8 @@ int64_t ms_workspace_bytes(int64_t cap_total) {
 
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
-              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed) {
+              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed, int fold) {
+    if (fold && (!hashed || !x || !zero_x || arc)) return 1001;  // ARCTOPK_EINVAL
     const int cnt = b.cnt;
     if (cnt < 1) return 0;
     int gr = 1;
@@ -452,6 +479,26 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
         hipLaunchKernelGGL((k_ms_write<FF, AR>), gflat, dim3(256), 0, st, b, keys, x, ws, out_idx,     \
                            out_val, out_slot, zero_x);                                                 \
     } while (0)
+    // the RandK select with the EF14 fold in its write pass: the passes before it never read x
+#define MS_LAUNCH_FOLD(FF, FO)                                                                         \
+    do {                                                                                               \
+        hipLaunchKernelGGL(k_ms_init<FF>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
+        hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey);      \
+        hipLaunchKernelGGL(k_ms_compact<FF>, gc, dim3(256), 0, st, b, keys, nullptr, ws, ckey, cidx);  \
+        hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey);      \
+        hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey);      \
+        hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, nullptr, ws, ckey, cidx);    \
+        hipLaunchKernelGGL((k_ms_write<FF, false, FO>), gflat, dim3(256), 0, st, b, keys, x, ws,       \
+                           out_idx, out_val, out_slot, zero_x);                                        \
+    } while (0)
+    if (fold) {
+        if (x_bf16 && fold == 1) MS_LAUNCH_FOLD(4, 1);
+        else if (x_bf16) MS_LAUNCH_FOLD(4, 2);
+        else if (fold == 1) MS_LAUNCH_FOLD(3, 1);
+        else MS_LAUNCH_FOLD(3, 2);
+        return (int)hipGetLastError();
+    }
+#undef MS_LAUNCH_FOLD
     if (arc)
         MS_LAUNCH(0, true);
     else if (hashed && x_bf16)

@@ -62,11 +62,31 @@ __device__ __forceinline__ uint32_t popc64(uint64_t v) { return (uint32_t)__popc
 // TopK (!ARC) with zero_x (= x): the tile is rewritten with its selected elements zeroed,
 // whole tiles, so no line is left partially dirty -- EF14's `tensor.view(-1)[indices] = 0`
 // (sparse_hook.py:104) fused into the pass that already reads every element
-template <int SRC, bool ARC>
+// FOLD (RandK hash keys only: the keys do not depend on x, so the select's earlier passes never
+// read it): x is the bucket G and zero_x the residual E, and the pass applies EF14 itself --
+// v = G + E (FOLD 1; FOLD 2, the first call: v = G), rounded to x's type as the reference's
+// tensor.add_(E) (sparse_hook.py:205) -- gathers v, and writes E := v with the selected
+// elements zeroed (:104): the separate fold pass over G and E is not needed.
+template <int SRC>
+__device__ __forceinline__ uint32_t fold_bits(const void* __restrict__ g, const void* __restrict__ e, int64_t i,
+                                              int fold) {
+    if constexpr (SRC == 3) {
+        const float gv = static_cast<const float*>(g)[i];
+        return __float_as_uint(fold == 1 ? __fadd_rn(gv, static_cast<const float*>(e)[i]) : gv);
+    } else {
+        const bf16_t gv = static_cast<const bf16_t*>(g)[i];
+        if (fold != 1) return (uint32_t)gv.u << 16;
+        const float f = __fadd_rn(to_f(gv), to_f(static_cast<const bf16_t*>(e)[i]));
+        return (uint32_t)from_f<bf16_t>(f).u << 16;
+    }
+}
+
+template <int SRC, bool ARC, int FOLD = 0>
 __device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, const uint32_t* __restrict__ keys,
                                               const void* __restrict__ x, MWorkspace* ws,
                                               int32_t* __restrict__ out_idx, void* __restrict__ out_val,
                                               int32_t* __restrict__ out_slot, void* zero_x) {
+    static_assert(FOLD == 0 || SRC >= 3, "the fused EF14 fold needs keys that do not read x");
     __shared__ uint32_t s_eq[4], s_gt[4];
     const MItem it = b.it[t];
     const uint32_t T = ws->st[t].prefix;
@@ -84,7 +104,8 @@ __device__ __forceinline__ void ms_write_body(const MBatch& b, int t, int r, con
             const int64_t i = min<int64_t>(wb + j * 64 + lane, r1 - 1);
             if constexpr (SRC >= 3) {  // RandK: keys from the index; x only for values / zero_x
                 kv[j] = rk_key(it.hseed, i);
-                bits[j] = x ? load_bits<SRC>(keys, x, it.key_off + i) : 0u;
+                if constexpr (FOLD != 0) bits[j] = fold_bits<SRC>(x, zero_x, it.key_off + i, FOLD);
+                else bits[j] = x ? load_bits<SRC>(keys, x, it.key_off + i) : 0u;
             } else {
                 bits[j] = load_bits<SRC>(keys, x, it.key_off + i);
                 kv[j] = key_of<SRC>(bits[j]);

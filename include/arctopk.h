@@ -422,6 +422,18 @@ int arctopk_randk_select(const void* x, int32_t ntensors, const int64_t* offsets
                          const int64_t* numels, const int64_t* ks, const int64_t* k_off,
                          uint64_t seed, int32_t* idx, void* vals, void* workspace, int32_t dtype,
                          int32_t zero_selected, void* stream);
+/*
+ * The same RandK draw with EF14 applied in the select's write pass (the hash keys never read the
+ * data, so the passes before it do not either): v = g + E (err_in; else v = g, the first call),
+ * rounded to the dtype as tensor.add_(E) is (sparse_hook.py:205), vals = v[idx], and E := v with
+ * the selected elements zeroed (:104).  g (the bucket) is not written.  Replaces arctopk_ef14_fold
+ * followed by arctopk_randk_select(E, ..., zero_selected = 1): one pass over the bucket and the
+ * residual instead of two.
+ */
+int arctopk_randk_select_ef14(const void* g, void* E, int32_t err_in, int32_t ntensors,
+                              const int64_t* offsets, const int64_t* numels, const int64_t* ks,
+                              const int64_t* k_off, uint64_t seed, int32_t* idx, void* vals,
+                              void* workspace, int32_t dtype, void* stream);
 
 /* Gather vals[k_off[i] + j] = x[offsets[i] + idx[k_off[i] + j]]  (sparse_hook.py:22). */
 int arctopk_sparse_gather(const void* x, int32_t ntensors, const int64_t* offsets,

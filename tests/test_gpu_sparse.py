@@ -163,6 +163,44 @@ def test_randk_select_kernel_vs_restatement(dtype, zero):
     assert_bitwise(xo, expect_x, "x after the select")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("err_in", [1, 0])
+def test_randk_select_ef14_fold(dtype, err_in):
+    """arctopk_randk_select_ef14: the EF14 pre-apply folded into the draw's write pass gives the
+    bits of arctopk_ef14_fold then arctopk_randk_select(E, zero_selected=1): X = G + E rounded to
+    the dtype (err_in; else X = G), vals = X[idx] at the restated indices, E := X with them zeroed,
+    G untouched."""
+    L = N.lib()
+    g = torch.Generator().manual_seed(22)
+    numels = [5, 4096, 65_537, 1_000_003] + [700 + 13 * i for i in range(50)]
+    ks = [2, 819, 13_107, 200_000] + [max(1, (700 + 13 * i) // 5) for i in range(50)]
+    offs = [sum(numels[:i]) for i in range(len(numels))]
+    kof = [sum(ks[:i]) for i in range(len(ks))]
+    G = torch.randn(sum(numels), generator=g).to(dtype)
+    E0 = torch.randn(sum(numels), generator=g).to(dtype)
+    Gd, Ed = G.to(DEV), E0.to(DEV)
+    idx = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
+    vals = torch.empty(sum(ks), dtype=dtype, device=DEV)
+    ws = torch.empty(int(L.arctopk_sparse_workspace_bytes(len(numels), N.i64_array(numels))),
+                     dtype=torch.uint8, device=DEV)
+    seed = 987_654_321
+    N.check(L.arctopk_randk_select_ef14(Gd.data_ptr(), Ed.data_ptr(), err_in, len(numels), N.i64_array(offs),
+                                        N.i64_array(numels), N.i64_array(ks), N.i64_array(kof), seed,
+                                        idx.data_ptr(), vals.data_ptr(), ws.data_ptr(), N.DTYPE_CODE[dtype],
+                                        torch.cuda.current_stream().cuda_stream), "randk_select_ef14")
+    torch.cuda.synchronize()
+    X = (G.float() + E0.float()).to(dtype) if err_in else G.clone()  # torch's own bf16 add rounding
+    expect_E = X.clone()
+    i, v = idx.cpu().long(), vals.cpu()
+    for t, (n, k, o, ko) in enumerate(zip(numels, ks, offs, kof)):
+        ref = S.randk_hash_indices(n, k, seed, t).long()
+        assert torch.equal(i[ko:ko + k], ref), f"tensor {t} indices"
+        assert_bitwise(v[ko:ko + k], X[o + ref], f"tensor {t} values")
+        expect_E[o + ref] = 0
+    assert_bitwise(Ed, expect_E, "E after the select")
+    assert_bitwise(Gd, G, "G untouched")
+
+
 @pytest.mark.parametrize("ef", ["noef", "ef14", "ef21"])
 @pytest.mark.parametrize("source", ["torch", "host", "hash"])
 def test_randk_hook_vs_oracle(ef, source):
