@@ -103,6 +103,9 @@ _SIGS = {
     "arctopk_randk_select": (c_int32, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64),
                                        POINTER(c_int64), POINTER(c_int64), c_uint64, c_void_p, c_void_p,
                                        c_void_p, c_int32, c_int32, c_void_p]),
+    "arctopk_topk_select_ef14": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, POINTER(c_int64),
+                                           POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), c_void_p,
+                                           c_void_p, c_void_p, c_int32, c_void_p]),
     "arctopk_randk_select_ef14": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, POINTER(c_int64),
                                             POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), c_uint64,
                                             c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),

@@ -140,7 +140,8 @@ def _sparse_hook_impl(state: SparseState, bucket, c4: bool = False) -> "torch.fu
         # E := G + E (:205, :258); selection and gathers then read the pre-compression bucket
         # from E, and the decode writes the bucket once.  RandK's device draw folds E itself in
         # its write pass (arctopk_randk_select_ef14: its keys never read the data)
-        if not (state.random and state.index_source == "hash"):
+        # (and fp32 TopK folds it in its first pass: arctopk_topk_select_ef14)
+        if not _select_folds(state, dtype):
             N.check(L.arctopk_ef14_fold(input_tensor.data_ptr(), err.data_ptr(), total, int(err_in),
                                         dt, stream), "arctopk_ef14_fold")
         state._fold_in = int(err_in)
@@ -161,7 +162,7 @@ def _sparse_hook_impl(state: SparseState, bucket, c4: bool = False) -> "torch.fu
             fut.set_result(input_tensor)
             return fut
 
-    if ef != N.EF14 or not (state.random and state.index_source == "hash"):
+    if ef != N.EF14 or not _select_folds(state, dtype):
         state._fold_in = None  # (set above only when the select folds E itself)
     seed = None
     if state.random:  # shared reseed so every rank draws the same indices (:230-235)
@@ -173,6 +174,14 @@ def _sparse_hook_impl(state: SparseState, bucket, c4: bool = False) -> "torch.fu
     fut = torch.futures.Future()
     fut.set_result(input_tensor)
     return fut
+
+
+def _select_folds(state: SparseState, dtype) -> bool:
+    """EF14's E := G + E is applied by the select itself (RandK's device draw: in its write pass;
+    fp32 TopK: in its first histogram pass), not by a fold pass of its own."""
+    if state.random:
+        return state.index_source == "hash"
+    return dtype == torch.float32
 
 
 def _check_compressible(state: SparseState, input_tensor: torch.Tensor) -> None:
@@ -253,10 +262,19 @@ def _compress_exchange(state: SparseState, bucket, group, world_size: int, ef: i
         bits_sum = sum_k * dtype_bits(dtype)
     else:
         ws_buf = _workspace(state, device, numels)
-        # EF14: the residual's `E[indices] = 0` (:104) happens in the select's last pass
-        N.check(L.arctopk_topk_select(xsrc, nt, a_off, a_n, a_k, a_ko, indices.data_ptr(),
-                                      values.data_ptr(), ws_buf.data_ptr(), dt, int(fold14), stream),
-                "arctopk_topk_select")
+        rc = N.EINVAL
+        if fold14 and state._fold_in is not None:  # E := G + E (:205) in the select's first pass
+            rc = L.arctopk_topk_select_ef14(x, xsrc, state._fold_in, nt, a_off, a_n, a_k, a_ko,
+                                            indices.data_ptr(), values.data_ptr(), ws_buf.data_ptr(), dt, stream)
+            if rc == N.EINVAL:  # (a tensor not 16-B aligned / of numel % 4 != 0): fold, then select
+                N.check(L.arctopk_ef14_fold(x, xsrc, total, state._fold_in, dt, stream), "arctopk_ef14_fold")
+            else:
+                N.check(rc, "arctopk_topk_select_ef14")
+        if rc == N.EINVAL:
+            # EF14: the residual's `E[indices] = 0` (:104) happens in the select's last pass
+            N.check(L.arctopk_topk_select(xsrc, nt, a_off, a_n, a_k, a_ko, indices.data_ptr(),
+                                          values.data_ptr(), ws_buf.data_ptr(), dt, int(fold14), stream),
+                    "arctopk_topk_select")
         bits_sum = sum_k * (dtype_bits(dtype) + 32)
 
     # the call's selection, for inspection and tests (int32 indices per tensor, concatenated

@@ -249,12 +249,15 @@ int64_t ms_workspace_bytes(int64_t cap_total);
 // hashed (RandK): the keys are rk_key(it.hseed, index) instead of |x| -- the k largest of these
 // distinct keys are a uniformly random k-subset, emitted in ascending index order; x (may be null:
 // indices only) is then only the source of the gathered values and of zero_x
-// fold (hashed only; 1: EF14 with a residual, 2: EF14's first call): x is the bucket G and zero_x the
+// fold (1: EF14 with a residual, 2: EF14's first call).  hashed: x is the bucket G and zero_x the
 // residual E; the write pass forms v = G (+ E) itself, gathers it and writes E := v with the
-// selected elements zeroed (mselect_dev.h, fold_bits)
+// selected elements zeroed (mselect_dev.h, fold_bits).  TopK (fp32, every item 16-B aligned with
+// n % 4 == 0): x = zero_x is the residual E and fold_g the bucket G; the first histogram pass
+// writes E := G (+ E) as it streams, the later passes read it
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
-              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed = false, int fold = 0);
+              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed = false, int fold = 0,
+              const void* fold_g = nullptr);
 
 // ARC selection after the fused key kernel (keys + first-pass histogram + digit, every
 // item in candidate mode), in three launches per batch: ms_arc_compact (per range: the

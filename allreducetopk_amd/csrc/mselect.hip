@@ -18,6 +18,9 @@ namespace {
 constexpr int kW1 = 12;  // first-pass digit width (kMBins = 1 << kW1)
 constexpr int kW2 = 10;  // refinement digit width (12 + 10 + 10 >= 32 key bits)
 constexpr int kCandPerBlock = 2048;     // candidates per block of a refinement pass
+#ifndef ARCTOPK_COMPACT_NT
+#define ARCTOPK_COMPACT_NT 0            // TopK compact: nontemporal 16-B loads of |x| (A/B switch)
+#endif
 constexpr int kCompactRanges = 4;       // ranges per block of the TopK / RandK compact pass
 constexpr int kCompactStage = 4096;     // candidates a compact block stages in LDS (32 KiB)
 
@@ -82,10 +85,16 @@ __global__ void __launch_bounds__(256) k_ms_init(MBatch b, MWorkspace* ws) {
 // has them.  LDS histogram, merged with one global atomic per non-empty bin; the last
 // block then reads (and clears) the global histogram and fixes the digit holding the
 // kk-th largest key.  PASS 0 also fixes the candidate bin and mode.
-template <int SRC, int PASS>
+// FOLD (TopK, fp32, PASS 0; the host checks every item is 16-B aligned with n % 4 == 0): x is the
+// residual E and g the bucket G; the pass applies EF14 as it streams -- v = G + E (FOLD 1) or G
+// (FOLD 2, the first call), E := v -- and histograms |v|, so the separate fold pass over G and E
+// (arctopk_ef14_fold) is not needed; the later passes read the folded E
+template <int SRC, int PASS, int FOLD = 0>
 __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __restrict__ keys,
                                                  const void* __restrict__ x, MWorkspace* ws,
-                                                 const uint32_t* __restrict__ ckey) {
+                                                 const uint32_t* __restrict__ ckey,
+                                                 const float* __restrict__ g = nullptr) {
+    static_assert(FOLD == 0 || (SRC == 1 && PASS == 0), "the fold is fp32 TopK's first pass");
     // RandK hash keys are uniform over 32 bits, so every block finds every first-pass bin
     // occupied: their first digit is 8 bits (256 bins to merge per block, not 4,096; the k-th
     // key's bin then holds ~n/256 candidates) and the two refinements 12 bits each (8+12+12)
@@ -113,11 +122,11 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
     const uint32_t* src = from_cand ? ckey + it.cand_off : nullptr;
     int64_t n = from_cand ? ncand : it.n;
     if constexpr (PASS == 0 && SRC == 1) {
-        // fp32 |x| over the whole item: 16-B loads, four in flight per lane (4-B loads left the
-        // pass at ~2.7 TB/s), then the < 4 tail elements below.  Plain (not nontemporal) loads:
-        // the compact pass reads the item again right after, partly from the Infinity Cache
+        // fp32 |x| over the whole item: 16-B nontemporal loads, four in flight per lane (4-B loads
+        // left the pass at ~2.7 TB/s: 94 -> 73 us on the headline; plain 16-B loads measured
+        // 110 us), then the < 4 tail elements below
         const float* xf = static_cast<const float*>(x) + it.key_off;
-        if ((reinterpret_cast<uintptr_t>(xf) & 15) == 0) {
+        if (FOLD || (reinterpret_cast<uintptr_t>(xf) & 15) == 0) {
             const int64_t n4 = it.n >> 2;
             int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
             auto add4 = [&](float4 v) {
@@ -127,15 +136,51 @@ __global__ void __launch_bounds__(256) k_ms_hist(MBatch b, const uint32_t* __res
                 for (int c = 0; c < 4; ++c)
                     if ((kq[c] & s.mask) == s.prefix) atomicAdd(&h[(kq[c] >> shift) & dmask], 1u);
             };
+            if constexpr (FOLD != 0) {  // (n % 4 == 0: no tail)
+                const float* gf = g + it.key_off;
+                float* ef = const_cast<float*>(xf);
+                auto fold4 = [&](float4 gv, float4 ev) {
+                    if constexpr (FOLD == 1) {  // tensor.add_(E) (sparse_hook.py:205): fp32 adds, no contraction
+                        gv.x = __fadd_rn(gv.x, ev.x);
+                        gv.y = __fadd_rn(gv.y, ev.y);
+                        gv.z = __fadd_rn(gv.z, ev.z);
+                        gv.w = __fadd_rn(gv.w, ev.w);
+                    }
+                    return gv;
+                };
+                for (; q + 3 * stride < n4; q += 4 * stride) {
+                    float4 gv[4], ev[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        gv[u] = ldq<float, true>(gf, q + u * stride);
+                        if constexpr (FOLD == 1) ev[u] = ldq<float, true>(xf, q + u * stride);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float4 v = fold4(gv[u], ev[u]);
+                        stq<float, true>(ef, q + u * stride, v);
+                        add4(v);
+                    }
+                }
+                for (; q < n4; q += stride) {
+                    const float4 gv = ldq<float, true>(gf, q);
+                    const float4 ev = FOLD == 1 ? ldq<float, true>(xf, q) : gv;
+                    const float4 v = fold4(gv, ev);
+                    stq<float, true>(ef, q, v);
+                    add4(v);
+                }
+                n = 0;  // nothing left for the scalar loops
+            } else {
             for (; q + 3 * stride < n4; q += 4 * stride) {
                 float4 v[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = ldq<float, false>(xf, q + u * stride);
+                for (int u = 0; u < 4; ++u) v[u] = ldq<float, true>(xf, q + u * stride);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) add4(v[u]);
             }
-            for (; q < n4; q += stride) add4(ldq<float, false>(xf, q));
+            for (; q < n4; q += stride) add4(ldq<float, true>(xf, q));
             i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x;  // the tail, element by element
+            }
         }
     }
     for (; i + 3 * stride < n; i += 4 * stride) {  // four loads in flight per lane
@@ -218,6 +263,15 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     uint32_t staged = 0;  // candidates in the LDS stage (uniform)
+    // fp32 |x| keys of a 16-B aligned item of 4k elements: each lane loads 4 quads of a tile (16-B
+    // loads); key j of the lane is element 4 (64 (j / 4) + lane) + j % 4 of its wave's quarter
+    bool vec = false;
+    if constexpr (SRC == 1)
+        vec = (it.n & 3) == 0 &&
+              (reinterpret_cast<uintptr_t>(static_cast<const float*>(x) + it.key_off) & 15) == 0;
+    auto el = [&](int64_t wb, int j) -> int64_t {
+        return vec ? wb + 4 * ((j >> 2) * 64 + lane) + (j & 3) : wb + j * 64 + lane;
+    };
     auto flush = [&]() {  // uniform; the stage -> the item's list, one counter atomic
         if (threadIdx.x == 0) s_base = atomicAdd(&ws->ncand[t].v, staged);
         __syncthreads();
@@ -236,13 +290,31 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
         for (int64_t tile = r0; tile < r1; tile += kMTile) {
             const int64_t wb = tile + (int64_t)wave * (kMTile / 4);
             uint32_t kv[kPerLane];
+            bool loaded = false;
+            if constexpr (SRC == 1) {
+                if (vec) {
+                    const float* xf = static_cast<const float*>(x) + it.key_off;
 #pragma unroll
-            for (int j = 0; j < kPerLane; ++j)
-                kv[j] = item_key<SRC>(it, keys, x, min<int64_t>(wb + j * 64 + lane, r1 - 1));
+                    for (int u = 0; u < kPerLane / 4; ++u) {
+                        const int64_t q = min<int64_t>((wb >> 2) + u * 64 + lane, ((r1 - 1) >> 2));
+                        const float4 v = ldq<float, ARCTOPK_COMPACT_NT != 0>(xf, q);
+                        kv[4 * u + 0] = __float_as_uint(v.x) & 0x7FFFFFFFu;
+                        kv[4 * u + 1] = __float_as_uint(v.y) & 0x7FFFFFFFu;
+                        kv[4 * u + 2] = __float_as_uint(v.z) & 0x7FFFFFFFu;
+                        kv[4 * u + 3] = __float_as_uint(v.w) & 0x7FFFFFFFu;
+                    }
+                    loaded = true;
+                }
+            }
+            if (!loaded) {
+#pragma unroll
+                for (int j = 0; j < kPerLane; ++j)
+                    kv[j] = item_key<SRC>(it, keys, x, min<int64_t>(wb + j * 64 + lane, r1 - 1));
+            }
             uint32_t nin = 0;
 #pragma unroll
             for (int j = 0; j < kPerLane; ++j) {
-                const bool valid = wb + j * 64 + lane < r1;
+                const bool valid = el(wb, j) < r1;
                 gt += (valid && kv[j] > hi) ? 1u : 0u;
                 if (s.cand) nin += popc64(__ballot(valid && (kv[j] & s.m1) == s.p1));
             }
@@ -258,7 +330,7 @@ __global__ void __launch_bounds__(256) k_ms_compact(MBatch b, const uint32_t* __
                 uint32_t pos = staged + before;
 #pragma unroll
                 for (int j = 0; j < kPerLane; ++j) {
-                    const int64_t i = wb + j * 64 + lane;
+                    const int64_t i = el(wb, j);
                     const bool in = i < r1 && (kv[j] & s.m1) == s.p1;
                     const uint64_t bm = __ballot(in);
                     if (in) {
@@ -445,8 +517,8 @@ int64_t ms_workspace_bytes(int64_t cap_total) {
 
 int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x, int x_bf16, bool arc,
               MWorkspace* ws, int64_t cap_total, int32_t* out_idx, void* out_val,
-              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed, int fold) {
-    if (fold && (!hashed || !x || !zero_x || arc)) return 1001;  // ARCTOPK_EINVAL
+              int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed, int fold, const void* fold_g) {
+    if (fold && (!x || !zero_x || arc || (!hashed && (!fold_g || x_bf16)))) return 1001;  // ARCTOPK_EINVAL
     const int cnt = b.cnt;
     if (cnt < 1) return 0;
     int gr = 1;
@@ -471,10 +543,10 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
 #define MS_LAUNCH(FF, AR)                                                                              \
     do {                                                                                               \
         if (!AR) hipLaunchKernelGGL(k_ms_init<FF>, dim3(cnt), dim3(256), 0, st, b, ws);                \
-        hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
+        hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, x, ws, ckey, nullptr);   \
         hipLaunchKernelGGL(k_ms_compact<FF>, gc, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);        \
-        hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
-        hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey);            \
+        hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey, nullptr);   \
+        hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey, nullptr);   \
         hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);          \
         hipLaunchKernelGGL((k_ms_write<FF, AR>), gflat, dim3(256), 0, st, b, keys, x, ws, out_idx,     \
                            out_val, out_slot, zero_x);                                                 \
@@ -483,14 +555,33 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
 #define MS_LAUNCH_FOLD(FF, FO)                                                                         \
     do {                                                                                               \
         hipLaunchKernelGGL(k_ms_init<FF>, dim3(cnt), dim3(256), 0, st, b, ws);                         \
-        hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey);      \
+        hipLaunchKernelGGL((k_ms_hist<FF, 0>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey, nullptr);\
         hipLaunchKernelGGL(k_ms_compact<FF>, gc, dim3(256), 0, st, b, keys, nullptr, ws, ckey, cidx);  \
-        hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey);      \
-        hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey);      \
+        hipLaunchKernelGGL((k_ms_hist<FF, 1>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey, nullptr);\
+        hipLaunchKernelGGL((k_ms_hist<FF, 2>), gh, dim3(256), 0, st, b, keys, nullptr, ws, ckey, nullptr);\
         hipLaunchKernelGGL(k_ms_count<FF>, gt, dim3(256), 0, st, b, keys, nullptr, ws, ckey, cidx);    \
         hipLaunchKernelGGL((k_ms_write<FF, false, FO>), gflat, dim3(256), 0, st, b, keys, x, ws,       \
                            out_idx, out_val, out_slot, zero_x);                                        \
     } while (0)
+    // TopK (fp32) with the EF14 fold in its first histogram pass: x is the residual E
+#define MS_LAUNCH_TOPK_FOLD(FO)                                                                        \
+    do {                                                                                               \
+        hipLaunchKernelGGL(k_ms_init<1>, dim3(cnt), dim3(256), 0, st, b, ws);                          \
+        hipLaunchKernelGGL((k_ms_hist<1, 0, FO>), gh, dim3(256), 0, st, b, keys, x, ws, ckey,          \
+                           static_cast<const float*>(fold_g));                                         \
+        hipLaunchKernelGGL(k_ms_compact<1>, gc, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);         \
+        hipLaunchKernelGGL((k_ms_hist<1, 1>), gh, dim3(256), 0, st, b, keys, x, ws, ckey, nullptr);   \
+        hipLaunchKernelGGL((k_ms_hist<1, 2>), gh, dim3(256), 0, st, b, keys, x, ws, ckey, nullptr);   \
+        hipLaunchKernelGGL(k_ms_count<1>, gt, dim3(256), 0, st, b, keys, x, ws, ckey, cidx);           \
+        hipLaunchKernelGGL((k_ms_write<1, false>), gflat, dim3(256), 0, st, b, keys, x, ws, out_idx,   \
+                           out_val, out_slot, zero_x);                                                 \
+    } while (0)
+    if (fold && !hashed) {
+        if (fold == 1) MS_LAUNCH_TOPK_FOLD(1);
+        else MS_LAUNCH_TOPK_FOLD(2);
+        return (int)hipGetLastError();
+    }
+#undef MS_LAUNCH_TOPK_FOLD
     if (fold) {
         if (x_bf16 && fold == 1) MS_LAUNCH_FOLD(4, 1);
         else if (x_bf16) MS_LAUNCH_FOLD(4, 2);

@@ -284,6 +284,45 @@ extern "C" int arctopk_randk_select(const void* x, int32_t nt, const int64_t* of
     return 0;
 }
 
+extern "C" int arctopk_topk_select_ef14(const void* g, void* E, int32_t err_in, int32_t nt, const int64_t* offsets,
+                                        const int64_t* numels, const int64_t* ks, const int64_t* k_off, int32_t* idx,
+                                        void* vals, void* workspace, int32_t dtype, void* stream) {
+    if (!g || !E || !offsets || !numels || !ks || !k_off || !idx || !vals || !workspace || nt < 1)
+        return ARCTOPK_EINVAL;
+    // the fold streams 16-B quads: fp32, every tensor 16-B aligned in both buffers and n % 4 == 0
+    // (ARCTOPK_EINVAL otherwise: the caller folds first and calls arctopk_topk_select)
+    if (dtype != ARCTOPK_F32 || (((uintptr_t)g | (uintptr_t)E) & 15)) return ARCTOPK_EINVAL;
+    for (int32_t j = 0; j < nt; ++j)
+        if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j] || (numels[j] & 3) ||
+            (offsets[j] & 3))
+            return ARCTOPK_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    arctopk::MWorkspace* ws = (arctopk::MWorkspace*)workspace;
+    const int64_t cap_total = topk_cap_total(nt, numels);
+    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
+        arctopk::MBatch b;
+        b.cnt = std::min<int32_t>(arctopk::kMB, nt - first);
+        int64_t maxn = 0, cap = 0;
+        for (int i = 0; i < b.cnt; ++i) {
+            const int j = first + i;
+            arctopk::MItem& it = b.it[i];
+            it.key_off = offsets[j];
+            it.n = numels[j];
+            it.k = ks[j];
+            it.out_off = k_off[j];
+            it.slot_off = 0;
+            arctopk::ms_item_geometry(it);
+            it.cand_off = cap;
+            cap += it.cand_cap;
+            maxn = std::max(maxn, numels[j]);
+        }
+        int e = arctopk::ms_select(b, maxn, nullptr, E, 0, false, ws, cap_total, idx, vals, nullptr, E, st, false,
+                                   err_in ? 1 : 2, g);
+        if (e) return e;
+    }
+    return 0;
+}
+
 extern "C" int arctopk_randk_select_ef14(const void* g, void* E, int32_t err_in, int32_t nt, const int64_t* offsets,
                                          const int64_t* numels, const int64_t* ks, const int64_t* k_off,
                                          uint64_t seed, int32_t* idx, void* vals, void* workspace, int32_t dtype,

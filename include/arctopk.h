@@ -423,6 +423,19 @@ int arctopk_randk_select(const void* x, int32_t ntensors, const int64_t* offsets
                          uint64_t seed, int32_t* idx, void* vals, void* workspace, int32_t dtype,
                          int32_t zero_selected, void* stream);
 /*
+ * arctopk_topk_select on x = E with EF14 applied in the select's first pass (fp32 only, every
+ * tensor 16-B aligned with numel % 4 == 0; ARCTOPK_EINVAL otherwise, and nothing is enqueued):
+ * that pass streams g (the bucket) and E, writes E := g + E (err_in; else E := g, the first call)
+ * -- tensor.add_(E) (sparse_hook.py:205) -- and histograms it; the later passes select, gather and
+ * (:104) zero E as arctopk_topk_select(E, ..., zero_selected = 1) does.  g is not written.
+ * Replaces arctopk_ef14_fold followed by that select: one pass over the bucket and the residual
+ * fewer.
+ */
+int arctopk_topk_select_ef14(const void* g, void* E, int32_t err_in, int32_t ntensors,
+                             const int64_t* offsets, const int64_t* numels, const int64_t* ks,
+                             const int64_t* k_off, int32_t* idx, void* vals, void* workspace,
+                             int32_t dtype, void* stream);
+/*
  * The same RandK draw with EF14 applied in the select's write pass (the hash keys never read the
  * data, so the passes before it do not either): v = g + E (err_in; else v = g, the first call),
  * rounded to the dtype as tensor.add_(E) is (sparse_hook.py:205), vals = v[idx], and E := v with

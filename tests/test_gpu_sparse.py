@@ -163,6 +163,49 @@ def test_randk_select_kernel_vs_restatement(dtype, zero):
     assert_bitwise(xo, expect_x, "x after the select")
 
 
+@pytest.mark.parametrize("err_in", [1, 0])
+def test_topk_select_ef14_fold(err_in):
+    """arctopk_topk_select_ef14 (the EF14 fold in the first histogram pass) gives the bits of
+    arctopk_ef14_fold then arctopk_topk_select(E, zero_selected=1); a tensor of numel % 4 != 0 is
+    refused (ARCTOPK_EINVAL, nothing enqueued) and the hook then folds first."""
+    L = N.lib()
+    g = torch.Generator().manual_seed(23)
+    numels = [4096, 65_536, 1_000_000, 8, 3_000_000] + [1024 + 64 * i for i in range(40)]
+    ks = [1, 13_107, 200_000, 3, 600_000] + [max(1, (1024 + 64 * i) // 5) for i in range(40)]
+    offs = [sum(numels[:i]) for i in range(len(numels))]
+    kof = [sum(ks[:i]) for i in range(len(ks))]
+    G = torch.randn(sum(numels), generator=g)
+    E0 = torch.randn(sum(numels), generator=g)
+    E0[offs[3]:offs[3] + 8] = 0.5  # ties across G + E
+    G[offs[3]:offs[3] + 8] = 0.25
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.empty(int(L.arctopk_sparse_workspace_bytes(len(numels), N.i64_array(numels))),
+                     dtype=torch.uint8, device=DEV)
+    args = (len(numels), N.i64_array(offs), N.i64_array(numels), N.i64_array(ks), N.i64_array(kof))
+    # reference: fold, then select
+    Gr, Er = G.to(DEV), E0.to(DEV)
+    idx_r = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
+    val_r = torch.empty(sum(ks), device=DEV)
+    N.check(L.arctopk_ef14_fold(Gr.data_ptr(), Er.data_ptr(), Gr.numel(), err_in, 0, st), "fold")
+    N.check(L.arctopk_topk_select(Er.data_ptr(), *args, idx_r.data_ptr(), val_r.data_ptr(), ws.data_ptr(), 0, 1,
+                                  st), "select")
+    # fused
+    Gd, Ed = G.to(DEV), E0.to(DEV)
+    idx = torch.empty(sum(ks), dtype=torch.int32, device=DEV)
+    val = torch.empty(sum(ks), device=DEV)
+    N.check(L.arctopk_topk_select_ef14(Gd.data_ptr(), Ed.data_ptr(), err_in, *args, idx.data_ptr(),
+                                       val.data_ptr(), ws.data_ptr(), 0, st), "select_ef14")
+    torch.cuda.synchronize()
+    assert_bitwise(idx, idx_r, "indices")
+    assert_bitwise(val, val_r, "values")
+    assert_bitwise(Ed, Er, "E")
+    assert_bitwise(Gd, G, "G untouched")
+    bad = [7] + numels[1:]
+    assert L.arctopk_topk_select_ef14(Gd.data_ptr(), Ed.data_ptr(), err_in, len(bad), N.i64_array(offs),
+                                      N.i64_array(bad), N.i64_array([1] + ks[1:]), N.i64_array(kof),
+                                      idx.data_ptr(), val.data_ptr(), ws.data_ptr(), 0, st) == N.EINVAL
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("err_in", [1, 0])
 def test_randk_select_ef14_fold(dtype, err_in):
