@@ -15,6 +15,6 @@ for ent in ${PROFILES}; do
   BENCH_ARGS="$args" bash scripts/profile.sh ev_$tag > $OUT/profile_$tag.log 2>&1 || { echo "profile $tag failed"; tail -20 $OUT/profile_$tag.log; exit 1; }
   cp gpurun_out/prof_ev_$tag/summary.txt $OUT/rocprof_summary_$tag.txt
   cp gpurun_out/prof_ev_$tag/pmc_per_launch.json $OUT/pmc_$tag.json
-  tail -1 gpurun_out/prof_ev_$tag/bench_trace.log > $OUT/bench_$tag.json
+  grep -h '"metric"' gpurun_out/prof_ev_$tag/bench_trace.log > $OUT/bench_$tag.json
   echo "$tag done"
 done
