@@ -2015,10 +2015,6 @@ __device__ __forceinline__ void scatter_chunk(const SegDev* __restrict__ segs, c
 template <typename T, int EF>
 __device__ __forceinline__ void ride_chunk(const DecodeRide<T>& d, int c, float* __restrict__ dlds) {
     if constexpr (EF != ARCTOPK_EF21) {
-        if (d.fin == 3) {
-            scatter_chunk<T>(d.segs, d.chunks[c], d.packed, d.slotmap, d.out, d.sc);
-            return;
-        }
         if (d.fin) {
             finalize_chunk<T>(d.segs, d.chunks[c], d.slotmap, d.E, d.out, d.fin, d.sc);
             return;
@@ -3058,6 +3054,14 @@ __global__ void __launch_bounds__(256) k_decode(DecodeRide<T> d) {
     ride_chunk<T, EF>(d, (int)blockIdx.x, dlds);
 }
 
+// the decode into a bucket that is already zero (fin 3, the zero-ahead drain: only ever the
+// backward's last step's own decode, never a ride -- a kernel of its own, so the kernels the
+// rides run in keep their code)
+template <typename T>
+__global__ void __launch_bounds__(256) k_decode_scatter(DecodeRide<T> d) {
+    scatter_chunk<T>(d.segs, d.chunks[blockIdx.x], d.packed, d.slotmap, d.out, d.sc);
+}
+
 // Two buckets' decodes in one launch (the backward's last exchange step: the previous bucket's
 // deferred decode and its own), blocks [0, a.n) of `a`, then `b`'s
 template <typename T, int EF>
@@ -3327,6 +3331,7 @@ DecodeRide<T> make_ride(const RideArgs* ra) {
     dr.sc = make_scale(ra->ws);
     dr.n = rp->n_dec;
     dr.fin = ride_fin(rp, ra->ef);
+    if (dr.fin == 3) dr.fin = 0;  // (a ride never follows a zero-ahead; a whole decode is right anyway)
     dr.E = static_cast<T*>(rp->x_err);
     return dr;
 }
@@ -3611,7 +3616,10 @@ int launch_decode(const arctopk_plan* p, int c0, int c1, const int32_t* dfirst, 
     d.E = static_cast<T*>(E);
     const dim3 grid(c1 - c0);
     const size_t lds = (size_t)p->dec_lds_bytes;
-    if (ef == ARCTOPK_EF21 && !fin)
+    if (fin == 3) {
+        if (done) hipExtLaunchKernelGGL(k_decode_scatter<T>, grid, dim3(256), 0, st, nullptr, done, 0, d);
+        else hipLaunchKernelGGL(k_decode_scatter<T>, grid, dim3(256), 0, st, d);
+    } else if (ef == ARCTOPK_EF21 && !fin)
         decode_launch<T, ARCTOPK_EF21>(grid, lds, st, done, d);
     else if (ef == ARCTOPK_EF_NONE || ef == ARCTOPK_EF14)
         decode_launch<T, ARCTOPK_EF_NONE>(grid, lds, st, done, d);
@@ -3738,6 +3746,7 @@ int launch_select_ride(const arctopk_plan* p, const void* sketch_, int32_t ws, i
     dr.sc = make_scale(rp_ws);
     dr.n = rp->n_dec;
     dr.fin = ride_fin(rp, rp_ef);
+    if (dr.fin == 3) dr.fin = 0;
     dr.E = static_cast<T*>(rp->x_err);
     const size_t shm = (size_t)std::max(p->small_lds, rp->dec_lds_bytes);
     const dim3 grid(p->n_small + dr.n + job.n);

@@ -259,6 +259,13 @@ int ms_select(const MBatch& b, int64_t maxn, const uint32_t* keys, const void* x
               int32_t* out_slot, void* zero_x, hipStream_t st, bool hashed = false, int fold = 0,
               const void* fold_g = nullptr);
 
+// TopK / RandK items of at most kMSmallSel keys: one 1,024-thread block per item of the batch (keys in
+// LDS, 8-bit radix rounds, ordered write); the same outputs as ms_select (x / zero_x / fold / fold_g
+// as there).  ARCTOPK_EINVAL if an item is larger.
+constexpr int kMSmallSel = 12288;  // 48 KiB of LDS keys
+int ms_select_small(const MBatch& b, const void* x, int x_bf16, int32_t* out_idx, void* out_val, void* zero_x,
+                    hipStream_t st, bool hashed, int fold, const void* fold_g);
+
 // ARC selection after the fused key kernel (keys + first-pass histogram + digit, every
 // item in candidate mode), in three launches per batch: ms_arc_compact (per range: the
 // bin's keys -> that range's own region of the candidate list, the counts of candidates

@@ -22,6 +22,7 @@ constexpr int kCandPerBlock = 2048;     // candidates per block of a refinement 
 #define ARCTOPK_COMPACT_NT 0            // TopK compact: nontemporal 16-B loads of |x| (A/B switch)
 #endif
 constexpr int kCompactRanges = 4;       // ranges per block of the TopK / RandK compact pass
+constexpr int kSmallSelThreads = 1024;  // threads of the single-block small-item select
 constexpr int kCompactStage = 4096;     // candidates a compact block stages in LDS (32 KiB)
 
 
@@ -489,6 +490,129 @@ __global__ void __launch_bounds__(256) k_arc_write(const MBatch* __restrict__ bp
     ms_write_body<0, true>(*bp, t, r, keys, nullptr, ws, out_idx, nullptr, out_slot, nullptr);
 }
 
+// Single-block select of one small item per block (TopK / RandK tensors of at most kSmallSel keys:
+// BatchNorm vectors, biases, small convs): its keys in LDS, four 8-bit radix rounds over them, then
+// the ordered write in chunks of the block (ascending indices; ties at the threshold lowest index
+// first, as the multi-block select), so a bucket of many small tensors costs one launch per 48 of
+// them instead of seven.  FOLD as in k_ms_hist (TopK: E := G + E written while the keys are
+// formed; the write pass then reads the folded E) and ms_write_body (RandK: v = G + E formed in
+// the write pass, E := v with the selected elements zeroed).
+template <int SRC, int FOLD>
+__global__ void __launch_bounds__(kSmallSelThreads) k_ms_small(MBatch b, const void* __restrict__ x,
+                                                               const void* __restrict__ g, int32_t* __restrict__ out_idx,
+                                                               void* __restrict__ out_val, void* zero_x) {
+    constexpr int NT = kSmallSelThreads, NW = NT / 64;
+    extern __shared__ __attribute__((aligned(16))) uint32_t skeys[];
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_w[2][NW];
+    __shared__ uint32_t s_digit, s_acc;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const MItem it = b.it[blockIdx.x];
+    const int n = (int)it.n;
+    for (int i = tid; i < n; i += NT) {
+        uint32_t key;
+        if constexpr (SRC >= 3) {
+            key = rk_key(it.hseed, i);
+        } else if constexpr (FOLD != 0) {  // fp32 TopK: E := G (+ E), keyed by |E|
+            float v = static_cast<const float*>(g)[it.key_off + i];
+            if constexpr (FOLD == 1) v = __fadd_rn(v, static_cast<const float*>(x)[it.key_off + i]);
+            static_cast<float*>(const_cast<void*>(x))[it.key_off + i] = v;
+            key = __float_as_uint(v) & 0x7FFFFFFFu;
+        } else {
+            key = item_key<SRC>(it, nullptr, x, i);
+        }
+        skeys[i] = key;
+    }
+    __syncthreads();
+    uint32_t prefix = 0u, mask = 0u;
+    int64_t kk = it.k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int j = tid; j < 256; j += NT) hist[j] = 0u;
+        __syncthreads();
+        for (int i = tid; i < n; i += NT) {
+            const uint32_t k = skeys[i];
+            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {  // lane l: bins 255 - 4l .. 252 - 4l, scanned from the top
+            uint32_t c[4], tot = 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = hist[255 - (4 * lane + q)];
+                tot += c[q];
+            }
+            uint32_t incl = tot;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint64_t excl = incl - tot;
+            if (excl < (uint64_t)kk && excl + tot >= (uint64_t)kk) {
+                uint64_t acc = excl;
+                int q = 0;
+                for (; q < 3; ++q) {
+                    if (acc + c[q] >= (uint64_t)kk) break;
+                    acc += c[q];
+                }
+                s_digit = (uint32_t)(255 - (4 * lane + q));
+                s_acc = (uint32_t)acc;
+            }
+        }
+        __syncthreads();
+        prefix |= s_digit << shift;
+        mask |= 255u << shift;
+        kk -= (int64_t)s_acc;
+        __syncthreads();  // s_digit / s_acc / hist are rewritten by the next round
+    }
+    const uint32_t T = prefix;
+    const uint32_t take_eq = (uint32_t)kk;  // threshold-equal keys to take, lowest index first
+    uint32_t run = 0u, eq_run = 0u;
+    for (int c0 = 0; c0 < n; c0 += NT) {
+        const int i = c0 + tid;
+        const bool valid = i < n;
+        const uint32_t key = valid ? skeys[i] : 0u;
+        const bool gt = valid && key > T, eq = valid && key == T;
+        const uint64_t beq = __ballot(eq);
+        if (lane == 0) s_w[0][wave] = popc64(beq);
+        __syncthreads();
+        uint32_t eq_before = popc64(beq & lt), eq_tot = 0u;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            eq_before += w < wave ? s_w[0][w] : 0u;
+            eq_tot += s_w[0][w];
+        }
+        const bool sel = gt || (eq && eq_run + eq_before < take_eq);
+        const uint64_t bsel = __ballot(sel);
+        if (lane == 0) s_w[1][wave] = popc64(bsel);
+        __syncthreads();
+        uint32_t sel_before = popc64(bsel & lt), sel_tot = 0u;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            sel_before += w < wave ? s_w[1][w] : 0u;
+            sel_tot += s_w[1][w];
+        }
+        if (valid) {
+            uint32_t bits = 0u;
+            if constexpr (SRC >= 3 && FOLD != 0) bits = fold_bits<SRC>(g, zero_x, it.key_off + i, FOLD);
+            else if (x && (sel || (SRC >= 3 && zero_x))) bits = load_bits<SRC>(nullptr, x, it.key_off + i);
+            const uint32_t pos = run + sel_before;
+            if (sel && pos < (uint32_t)it.k) {
+                out_idx[it.out_off + pos] = i;
+                if (out_val) store_val<SRC>(out_val, it.out_off + pos, bits);
+            }
+            if (zero_x && (sel || (SRC >= 3 && FOLD != 0))) {  // E[idx] = 0 (:104); RandK fold: E := v elsewhere
+                if constexpr (SRC == 1 || SRC == 3) static_cast<float*>(zero_x)[it.key_off + i] = sel ? 0.f : __uint_as_float(bits);
+                else static_cast<uint16_t*>(zero_x)[it.key_off + i] = sel ? (uint16_t)0 : (uint16_t)(bits >> 16);
+            }
+        }
+        run += sel_tot;
+        eq_run += eq_tot;
+        __syncthreads();  // s_w is rewritten by the next chunk
+    }
+}
+
 }  // namespace
 
 void ms_item_geometry(MItem& it, int max_ranges) {
@@ -501,6 +625,30 @@ void ms_item_geometry(MItem& it, int max_ranges) {
     // n on degenerate data (e.g. a zero tensor) -> full mode past the cap
     it.cand_cap = it.n <= 65536 ? it.n : std::max<int64_t>(65536, it.n / 8);
     it.hseed = 0;
+}
+
+int ms_select_small(const MBatch& b, const void* x, int x_bf16, int32_t* out_idx, void* out_val, void* zero_x,
+                    hipStream_t st, bool hashed, int fold, const void* fold_g) {
+    if (b.cnt < 1) return 0;
+    int64_t maxn = 0;
+    for (int i = 0; i < b.cnt; ++i) maxn = std::max(maxn, b.it[i].n);
+    if (maxn > kMSmallSel || (fold && (!x || !zero_x || !fold_g || (!hashed && x_bf16)))) return 1001;
+    const size_t lds = (size_t)maxn * 4;
+    const dim3 grid(b.cnt), block(kSmallSelThreads);
+#define MS_SMALL(FF, FO) hipLaunchKernelGGL((k_ms_small<FF, FO>), grid, block, lds, st, b, x, fold_g, out_idx, out_val, zero_x)
+    if (hashed) {
+        if (fold == 1) { if (x_bf16) MS_SMALL(4, 1); else MS_SMALL(3, 1); }
+        else if (fold == 2) { if (x_bf16) MS_SMALL(4, 2); else MS_SMALL(3, 2); }
+        else if (x_bf16) MS_SMALL(4, 0);
+        else MS_SMALL(3, 0);
+    } else {
+        if (fold == 1) MS_SMALL(1, 1);
+        else if (fold == 2) MS_SMALL(1, 2);
+        else if (x_bf16) MS_SMALL(2, 0);
+        else MS_SMALL(1, 0);
+    }
+#undef MS_SMALL
+    return (int)hipGetLastError();
 }
 
 RangeGrid ms_range_grid(const MBatch& b) {

@@ -178,14 +178,22 @@ inline int grid_for(int64_t work, int cap) {
 
 }  // namespace
 
-// candidate slots the TopK select needs: the largest per-batch sum of item capacities
+// Tensors of at most kMSmallSel elements take the single-block select (ms_select_small), the rest
+// the multi-block one, in batches of kMB in tensor order within each group
+static void split_small(int32_t nt, const int64_t* numels, std::vector<int32_t>* small, std::vector<int32_t>* large) {
+    for (int32_t j = 0; j < nt; ++j) (numels[j] <= arctopk::kMSmallSel ? small : large)->push_back(j);
+}
+
+// candidate slots the multi-block select needs: the largest per-batch sum of its items' capacities
 static int64_t topk_cap_total(int32_t nt, const int64_t* numels) {
+    std::vector<int32_t> small, large;
+    split_small(nt, numels, &small, &large);
     int64_t best = 0;
-    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
+    for (size_t a = 0; a < large.size(); a += arctopk::kMB) {
         int64_t cap = 0;
-        for (int32_t j = first; j < std::min<int32_t>(nt, first + arctopk::kMB); ++j) {
+        for (size_t q = a; q < std::min(large.size(), a + (size_t)arctopk::kMB); ++q) {
             arctopk::MItem it{};
-            it.n = std::max<int64_t>(1, numels[j]);
+            it.n = std::max<int64_t>(1, numels[large[q]]);
             arctopk::ms_item_geometry(it);
             cap += it.cand_cap;
         }
@@ -193,6 +201,13 @@ static int64_t topk_cap_total(int32_t nt, const int64_t* numels) {
     }
     return best;
 }
+
+// the TopK / RandK select over every tensor: key_off = offsets[j] (0 without x), out_off = k_off[j];
+// hashed: RandK keys of tensor j's seed; zero_x / fold / fold_g as ms_select's
+static int sparse_select(const void* x, int x_bf16, int32_t nt, const int64_t* offsets, const int64_t* numels,
+                         const int64_t* ks, const int64_t* k_off, bool hashed, uint64_t seed, int32_t* idx,
+                         void* vals, arctopk::MWorkspace* ws, void* zero_x, int fold, const void* fold_g,
+                         hipStream_t st);
 
 extern "C" int64_t arctopk_sparse_workspace_bytes(int32_t nt, const int64_t* numels) {
     if (nt < 1 || !numels) return -(int64_t)ARCTOPK_EINVAL;
@@ -212,30 +227,8 @@ extern "C" int arctopk_topk_select(const void* x, int32_t nt, const int64_t* off
         if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j])
             return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    arctopk::MWorkspace* ws = (arctopk::MWorkspace*)workspace;
-    const int64_t cap_total = topk_cap_total(nt, numels);
-    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
-        arctopk::MBatch b;
-        b.cnt = std::min<int32_t>(arctopk::kMB, nt - first);
-        int64_t maxn = 0, cap = 0;
-        for (int i = 0; i < b.cnt; ++i) {
-            const int j = first + i;
-            arctopk::MItem& it = b.it[i];
-            it.key_off = offsets[j];
-            it.n = numels[j];
-            it.k = ks[j];
-            it.out_off = k_off[j];
-            it.slot_off = 0;
-            arctopk::ms_item_geometry(it);
-            it.cand_off = cap;
-            cap += it.cand_cap;
-            maxn = std::max(maxn, numels[j]);
-        }
-        int e = arctopk::ms_select(b, maxn, nullptr, x, dtype == ARCTOPK_BF16, false, ws, cap_total, idx, vals,
-                                   nullptr, zero_selected ? const_cast<void*>(x) : nullptr, st);
-        if (e) return e;
-    }
-    return 0;
+    return sparse_select(x, dtype == ARCTOPK_BF16, nt, offsets, numels, ks, k_off, false, 0, idx, vals,
+                         (arctopk::MWorkspace*)workspace, zero_selected ? const_cast<void*>(x) : nullptr, 0, nullptr, st);
 }
 
 // RandK's per-tensor key seed: splitmix64 of the call's seed and the tensor's place in the bucket
@@ -244,6 +237,43 @@ static uint32_t rk_tensor_seed(uint64_t seed, int32_t t) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return (uint32_t)(z ^ (z >> 31));
+}
+
+static int sparse_select(const void* x, int x_bf16, int32_t nt, const int64_t* offsets, const int64_t* numels,
+                         const int64_t* ks, const int64_t* k_off, bool hashed, uint64_t seed, int32_t* idx,
+                         void* vals, arctopk::MWorkspace* ws, void* zero_x, int fold, const void* fold_g,
+                         hipStream_t st) {
+    std::vector<int32_t> small, large;
+    split_small(nt, numels, &small, &large);
+    const int64_t cap_total = topk_cap_total(nt, numels);
+    for (int pass = 0; pass < 2; ++pass) {
+        const std::vector<int32_t>& list = pass == 0 ? small : large;
+        for (size_t a = 0; a < list.size(); a += arctopk::kMB) {
+            arctopk::MBatch b;
+            b.cnt = (int32_t)std::min(list.size() - a, (size_t)arctopk::kMB);
+            int64_t maxn = 0, cap = 0;
+            for (int i = 0; i < b.cnt; ++i) {
+                const int j = list[a + i];
+                arctopk::MItem& it = b.it[i];
+                it.key_off = x ? offsets[j] : 0;
+                it.n = numels[j];
+                it.k = ks[j];
+                it.out_off = k_off[j];
+                it.slot_off = 0;
+                arctopk::ms_item_geometry(it);
+                it.hseed = hashed ? rk_tensor_seed(seed, j) : 0u;
+                it.cand_off = cap;
+                cap += it.cand_cap;
+                maxn = std::max(maxn, numels[j]);
+            }
+            const int e = pass == 0
+                ? arctopk::ms_select_small(b, x, x_bf16, idx, vals, zero_x, st, hashed, fold, fold_g)
+                : arctopk::ms_select(b, maxn, nullptr, x, x_bf16, false, ws, cap_total, idx, vals, nullptr, zero_x, st,
+                                     hashed, fold, fold_g);
+            if (e) return e;
+        }
+    }
+    return 0;
 }
 
 extern "C" int arctopk_randk_select(const void* x, int32_t nt, const int64_t* offsets, const int64_t* numels,
@@ -257,31 +287,8 @@ extern "C" int arctopk_randk_select(const void* x, int32_t nt, const int64_t* of
         if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j])
             return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    arctopk::MWorkspace* ws = (arctopk::MWorkspace*)workspace;
-    const int64_t cap_total = topk_cap_total(nt, numels);
-    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
-        arctopk::MBatch b;
-        b.cnt = std::min<int32_t>(arctopk::kMB, nt - first);
-        int64_t maxn = 0, cap = 0;
-        for (int i = 0; i < b.cnt; ++i) {
-            const int j = first + i;
-            arctopk::MItem& it = b.it[i];
-            it.key_off = x ? offsets[j] : 0;
-            it.n = numels[j];
-            it.k = ks[j];
-            it.out_off = k_off[j];
-            it.slot_off = 0;
-            arctopk::ms_item_geometry(it);
-            it.hseed = rk_tensor_seed(seed, j);
-            it.cand_off = cap;
-            cap += it.cand_cap;
-            maxn = std::max(maxn, numels[j]);
-        }
-        int e = arctopk::ms_select(b, maxn, nullptr, x, dtype == ARCTOPK_BF16, false, ws, cap_total, idx, vals,
-                                   nullptr, zero_selected ? const_cast<void*>(x) : nullptr, st, true);
-        if (e) return e;
-    }
-    return 0;
+    return sparse_select(x, dtype == ARCTOPK_BF16, nt, offsets, numels, ks, k_off, true, seed, idx, vals,
+                         (arctopk::MWorkspace*)workspace, zero_selected ? const_cast<void*>(x) : nullptr, 0, nullptr, st);
 }
 
 extern "C" int arctopk_topk_select_ef14(const void* g, void* E, int32_t err_in, int32_t nt, const int64_t* offsets,
@@ -297,30 +304,8 @@ extern "C" int arctopk_topk_select_ef14(const void* g, void* E, int32_t err_in, 
             (offsets[j] & 3))
             return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    arctopk::MWorkspace* ws = (arctopk::MWorkspace*)workspace;
-    const int64_t cap_total = topk_cap_total(nt, numels);
-    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
-        arctopk::MBatch b;
-        b.cnt = std::min<int32_t>(arctopk::kMB, nt - first);
-        int64_t maxn = 0, cap = 0;
-        for (int i = 0; i < b.cnt; ++i) {
-            const int j = first + i;
-            arctopk::MItem& it = b.it[i];
-            it.key_off = offsets[j];
-            it.n = numels[j];
-            it.k = ks[j];
-            it.out_off = k_off[j];
-            it.slot_off = 0;
-            arctopk::ms_item_geometry(it);
-            it.cand_off = cap;
-            cap += it.cand_cap;
-            maxn = std::max(maxn, numels[j]);
-        }
-        int e = arctopk::ms_select(b, maxn, nullptr, E, 0, false, ws, cap_total, idx, vals, nullptr, E, st, false,
-                                   err_in ? 1 : 2, g);
-        if (e) return e;
-    }
-    return 0;
+    return sparse_select(E, 0, nt, offsets, numels, ks, k_off, false, 0, idx, vals, (arctopk::MWorkspace*)workspace,
+                         E, err_in ? 1 : 2, g, st);
 }
 
 extern "C" int arctopk_randk_select_ef14(const void* g, void* E, int32_t err_in, int32_t nt, const int64_t* offsets,
@@ -334,31 +319,8 @@ extern "C" int arctopk_randk_select_ef14(const void* g, void* E, int32_t err_in,
         if (numels[j] < 1 || numels[j] >= (1ll << 31) || ks[j] < 1 || ks[j] > numels[j])
             return ARCTOPK_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    arctopk::MWorkspace* ws = (arctopk::MWorkspace*)workspace;
-    const int64_t cap_total = topk_cap_total(nt, numels);
-    for (int32_t first = 0; first < nt; first += arctopk::kMB) {
-        arctopk::MBatch b;
-        b.cnt = std::min<int32_t>(arctopk::kMB, nt - first);
-        int64_t maxn = 0, cap = 0;
-        for (int i = 0; i < b.cnt; ++i) {
-            const int j = first + i;
-            arctopk::MItem& it = b.it[i];
-            it.key_off = offsets[j];
-            it.n = numels[j];
-            it.k = ks[j];
-            it.out_off = k_off[j];
-            it.slot_off = 0;
-            arctopk::ms_item_geometry(it);
-            it.hseed = rk_tensor_seed(seed, j);
-            it.cand_off = cap;
-            cap += it.cand_cap;
-            maxn = std::max(maxn, numels[j]);
-        }
-        int e = arctopk::ms_select(b, maxn, nullptr, g, dtype == ARCTOPK_BF16, false, ws, cap_total, idx, vals,
-                                   nullptr, E, st, true, err_in ? 1 : 2);
-        if (e) return e;
-    }
-    return 0;
+    return sparse_select(g, dtype == ARCTOPK_BF16, nt, offsets, numels, ks, k_off, true, seed, idx, vals,
+                         (arctopk::MWorkspace*)workspace, E, err_in ? 1 : 2, g, st);
 }
 
 extern "C" int arctopk_sparse_gather(const void* x, int32_t nt, const int64_t* offsets,
