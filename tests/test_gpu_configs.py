@@ -171,6 +171,38 @@ def test_roberta_embedding_ef14():
     assert run.checked == 3
 
 
+@pytest.mark.parametrize("ef", ["ef14", "noef", "ef21"])
+def test_zero_ahead_drain_large_buckets(ef):
+    """The zero-ahead drain (the exchange path's backward-last step on a bucket of >= 64 MiB zeroes the
+    bucket while its packed values are on the wire; the decode after the wire writes only the
+    selected rows; EF21 keeps the whole decode) gives the bits of the world-size-1 step path: two
+    64 MiB buckets over two backwards, forced exchange (one-rank RCCL) against the step path."""
+    shapes = [[4096, 4096]]
+    n = bucket_numel(shapes)
+    assert n * 4 >= 64 << 20
+    outs = {}
+    for force in (False, True):
+        st = GroupTopKState(None, r=4, compress_ratio=0.2, start_compress_iter=0, use_error_feedback=ef, seed=21)
+        st.force_exchange = force
+        st.defer_decode = True
+        res = []
+        for it in range(3 if ef == "ef21" else 2):  # (EF21: a dense init backward first)
+            futs = [group_topk_hook(st, SyntheticBucket(_randn(n, 50 + 10 * it + b).to(DEV), shapes, index=b,
+                                                        is_last=(b == 1))) for b in range(2)]
+            res.append([f.wait().cpu() for f in futs])
+        torch.cuda.synchronize()
+        outs[force] = (res, {b: e.cpu() for b, e in st.error_dict.items()},
+                       {b: e.cpu() for b, e in st.global_error_dict.items()})
+    step, fx = outs[False], outs[True]
+    for it, (a, c) in enumerate(zip(step[0], fx[0])):
+        for b in range(2):
+            assert_bitwise(c[b], a[b], f"backward {it} bucket {b} output")
+    for b in step[1]:
+        assert_bitwise(fx[1][b], step[1][b], f"bucket {b} E")
+    for b in step[2]:
+        assert_bitwise(fx[2][b], step[2][b], f"bucket {b} gE")
+
+
 @pytest.mark.parametrize("force_exchange,select_streams,trail", [(False, "auto", True), (True, "auto", True),
                                                                  (False, "off", True), (True, "off", True),
                                                                  (False, "auto", False), (False, "on", True)])
